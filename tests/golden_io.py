@@ -1,0 +1,36 @@
+"""Load the committed golden fixtures (arrays only, no pickle)."""
+import glob
+import json
+import os
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def names(prefix=""):
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as f:
+        meta = json.loads(str(f["meta"]))
+        arrays = {k: torch.from_numpy(f[k].copy()) for k in f.files if k != "meta"}
+    sd = {k[3:]: v for k, v in arrays.items() if k.startswith("sd.")}
+    data = {k: v for k, v in arrays.items() if not k.startswith("sd.")}
+    return meta, data, sd
+
+
+def layer_spec(meta, prefix=""):
+    kw = dict(meta["kwargs"])
+    spec = dict(type=meta["type"], prefix=prefix, **kw)
+    if meta["type"] == "Planar":
+        spec["nonlinearity"] = meta.get("nonlinearity", "tanh")
+    if meta["type"] in ("NSF_CL", "NSF_AR"):
+        spec.setdefault("K", 32)
+        spec.setdefault("B", 3)
+    if meta["type"] == "NSF_CL":
+        spec.setdefault("dim", 3)
+        spec.setdefault("mask", [1])
+    return spec

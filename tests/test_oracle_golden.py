@@ -1,0 +1,86 @@
+"""Pin the CPU oracle to the reference: oracle(inputs, weights) == golden outputs.
+
+The golden outputs were produced by the reference code itself
+(tests/golden/make_golden.py).  The oracle runs the same torch CPU fp32 ops in
+the same order, so agreement is expected to the last few ulps.
+"""
+import pytest
+import torch
+
+import golden_io as gio
+from oracle import nf_oracle as orc
+
+RT, AT = 2e-6, 2e-6  # oracle vs reference: same torch CPU ops, ulp-level slack
+
+
+def _close(a, b, rtol=RT, atol=AT):
+    torch.testing.assert_close(a, b, rtol=rtol, atol=atol, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", gio.names("rqs_"))
+def test_rqs_fixture(name):
+    meta, d, _ = gio.load(name)
+    tb = meta["tail_bound"]
+    y, lad = orc.unconstrained_rq_spline(d["x"], d["uw"], d["uh"], d["ud"], tail_bound=tb)
+    _close(y, d["y"]); _close(lad, d["lad"])
+    yi, ladi = orc.unconstrained_rq_spline(d["y"], d["uw"], d["uh"], d["ud"], inverse=True,
+                                           tail_bound=tb)
+    _close(yi, d["inv_y"], atol=1e-5); _close(ladi, d["inv_lad"], atol=1e-5)
+    y64, lad64 = orc.unconstrained_rq_spline(d["x"].double(), d["uw"].double(), d["uh"].double(),
+                                             d["ud"].double(), tail_bound=tb)
+    _close(y64, d["y_f64"], rtol=1e-12, atol=1e-12); _close(lad64, d["lad_f64"], rtol=1e-12, atol=1e-12)
+
+
+LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar")]
+
+
+@pytest.mark.parametrize("name", LAYERS)
+def test_layer_fixture(name):
+    meta, d, sd = gio.load(name)
+    spec = gio.layer_spec(meta)
+    z, ld = orc.apply_layer(spec, d["x"], sd)
+    _close(z, d["z"]); _close(ld.expand_as(d["ld"]), d["ld"])
+    if "rt_x" in d:
+        xi, ldi = orc.apply_layer(spec, d["z"], sd, inverse=True)
+        _close(xi, d["rt_x"], atol=1e-5); _close(ldi, d["rt_ld"], atol=1e-5)
+        xa, lda = orc.apply_layer(spec, d["x"], sd, inverse=True)
+        _close(xa, d["inv_x"], atol=1e-5); _close(lda, d["inv_ld"], atol=1e-5)
+    if "z_f64" in d:
+        sd64 = {k: v.double() for k, v in sd.items()}
+        z64, ld64 = orc.apply_layer(spec, d["x"].double(), sd64)
+        _close(z64, d["z_f64"], rtol=1e-12, atol=1e-12)
+        # the reference accumulates NSF_CL's log_det in an fp32 zeros() buffer (flows.py:228)
+        _close(ld64.to(d["ld_f64"].dtype).expand_as(d["ld_f64"]), d["ld_f64"], rtol=1e-6, atol=1e-5)
+
+
+def _model_specs(meta):
+    return [dict(gio.layer_spec(dict(type=l["type"], kwargs=l["kwargs"])), prefix="flows.%d." % i)
+            for i, l in enumerate(meta["layers"])]
+
+
+@pytest.mark.parametrize("name", gio.names("model_"))
+def test_model_fixture(name):
+    meta, d, sd = gio.load(name)
+    specs = _model_specs(meta)
+    z, plp, ld = orc.model_forward(specs, sd, d["x"], meta["var"])
+    _close(z, d["z"]); _close(plp, d["prior_lp"]); _close(ld, d["ld"], atol=1e-5)
+    _close(plp + ld, d["log_prob"], atol=1e-5)
+    if "rt_x" in d:
+        xi, ldi = orc.model_inverse(specs, sd, d["z"])
+        _close(xi, d["rt_x"], atol=1e-5); _close(ldi, d["rt_ld"], atol=1e-5)
+        xs, lps, zs = orc.model_sample_from(specs, sd, d["sample_z"], meta["var"])
+        _close(xs, d["sample_x"], atol=1e-5); _close(lps, d["sample_log_px"], atol=1e-4)
+
+
+def test_no_inside_raises():
+    x = torch.full((4,), 10.0)
+    w = torch.zeros(4, 8)
+    with pytest.raises(RuntimeError):
+        orc.unconstrained_rq_spline(x, w, w, torch.zeros(4, 7), tail_bound=3.0)
+
+
+def test_bin_width_check():
+    x = torch.zeros(4)
+    w = torch.zeros(4, 2000)
+    with pytest.raises(ValueError):
+        orc.unconstrained_rq_spline(x, w, w, torch.zeros(4, 1999), tail_bound=3.0)
