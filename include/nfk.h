@@ -1,0 +1,169 @@
+/*
+ * nfk.h -- C ABI of libnfk.so, the MI355X (gfx950) kernels of the
+ * normalizing-flow coupling-layer hot path.
+ *
+ * The reference (sherryli59/NormalizingFlow) is pure PyTorch and has no FFI:
+ * each entry point below replaces a chain of ATen ops behind one of its Python
+ * functions (file:line cited per function).  The Python host layer
+ * (normalizingflow_amd/, re-exported as nf/) binds these with ctypes; see
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *   - every pointer is device memory owned by the caller (the library never
+ *     allocates or frees); fp32 unless the type says otherwise;
+ *   - "ld*" arguments are row strides in ELEMENTS;
+ *   - logdet_mode: 0 = do not touch logdet, 1 = logdet[b] = v, 2 = logdet[b] += v;
+ *   - work is enqueued on `stream` (a hipStream_t); no call synchronises;
+ *   - return value: 0 on success, a hipError_t (>0) from the launch, or
+ *     NFK_EINVAL (<0) for bad arguments (nfk_last_error() says which).
+ *   - data-dependent errors of the reference are recorded, not raised, as bits
+ *     in *status (nullable) so the hot path never syncs; the host checks them
+ *     lazily (see NFK_ST_*).
+ */
+#ifndef NFK_H_
+#define NFK_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* nfk_stream_t; /* hipStream_t */
+
+#define NFK_ABI_VERSION 1
+#define NFK_EINVAL (-1)
+
+/* status bits, OR-ed into *status by the kernels */
+#define NFK_ST_INSIDE_SEEN 1 /* >=1 element inside [-B, B]; absent => the reference's
+                                RuntimeError from torch.min of an empty tensor (utils.py:63) */
+#define NFK_ST_NEG_DISC 2    /* negative discriminant in an inverse spline: the
+                                reference's AssertionError (utils.py:121) */
+
+int nfk_abi_version(void);
+const char* nfk_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Rational-quadratic spline coupling.
+ * Replaces NSF_CL.forward / NSF_CL.inverse minus the conditioner
+ * (nf/flows.py:227-239, 241-253), unconstrained_RQS (nf/utils.py:27-56),
+ * RQS (nf/utils.py:58-152) and searchsorted (nf/utils.py:20-25).
+ *
+ *   params     dense [batch, n_up, 3K-1]: per transformed element the
+ *              (W[K], H[K], D[K-1]) block, i.e. psi(lower) reshaped as at
+ *              flows.py:231, or cat(W, H, D) for the bare unconstrained_RQS.
+ *   param_mode 0: raw NSF_CL conditioner output: W,H <- (right-left)*softmax,
+ *                 D <- softplus (flows.py:233-235, where right-left = 2B)
+ *                 before the spline's own normalisation;
+ *              1: already the unconstrained_RQS arguments (utils.py:27);
+ *              2: the bare RQS arguments (utils.py:58): params [batch, n_up, 3K+1]
+ *                 with all K+1 derivative logits (no boundary constant).
+ *   bounds     knots span [left, right] x [bottom, top] (utils.py:58-60)
+ *   tails      1: identity outside [left, right] (unconstrained_RQS, which
+ *                 passes left=bottom=-B, right=top=B); 0: every element is
+ *                 splined (RQS; the caller checks the domain like utils.py:63)
+ *   up_in[j]   column of x holding transformed element j; up_out[j] its column in z
+ *   lo_in/lo_out: identity-copied ("lower") columns; n_lo may be 0.
+ *   x and z must not alias.
+ *   lad_out    nullable per-element log|det| [batch, n_up] with row stride ld_lad
+ *   logdet     per-sample sum over j of log|det| (flows.py:238), per logdet_mode
+ * ------------------------------------------------------------------------- */
+int nfk_rqs_coupling(const float* x, int64_t ldx, const float* params,
+                     const int32_t* up_in, const int32_t* up_out, int32_t n_up,
+                     const int32_t* lo_in, const int32_t* lo_out, int32_t n_lo,
+                     float* z, int64_t ldz, float* logdet, int32_t logdet_mode,
+                     float* lad_out, int64_t ld_lad, int64_t batch, int32_t K,
+                     double left, double right, double bottom, double top, int32_t tails,
+                     double min_bin_width, double min_bin_height, double min_derivative,
+                     int32_t param_mode, int32_t inverse, int32_t* status,
+                     nfk_stream_t stream);
+
+/* searchsorted (nf/utils.py:20-25), including its side effect:
+ *   bin_locations[r, n_loc-1] += eps  (in place, fp32), then
+ *   idx[r] = #{j : inputs[r] >= bin_locations[r, j]} - 1
+ * bin_locations: dense [rows, n_loc]; inputs, idx: [rows]. */
+int nfk_searchsorted(float* bin_locations, const float* inputs, int64_t* idx, int64_t rows,
+                     int32_t n_loc, double eps, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Affine half-coupling of RealNVP (nf/flows.py:52-76):
+ *   forward: out = t + in * exp(s),       logdet (+)= sum_j s
+ *   inverse: out = (in - t) * exp(-s),    logdet (+)= sum_j (-s)
+ * in/out may alias.  s and t share the row stride ld_st.
+ * ------------------------------------------------------------------------- */
+int nfk_affine_coupling(const float* x_in, int64_t ld_in, const float* s, const float* t,
+                        int64_t ld_st, float* x_out, int64_t ld_out, float* logdet,
+                        int32_t logdet_mode, int64_t batch, int32_t n, int32_t inverse,
+                        nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Planar flow forward (nf/flows_1.py:42-60), parameters w,u [dim], b [1].
+ * nonlinearity: 0 tanh (u re-parameterised to u_hat), 1 leaky_relu, 2 elu
+ * (u used as is; derivative exactly as flows_1.py:12-18, incl. its -0.01).
+ * log|det| = log(|1 + phi.u_hat| + 1e-4).
+ * ------------------------------------------------------------------------- */
+int nfk_planar(const float* x, int64_t ldx, const float* w, const float* u, const float* b,
+               float* z, int64_t ldz, float* logdet, int32_t logdet_mode, float* ld_out,
+               int64_t batch, int32_t dim, int32_t nonlinearity, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Radial flow (nf/flows_1.py:85-97).  Its r = ||x - x0||_F is a BATCH-GLOBAL
+ * norm, so the flow is two calls with an optional cross-rank all-reduce of
+ * *sumsq in between:
+ *   nfk_radial_sumsq: *sumsq = sum_{b,i} (x[b,i]-x0[i])^2 (fp64, deterministic;
+ *                     workspace >= nfk_radial_workspace_elems() doubles)
+ *   nfk_radial_apply: z = x + beta_hat*h*(x-x0); ld_scalar[0] = log|det|
+ *                     (identical for every sample, shape [1] as in the reference)
+ * ------------------------------------------------------------------------- */
+int64_t nfk_radial_workspace_elems(void);
+int nfk_radial_sumsq(const float* x, int64_t ldx, const float* x0, int64_t batch, int32_t dim,
+                     double* workspace, double* sumsq, nfk_stream_t stream);
+int nfk_radial_apply(const float* x, int64_t ldx, const float* x0, const float* log_alpha,
+                     const float* beta, const double* sumsq, float* z, int64_t ldz,
+                     float* ld_scalar, float* logdet, int32_t logdet_mode, int64_t batch,
+                     int32_t dim, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Isotropic normal prior log-density epilogue: the reference's "Normal" prior
+ * MultivariateNormal(0, var*I).log_prob (applications/src/setup.py:25-30)
+ * combined with the flow log-det as in nf/models.py:34 and :39:
+ *   out[b] = -0.5*(D*log(2pi) + sum_i (z_i/scale)^2) - half_log_det
+ *            + sign * logdet[b]          (logdet nullable; sign = +1 or -1)
+ * scale = the prior's Cholesky diagonal sqrt(var) (its scale_tril), and
+ * half_log_det = sum_i log(scale) are passed in as torch evaluates them.
+ * ------------------------------------------------------------------------- */
+int nfk_normal_logprob(const float* z, int64_t ldz, const float* logdet, float* out,
+                       int64_t batch, int32_t dim, float scale, float half_log_det,
+                       int32_t sign, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * NSF_AR conditioner features (nf/flows.py:172-173, 183):
+ *   feat[b, j] = cos(pi*x[b,j]/B), feat[b, n+j] = sin(pi*x[b,j]/B), j < n
+ * ------------------------------------------------------------------------- */
+int nfk_trig_features(const float* x, int64_t ldx, float* feat, int64_t ldf, int64_t batch,
+                      int32_t n, double B, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused NSF coupling layer: conditioner MLP (FCNN, flows.py:20-35) on fp32
+ * MFMA (v_mfma_f32_16x16x4_f32) + spline epilogue, one launch per layer; the
+ * [batch, n_up, 3K-1] conditioner output never touches HBM.
+ *   wpack: weights re-packed by nfk_fused_nsf_pack() into MFMA fragment order
+ *   (a device buffer of nfk_fused_nsf_pack_elems() floats).
+ * Supported shapes: nfk_fused_nsf_supported() != 0.
+ * ------------------------------------------------------------------------- */
+int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K);
+int64_t nfk_fused_nsf_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K);
+int nfk_fused_nsf_pack(const float* w0, const float* b0, const float* w2, const float* b2,
+                       const float* w4, const float* b4, int32_t n_lo, int32_t n_up,
+                       int32_t hidden, int32_t K, float* wpack, nfk_stream_t stream);
+int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
+                  const int32_t* up_out, int32_t n_up, const int32_t* lo_in,
+                  const int32_t* lo_out, int32_t n_lo, int32_t hidden, float* z, int64_t ldz,
+                  float* logdet, int32_t logdet_mode, int64_t batch, int32_t K,
+                  double tail_bound, int32_t inverse, int32_t* status, nfk_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NFK_H_ */

@@ -1,0 +1,3 @@
+"""``nf.flows_1`` of the reference: Planar / Radial (and the shared layers)."""
+from normalizingflow_amd.flows import FCNN, NSF_CL, Planar, Radial, RealNVP  # noqa: F401
+from normalizingflow_amd.flows import functional_derivatives  # noqa: F401

@@ -1,0 +1,100 @@
+"""ctypes binding of libnfk.so (include/nfk.h).
+
+The product path has no CPU or eager-PyTorch fallback: if the HIP library is
+missing or was built for a different ABI, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NFK_LIBRARY", os.path.join(_HERE, "libnfk.so"))
+ABI_VERSION = 1
+
+NFK_EINVAL = -1
+ST_INSIDE_SEEN = 1
+ST_NEG_DISC = 2
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+F64 = ctypes.c_double
+F32 = ctypes.c_float
+
+# name -> (restype, argtypes); mirrors include/nfk.h one-to-one
+SIGNATURES = {
+    "nfk_abi_version": (ctypes.c_int, []),
+    "nfk_last_error": (ctypes.c_char_p, []),
+    "nfk_rqs_coupling": (ctypes.c_int, [
+        P, I64, P,                      # x, ldx, params
+        P, P, I32,                      # up_in, up_out, n_up
+        P, P, I32,                      # lo_in, lo_out, n_lo
+        P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
+        P, I64, I64, I32,               # lad_out, ld_lad, batch, K
+        F64, F64, F64, F64, I32,        # left, right, bottom, top, tails
+        F64, F64, F64,                  # min_bin_width, min_bin_height, min_derivative
+        I32, I32, P, P]),               # param_mode, inverse, status, stream
+    "nfk_searchsorted": (ctypes.c_int, [P, P, P, I64, I32, F64, P]),
+    "nfk_affine_coupling": (ctypes.c_int, [P, I64, P, P, I64, P, I64, P, I32, I64, I32, I32, P]),
+    "nfk_planar": (ctypes.c_int, [P, I64, P, P, P, P, I64, P, I32, P, I64, I32, I32, P]),
+    "nfk_radial_workspace_elems": (ctypes.c_int64, []),
+    "nfk_radial_sumsq": (ctypes.c_int, [P, I64, P, I64, I32, P, P, P]),
+    "nfk_radial_apply": (ctypes.c_int, [P, I64, P, P, P, P, P, I64, P, P, I32, I64, I32, P]),
+    "nfk_normal_logprob": (ctypes.c_int, [P, I64, P, P, I64, I32, F32, F32, I32, P]),
+    "nfk_trig_features": (ctypes.c_int, [P, I64, P, I64, I64, I32, F64, P]),
+    "nfk_fused_nsf_supported": (ctypes.c_int, [I32, I32, I32, I32]),
+    "nfk_fused_nsf_pack_elems": (ctypes.c_int64, [I32, I32, I32, I32]),
+    "nfk_fused_nsf_pack": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P, P]),
+    "nfk_fused_nsf": (ctypes.c_int, [
+        P, I64, P,                      # x, ldx, wpack
+        P, P, I32,                      # up_in, up_out, n_up
+        P, P, I32, I32,                 # lo_in, lo_out, n_lo, hidden
+        P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
+        I64, I32, F64, I32, P, P]),     # batch, K, tail_bound, inverse, status, stream
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NfkError(RuntimeError):
+    """A libnfk.so entry point returned an error code."""
+
+
+def load():
+    """Load (once) and return the library; raise if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                "normalizingflow_amd: HIP kernel library not found at %s -- build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C "
+                "normalizingflow_amd/csrc`); there is no CPU fallback." % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        ver = lib.nfk_abi_version()
+        if ver != ABI_VERSION:
+            raise ImportError("libnfk.so ABI %d != expected %d; rebuild" % (ver, ABI_VERSION))
+        _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    """Invoke an entry point and turn a non-zero return into an exception."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        msg = load().nfk_last_error()
+        msg = msg.decode() if msg else ""
+        if rc == NFK_EINVAL:
+            raise ValueError("%s: %s" % (name, msg))
+        raise NfkError("%s failed (hipError %d): %s" % (name, rc, msg))
+    return rc

@@ -1,0 +1,13 @@
+"""Runtime switches of the host layer (plain module globals).
+
+STRICT_CHECKS  raise the reference's data-dependent errors (RuntimeError when a
+               spline layer has no element inside [-B, B], AssertionError on a
+               negative discriminant) after each top-level call.  Costs one
+               device->host read of the status words per call; the kernels
+               themselves never sync.
+USE_FUSED      run NSF_CL layers whose conditioner is the stock FCNN through the
+               fused MFMA kernel (nfk_fused_nsf) when the shape is supported;
+               otherwise conditioner GEMMs + the streaming spline kernel.
+"""
+STRICT_CHECKS = True
+USE_FUSED = True

@@ -1,0 +1,196 @@
+// nfk_spline.h -- per-element rational-quadratic spline math for gfx950.
+//
+// One lane evaluates one (sample, coordinate) element entirely in registers:
+// no host syncs, no compaction.  The fp32 operation order follows the
+// reference (nf/utils.py:58-152, nf/flows.py:233-235) so results track the
+// PyTorch-CPU path to ulp level:
+//   * softmax = exp(u - max) / sequential sum, applied as * (1/sum);
+//   * cumsum of the floored bin fractions accumulated in double and rounded
+//     per prefix (what ATen's CPU cumsum does for fp32);
+//   * separate roundings everywhere (files are built with -ffp-contract=off).
+// Host-side constants (NfkSplineConst) are evaluated in double exactly as the
+// Python scalars of the reference are, then rounded to fp32 once.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct NfkSplineConst {
+    float scale2b;   // (float)(right-left) = (float)(2*B): NSF_CL's W,H <- 2B*softmax (flows.py:234)
+    float lo, hi;    // (float)left, (float)right: knot range in x and the tails' inside test
+    float span;      // (float)(right - left)
+    float ylo, yhi;  // (float)bottom, (float)top
+    float yspan;     // (float)(top - bottom)
+    int tails;       // 1: identity outside [left, right] (unconstrained_RQS)
+    float min_w, fw; // (float)min_bin_width, (float)(1 - min_bin_width*K)
+    float min_h, fh; // same for heights
+    float min_d;     // (float)min_derivative
+    float dpad;      // (float)log(exp(1 - min_derivative) - 1) (utils.py:37)
+    float knot_eps;  // 1e-6f (utils.py:20)
+};
+
+__device__ __forceinline__ float nfk_softplus(float v) {
+    // torch.nn.functional.softplus(beta=1, threshold=20)
+    return v > 20.0f ? v : log1pf(expf(v));
+}
+
+// softmax over K logits, in place (K compile-time so the arrays stay in VGPRs)
+template <int K>
+__device__ __forceinline__ void nfk_softmax(float (&u)[K]) {
+    float m = u[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) m = fmaxf(m, u[i]);
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        u[i] = expf(u[i] - m);
+        s = s + u[i];
+    }
+    const float r = 1.0f / s;
+#pragma unroll
+    for (int i = 0; i < K; ++i) u[i] = u[i] * r;
+}
+
+// Knot positions from unnormalised logits (utils.py:73-80 / 84-91):
+// edge[0..K]; edge[0] = lo, edge[K] = hi pinned.
+template <int K>
+__device__ __forceinline__ void nfk_knots(float (&u)[K], float lo, float hi, float span,
+                                          float min_b, float fb, float (&edge)[K + 1]) {
+    nfk_softmax<K>(u);
+    double acc = 0.0;
+    edge[0] = lo;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const float p = min_b + fb * u[i];
+        acc += (double)p;
+        edge[i + 1] = span * (float)acc + lo;
+    }
+    edge[K] = hi;
+}
+
+// Bin index: #{j : v >= edge'[j]} - 1 with edge'[K] = edge[K] + eps (utils.py:20-25),
+// clamped to [0, K-1].  Returns the selected (edge_k, size_k).
+template <int K>
+__device__ __forceinline__ int nfk_bin(const float (&edge)[K + 1], float v, float eps) {
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) c += (v >= edge[j]) ? 1 : 0;
+    c += (v >= edge[K] + eps) ? 1 : 0;
+    int k = c - 1;
+    k = k < 0 ? 0 : k;
+    k = k > K - 1 ? K - 1 : k;
+    return k;
+}
+
+template <int K>
+__device__ __forceinline__ float nfk_sel(const float (&a)[K], int k) {
+    // register-resident select (no dynamic indexing -> no scratch)
+    float r = a[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) r = (k == j) ? a[j] : r;
+    return r;
+}
+
+// number of derivative logits per element: K-1 interior ones (the two
+// boundary ones are the constant dpad, utils.py:36-39), or all K+1 (DFULL,
+// the bare RQS of utils.py:58)
+template <int K, bool DFULL>
+struct NfkDN {
+    static constexpr int n = DFULL ? K + 1 : (K - 1 > 0 ? K - 1 : 1);
+};
+
+// Evaluate one spline element.  wr/hr: K logits each, dr: derivative logits
+// (before NSF_CL pre-normalisation when PRE == true).
+// out/lad: transformed value and log|det| (identity, 0 outside [-B, B]).
+template <int K, bool INV, bool PRE, bool DFULL>
+__device__ __forceinline__ void nfk_rqs_element(float x, float (&wr)[K], float (&hr)[K],
+                                                const float (&dr)[NfkDN<K, DFULL>::n],
+                                                const NfkSplineConst& c, float& out, float& lad,
+                                                bool& inside, bool& neg_disc) {
+    inside = !c.tails || ((x >= c.lo) && (x <= c.hi));
+    neg_disc = false;
+    if (!inside) {
+        out = x;
+        lad = 0.0f;
+        return;
+    }
+    if (PRE) {
+        nfk_softmax<K>(wr);
+        nfk_softmax<K>(hr);
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            wr[i] = c.scale2b * wr[i];
+            hr[i] = c.scale2b * hr[i];
+        }
+    }
+    float cw[K + 1], ch[K + 1];
+    nfk_knots<K>(wr, c.lo, c.hi, c.span, c.min_w, c.fw, cw);
+    nfk_knots<K>(hr, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, ch);
+
+    const int k = nfk_bin<K>(INV ? ch : cw, x, c.knot_eps);
+    // gather (utils.py:98-109) without dynamic register indexing
+    float cw_k = cw[0], w_k = cw[1] - cw[0], ch_k = ch[0], h_k = ch[1] - ch[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+        if (k == j) {
+            cw_k = cw[j];
+            w_k = cw[j + 1] - cw[j];
+            ch_k = ch[j];
+            h_k = ch[j + 1] - ch[j];
+        }
+    }
+    // derivatives: padded logits [dpad, d_0..d_{K-2}, dpad] -> min_d + softplus(.)
+    // only the two that the bin uses are evaluated (utils.py:82, 105-107)
+    float raw_k = 0.0f, raw_k1 = 0.0f;
+    if (DFULL) {
+        raw_k = dr[0];
+        raw_k1 = dr[1];
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+            if (k == j) {
+                raw_k = dr[j];
+                raw_k1 = dr[j + 1];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < K - 1; ++j) {
+            if (k == j + 1) raw_k = dr[j];  // padded index j+1 holds logit j
+            if (k == j) raw_k1 = dr[j];
+        }
+        if (PRE) {  // NSF_CL's D <- softplus(D) (flows.py:235), only where it is used
+            raw_k = nfk_softplus(raw_k);
+            raw_k1 = nfk_softplus(raw_k1);
+        }
+        raw_k = (k == 0) ? c.dpad : raw_k;
+        raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
+    }
+    const float d_k = c.min_d + nfk_softplus(raw_k);
+    const float d_k1 = c.min_d + nfk_softplus(raw_k1);
+    const float delta = h_k / w_k;
+    const float gap = (d_k + d_k1) - 2.0f * delta;
+
+    float th;
+    if (INV) {
+        const float y = x - ch_k;
+        const float qa = y * gap + h_k * (delta - d_k);
+        const float qb = h_k * d_k - y * gap;
+        const float qc = (-delta) * y;
+        const float disc = qb * qb - (4.0f * qa) * qc;
+        neg_disc = !(disc >= 0.0f);
+        const float root = (2.0f * qc) / (-qb - sqrtf(disc));
+        out = root * w_k + cw_k;
+        th = root;
+    } else {
+        th = (x - cw_k) / w_k;
+    }
+    const float t1mt = th * (1.0f - th);
+    const float den = delta + gap * t1mt;
+    if (!INV) {
+        const float num = h_k * (delta * (th * th) + d_k * t1mt);
+        out = ch_k + num / den;
+    }
+    const float omt = 1.0f - th;
+    const float dnum = (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+    const float l = logf(dnum) - 2.0f * logf(den);
+    lad = INV ? -l : l;
+}

@@ -1,0 +1,75 @@
+"""Sample-sharded data parallelism over the GPUs of one node.
+
+Every layer in scope is independent per sample, so the
+batch is split by rows across ranks (one process per GPU, backend "nccl" =
+RCCL over xGMI) with replicated weights and no collective on the data path.
+The only exchanges are the ones the path really has:
+
+  * the NLL of training / evaluation (applications/src/train.py:22-25):
+    one all_reduce(SUM) of [sum log p, count] -- 16 bytes per step;
+  * Radial's batch-global norm (nf/flows_1.py:90): one all_reduce(SUM) of the
+    fp64 squared norm before its elementwise step (``attach_process_group``).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from .flows import Radial
+
+__all__ = ["shard_range", "shard", "nll_allreduce", "attach_process_group", "init_from_env"]
+
+
+def shard_range(n, rank, world):
+    """Rows [lo, hi) of an n-row batch owned by ``rank`` (contiguous, balanced)."""
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def shard(x, rank=None, world=None):
+    """This rank's contiguous row slice of a replicated batch."""
+    rank = dist.get_rank() if rank is None else rank
+    world = dist.get_world_size() if world is None else world
+    lo, hi = shard_range(x.shape[0], rank, world)
+    return x[lo:hi]
+
+
+def nll_allreduce(log_prob, group=None):
+    """Global mean negative log-likelihood, -mean(log p) over all ranks'
+    samples (train.py:23-25).  Reduces [sum, count] in fp64: 16 bytes."""
+    acc = torch.stack([log_prob.double().sum(),
+                       torch.tensor(float(log_prob.numel()), dtype=torch.float64,
+                                    device=log_prob.device)])
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=group)
+    return (-(acc[0] / acc[1])).to(log_prob.dtype)
+
+
+def attach_process_group(model, group=None):
+    """Make batch-global layers (Radial) reduce over ``group`` -- call once per
+    model when the batch is sharded; other layers need nothing."""
+    g = group if group is not None else dist.group.WORLD
+    for m in model.modules():
+        if isinstance(m, Radial):
+            m.process_group = g
+    return model
+
+
+def init_from_env(backend=None):
+    """torchrun-style init: RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* from env.
+    Returns (rank, world, local_rank); a no-op single process when WORLD_SIZE
+    is unset."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world, local

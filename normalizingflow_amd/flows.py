@@ -1,0 +1,431 @@
+"""Flow layers with the reference's class surface, backed by HIP kernels.
+
+Drop-in for ``nf.flows`` / ``nf.flows_1`` of sherryli59/NormalizingFlow: same
+class names, constructor arguments, attributes, ``forward``/``inverse``
+signatures, return shapes, parameter-initialisation order (so a given
+``torch.manual_seed`` yields the same weights) and ``state_dict`` keys.
+
+What runs where (ROCm device only -- CPU tensors raise, there is no fallback):
+  FCNN           stock nn.Linear/Tanh stack (library GEMMs) -- flows.py:20-35
+  NSF_CL         fused MFMA conditioner + spline kernel (nfk_fused_nsf) when the
+                 shape is supported, else FCNN + nfk_rqs_coupling -- flows.py:210-253
+  RealNVP        4 FCNN + nfk_affine_coupling per half -- flows.py:38-76
+  NSF_AR         per-dimension FCNN on nfk_trig_features + nfk_rqs_coupling
+                 -- flows.py:152-209
+  Planar         nfk_planar -- flows_1.py:21-63
+  Radial         nfk_radial_sumsq (+ optional all-reduce) + nfk_radial_apply
+                 -- flows_1.py:66-97
+Gradients do not flow through the kernels yet (backward kernels are the next
+row of the plan); calls under autograd warn once.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.nn.init as init
+
+from . import config
+from . import kernels as K_
+from ._lib import ST_INSIDE_SEEN, ST_NEG_DISC
+
+__all__ = ["FCNN", "RealNVP", "NSF_AR", "NSF_CL", "Planar", "Radial", "functional_derivatives"]
+
+# flows.py:12-18 -- kept for API parity (used by Planar's CPU reference semantics)
+functional_derivatives = {
+    torch.tanh: lambda x: 1 - torch.pow(torch.tanh(x), 2),
+    F.leaky_relu: lambda x: (x > 0).type(x.dtype) + (x < 0).type(x.dtype) * -0.01,
+    F.elu: lambda x: (x > 0).type(x.dtype) + (x < 0).type(x.dtype) * torch.exp(x),
+}
+
+_warned_grad = False
+
+
+def _grad_warning(module):
+    global _warned_grad
+    if _warned_grad or not torch.is_grad_enabled():
+        return
+    if any(p.requires_grad for p in module.parameters()):
+        _warned_grad = True
+        warnings.warn("normalizingflow_amd: outputs of the HIP flow kernels carry no autograd "
+                      "graph yet (backward kernels pending); use torch.no_grad() for inference",
+                      RuntimeWarning, stacklevel=3)
+
+
+def _check_input(x, what="x"):
+    if not torch.is_tensor(x) or x.dim() != 2:
+        raise ValueError("%s must be a 2-D tensor [batch, features]" % what)
+    if not x.is_cuda:
+        raise RuntimeError(
+            "normalizingflow_amd runs on the ROCm device only (got a %s tensor); move the model "
+            "and data to 'cuda' -- there is no CPU fallback" % x.device)
+    if x.dtype != torch.float32:
+        raise TypeError("normalizingflow_amd kernels compute in float32; got %s" % x.dtype)
+    return x
+
+
+def raise_on_status(status, n_slots=None):
+    """Reference-compatible errors from the kernels' status words (one sync)."""
+    if status is None:
+        return
+    st = status[:n_slots].cpu() if n_slots is not None else status.cpu()
+    if bool(((st & ST_NEG_DISC) != 0).any()):
+        raise AssertionError("negative discriminant in the inverse rational-quadratic spline "
+                             "(nf/utils.py:121)")
+    if bool(((st & ST_INSIDE_SEEN) == 0).any()):
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
+                           "(no element inside the spline interval [-B, B], nf/utils.py:63)")
+
+
+class _HipFlow(nn.Module):
+    """Base of the kernel-backed layers.
+
+    ``_run(x, inverse, logdet, mode, status)`` enqueues the layer and returns z;
+    ``logdet`` is written (mode 1) or accumulated (mode 2) in place, so a model
+    chains layers without temporaries or syncs.  ``_n_status`` status words
+    are needed per call (spline layers only).
+    """
+    _n_status = 0
+
+    def _run(self, x, inverse, logdet, mode, status):
+        raise NotImplementedError
+
+    def _call(self, x, inverse):
+        x = _check_input(x)
+        _grad_warning(self)
+        st = (torch.zeros(self._n_status, dtype=torch.int32, device=x.device)
+              if self._n_status else None)
+        logdet = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+        with torch.no_grad():
+            z = self._run(x, inverse, logdet, K_.MODE_WRITE, st)
+        if st is not None and config.STRICT_CHECKS:
+            raise_on_status(st)
+        return z, logdet
+
+
+class FCNN(nn.Module):
+    """Linear -> Tanh -> Linear -> Tanh -> Linear conditioner (flows.py:20-35)."""
+
+    def __init__(self, in_dim, out_dim, hidden_dim):
+        super().__init__()
+        self.network = nn.Sequential(
+            nn.Linear(in_dim, hidden_dim), nn.Tanh(),
+            nn.Linear(hidden_dim, hidden_dim), nn.Tanh(),
+            nn.Linear(hidden_dim, out_dim))
+
+    def forward(self, x):
+        return self.network(x)
+
+
+def _is_stock_fcnn(net):
+    if type(net) is not FCNN:
+        return False
+    n = net.network
+    return (len(n) == 5 and all(isinstance(n[i], nn.Linear) for i in (0, 2, 4))
+            and all(isinstance(n[i], nn.Tanh) for i in (1, 3)))
+
+
+class RealNVP(_HipFlow):
+    """Affine coupling, two halves per layer (flows.py:38-76).
+
+    forward:  up <- t1(lo) + up*exp(s1(lo));  lo <- t2(up) + lo*exp(s2(up))
+    inverse:  lo <- (lo - t2(up))*exp(-s2(up));  up <- (up - t1(lo))*exp(-s1(lo))
+    """
+
+    def __init__(self, dim, hidden_dim=800, base_network=FCNN):
+        super().__init__()
+        self.dim = dim
+        self.t1 = base_network(dim // 2, dim // 2, hidden_dim)
+        self.s1 = base_network(dim // 2, dim // 2, hidden_dim)
+        self.t2 = base_network(dim // 2, dim // 2, hidden_dim)
+        self.s2 = base_network(dim // 2, dim // 2, hidden_dim)
+
+    def _run(self, x, inverse, logdet, mode, status):
+        h = self.dim // 2
+        if x.shape[1] != self.dim or self.dim - h != h:
+            # the reference fails the same way (shape broadcast in flows.py:56)
+            raise RuntimeError("RealNVP needs an even feature dimension equal to dim=%d (got %d)"
+                               % (self.dim, x.shape[1]))
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        lo, up = x[:, :h], x[:, h:]
+        zlo, zup = z[:, :h], z[:, h:]
+        m2 = K_.MODE_ACC if mode != K_.MODE_NONE else K_.MODE_NONE
+        if not inverse:
+            s1, t1 = self.s1(lo), self.t1(lo)
+            K_.affine_coupling(up, s1, t1, zup, logdet=logdet, logdet_mode=mode)
+            s2, t2 = self.s2(zup), self.t2(zup)
+            K_.affine_coupling(lo, s2, t2, zlo, logdet=logdet, logdet_mode=m2)
+        else:
+            s2, t2 = self.s2(up), self.t2(up)
+            K_.affine_coupling(lo, s2, t2, zlo, logdet=logdet, logdet_mode=mode, inverse=True)
+            s1, t1 = self.s1(zlo), self.t1(zlo)
+            K_.affine_coupling(up, s1, t1, zup, logdet=logdet, logdet_mode=m2, inverse=True)
+        return z
+
+    def forward(self, x):
+        return self._call(x, False)
+
+    def inverse(self, z):
+        return self._call(z, True)
+
+
+class _SplineMaps:
+    """Device-resident int32 column maps of one coupling layer."""
+
+    def __init__(self, lo_in, lo_out, up_in, up_out, device):
+        mk = lambda v: torch.tensor(v, dtype=torch.int32, device=device)
+        self.lo_in, self.lo_out = mk(lo_in), mk(lo_out)
+        self.up_in, self.up_out = mk(up_in), mk(up_out)
+        self.lo_in_long = self.lo_in.long()
+
+
+class NSF_CL(_HipFlow):
+    """Neural-spline coupling layer (flows.py:210-253).
+
+    Per particle group of ``dim`` coordinates, ``mask`` selects the conditioning
+    ("lower") coordinates; the others are transformed by a rational-quadratic
+    spline whose (W, H, D) come from ``psi(lower)``.  The output places the
+    masked coordinates first in every group (flows.py:239), exactly as the
+    reference -- a non-prefix mask therefore permutes coordinates.
+    """
+    _n_status = 1
+
+    def __init__(self, size, dim=3, K=32, B=3, hidden_dim=800, base_network=FCNN, device="cpu",
+                 mask=[1]):
+        super().__init__()
+        self.size = size
+        self.dim = dim
+        self.K = K
+        self.B = B
+        self.device = device
+        self.mask = torch.Tensor(mask).long()
+        self.unmasked = torch.Tensor([x for x in range(self.dim) if x not in self.mask]).long()
+        self.psi = base_network(len(mask) * self.size,
+                                (3 * K - 1) * (self.dim - len(self.mask)) * self.size,
+                                hidden_dim).to(self.device)
+        self._maps_cache = {}
+        self._pack_cache = None
+
+    # column maps (x -> lower/upper, and where each lands in the output)
+    def _maps(self, device):
+        key = str(device)
+        m = self._maps_cache.get(key)
+        if m is None:
+            mk, um = [int(v) for v in self.mask], [int(v) for v in self.unmasked]
+            nm = len(mk)
+            lo_in = [p * self.dim + c for p in range(self.size) for c in mk]
+            up_in = [p * self.dim + c for p in range(self.size) for c in um]
+            lo_out = [p * self.dim + i for p in range(self.size) for i in range(nm)]
+            up_out = [p * self.dim + nm + i for p in range(self.size) for i in range(len(um))]
+            m = self._maps_cache[key] = _SplineMaps(lo_in, lo_out, up_in, up_out, device)
+        return m
+
+    def _fused_pack(self, device):
+        """Weights re-packed for the fused kernel; rebuilt when any weight changes."""
+        if not config.USE_FUSED or not _is_stock_fcnn(self.psi):
+            return None
+        lins = [self.psi.network[i] for i in (0, 2, 4)]
+        n_lo, n_up = len(self.mask) * self.size, len(self.unmasked) * self.size
+        hidden = lins[0].out_features
+        if not K_.fused_nsf_supported(n_lo, n_up, hidden, self.K):
+            return None
+        params = [t for l in lins for t in (l.weight, l.bias)]
+        if any(p.device != device or p.dtype != torch.float32 for p in params):
+            return None
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._pack_cache is not None and self._pack_cache[0] == key:
+            return self._pack_cache[1]
+        pack = K_.fused_nsf_pack(*params, n_lo, n_up, hidden, self.K)
+        self._pack_cache = (key, pack, hidden)
+        return pack
+
+    def _run(self, x, inverse, logdet, mode, status):
+        if x.shape[1] != self.size * self.dim:
+            raise RuntimeError("NSF_CL(size=%d, dim=%d) got %d features"
+                               % (self.size, self.dim, x.shape[1]))
+        maps = self._maps(x.device)
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        pack = self._fused_pack(x.device)
+        if pack is not None:
+            K_.fused_nsf(x, pack, maps.up_in, maps.up_out, maps.lo_in, maps.lo_out,
+                         self._pack_cache[2], z, logdet=logdet, logdet_mode=mode, K=self.K,
+                         tail_bound=self.B, inverse=inverse, status=status)
+            return z
+        lower = x.index_select(1, maps.lo_in_long)
+        params = self.psi(lower).contiguous()
+        b = float(self.B)
+        K_.rqs_coupling(x, params, maps.up_in, maps.up_out, z, lo_in=maps.lo_in,
+                        lo_out=maps.lo_out, logdet=logdet, logdet_mode=mode, K=self.K,
+                        left=-b, right=b, bottom=-b, top=b, tails=True, param_mode=0,
+                        inverse=inverse, status=status)
+        return z
+
+    def forward(self, x):
+        return self._call(x, False)
+
+    def inverse(self, z):
+        return self._call(z, True)
+
+
+class NSF_AR(_HipFlow):
+    """Autoregressive neural-spline flow (flows.py:152-209).
+
+    Coordinate i is splined with (W, H, D) = layers[i-1](cos/sin(pi*v[:, :i]/B))
+    (``init_param`` for i = 0), where v is the input in ``forward`` and the
+    already-inverted output in ``inverse`` (flows.py:201).
+    """
+
+    def __init__(self, dim, K=32, B=3, hidden_dim=800, base_network=FCNN, device="cpu"):
+        super().__init__()
+        self.dim = dim
+        self.K = K
+        self.B = B
+        self.device = device
+        self.layers = nn.ModuleList()
+        # registered as a Parameter on every device (the reference's `.to(device)`
+        # drops the registration for non-CPU devices, flows.py:164)
+        self.init_param = nn.Parameter(torch.Tensor(3 * K - 1))
+        for i in range(1, dim):
+            self.layers += [base_network(2 * i, 3 * K - 1, hidden_dim).to(self.device)]
+        self.reset_parameters()
+        self._cols = {}
+
+    @property
+    def _n_status(self):
+        return self.dim
+
+    def reset_parameters(self):
+        init.uniform_(self.init_param, -1 / 2, 1 / 2)
+
+    def trig_transform(self, x):
+        feat = torch.empty(x.shape[0], 2 * x.shape[1], dtype=torch.float32, device=x.device)
+        K_.trig_features(x, feat, self.B)
+        return feat
+
+    def _col(self, i, device):
+        key = (i, str(device))
+        c = self._cols.get(key)
+        if c is None:
+            c = self._cols[key] = torch.tensor([i], dtype=torch.int32, device=device)
+        return c
+
+    def _run(self, x, inverse, logdet, mode, status):
+        if x.shape[1] != self.dim:
+            raise RuntimeError("NSF_AR(dim=%d) got %d features" % (self.dim, x.shape[1]))
+        n = x.shape[0]
+        z = torch.zeros_like(x, memory_format=torch.contiguous_format)
+        cond = z if inverse else x
+        b = float(self.B)
+        for i in range(self.dim):
+            if i == 0:
+                params = self.init_param.detach().to(torch.float32).expand(n, -1).contiguous()
+            else:
+                params = self.layers[i - 1](self.trig_transform(cond[:, :i])).contiguous()
+            m = mode if (i == 0 or mode == K_.MODE_NONE) else K_.MODE_ACC
+            col = self._col(i, x.device)
+            K_.rqs_coupling(x, params, col, col, z, logdet=logdet, logdet_mode=m, K=self.K,
+                            left=-b, right=b, bottom=-b, top=b, tails=True, param_mode=0,
+                            inverse=inverse,
+                            status=None if status is None else status[i:i + 1])
+        return z
+
+    def forward(self, x):
+        return self._call(x, False)
+
+    def inverse(self, z):
+        return self._call(z, True)
+
+
+_NL_CODE = {torch.tanh: 0, F.leaky_relu: 1, F.elu: 2}
+
+
+class Planar(_HipFlow):
+    """Planar flow z = x + u_hat h(w.x + b) (flows_1.py:21-63)."""
+
+    def __init__(self, dim, nonlinearity=torch.tanh):
+        super().__init__()
+        self.h = nonlinearity
+        self.w = nn.Parameter(torch.Tensor(dim))
+        self.u = nn.Parameter(torch.Tensor(dim))
+        self.b = nn.Parameter(torch.Tensor(1))
+        self.reset_parameters(dim)
+
+    def reset_parameters(self, dim):
+        init.uniform_(self.w, -math.sqrt(1 / dim), math.sqrt(1 / dim))
+        init.uniform_(self.u, -math.sqrt(1 / dim), math.sqrt(1 / dim))
+        init.uniform_(self.b, -math.sqrt(1 / dim), math.sqrt(1 / dim))
+
+    def _run(self, x, inverse, logdet, mode, status):
+        if inverse:
+            raise NotImplementedError("Planar flow has no algebraic inverse.")
+        if self.h not in _NL_CODE:
+            raise NotImplementedError("Non-linearity is not supported.")
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        K_.planar(x, self.w.detach(), self.u.detach(), self.b.detach(), z, logdet=logdet,
+                  logdet_mode=mode, nonlinearity=_NL_CODE[self.h])
+        return z
+
+    def forward(self, x):
+        return self._call(x, False)
+
+    def inverse(self, z):
+        raise NotImplementedError("Planar flow has no algebraic inverse.")
+
+
+class Radial(_HipFlow):
+    """Radial flow (flows_1.py:66-97).
+
+    r = ||x - x0|| is the Frobenius norm over the WHOLE batch (flows_1.py:90),
+    so outputs depend on the batch, and log_det has shape [1].  When the batch
+    is sharded over ranks, set ``process_group`` (normalizingflow_amd.dist)
+    and the squared norm is all-reduced so every shard sees the global r.
+    The reference never initialises the parameters (its reset_parameters is
+    broken); here they start at zero and ``reset_parameters(dim)`` works.
+    """
+
+    def __init__(self, dim):
+        super().__init__()
+        self.x0 = nn.Parameter(torch.zeros(dim))
+        self.log_alpha = nn.Parameter(torch.zeros(1))
+        self.beta = nn.Parameter(torch.zeros(1))
+        self.process_group = None
+        self._ws = {}
+
+    def reset_parameters(self, dim):
+        init.uniform_(self.x0, -math.sqrt(1 / dim), math.sqrt(1 / dim))
+        init.uniform_(self.log_alpha, -math.sqrt(1 / dim), math.sqrt(1 / dim))
+        init.uniform_(self.beta, -math.sqrt(1 / dim), math.sqrt(1 / dim))
+
+    def _buffers_for(self, device):
+        key = str(device)
+        if key not in self._ws:
+            self._ws[key] = (torch.empty(K_.radial_workspace_elems(), dtype=torch.float64,
+                                         device=device),
+                             torch.empty(1, dtype=torch.float64, device=device))
+        return self._ws[key]
+
+    def _run(self, x, inverse, logdet, mode, status, ld_scalar=None):
+        if inverse:
+            raise AttributeError("'Radial' object has no attribute 'inverse'")
+        ws, sumsq = self._buffers_for(x.device)
+        K_.radial_sumsq(x, self.x0.detach(), ws, sumsq)
+        if self.process_group is not None:
+            torch.distributed.all_reduce(sumsq, group=self.process_group)
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        if ld_scalar is None:
+            ld_scalar = torch.empty(1, dtype=torch.float32, device=x.device)
+        K_.radial_apply(x, self.x0.detach(), self.log_alpha.detach(), self.beta.detach(), sumsq,
+                        z, ld_scalar, logdet=logdet, logdet_mode=mode)
+        return z
+
+    def forward(self, x):
+        x = _check_input(x)
+        _grad_warning(self)
+        ld = torch.empty(1, dtype=torch.float32, device=x.device)
+        with torch.no_grad():
+            z = self._run(x, False, None, K_.MODE_NONE, None, ld_scalar=ld)
+        return z, ld

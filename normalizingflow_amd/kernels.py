@@ -1,0 +1,254 @@
+"""Validated Python wrappers over the libnfk.so entry points.
+
+Each wrapper checks device / dtype / layout on the host (no device sync),
+then enqueues the kernel on the tensor's current HIP stream.  They are the
+only place the package touches raw pointers.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+F32 = torch.float32
+
+MODE_NONE, MODE_WRITE, MODE_ACC = 0, 1, 2
+
+
+class KernelTimer:
+    """Optional per-entry-point timing with HIP events recorded on the stream
+    each kernel is enqueued on (torch's current stream).  Install with
+    ``kernels.TIMER = KernelTimer()``; read ``summary()`` after a sync."""
+
+    def __init__(self):
+        self.events = {}
+
+    def start(self, name, dev):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        return ev
+
+    def stop(self, name, dev, ev0):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        self.events.setdefault(name, []).append((ev0, ev))
+
+    def summary(self):
+        """name -> (launches, mean ms, total ms)"""
+        out = {}
+        for name, evs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            out[name] = (len(ms), sum(ms) / len(ms), sum(ms))
+        return out
+
+
+TIMER = None
+
+
+def _timed(name, dev, fn, *args):
+    if TIMER is None:
+        return _lib.call(fn, *args)
+    ev0 = TIMER.start(name, dev)
+    rc = _lib.call(fn, *args)
+    TIMER.stop(name, dev, ev0)
+    return rc
+
+
+def _require_hip(*ts):
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "normalizingflow_amd runs on the ROCm device only (tensor on %s); move the model "
+                "and inputs to 'cuda' -- there is no CPU fallback" % t.device)
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError("tensors on different devices: %s vs %s" % (dev, t.device))
+    return dev
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _mat(t, name):
+    """(ptr, row stride) of a 2-D fp32 tensor with unit column stride."""
+    if t.dtype != F32:
+        raise TypeError("%s must be float32, got %s" % (name, t.dtype))
+    if t.dim() != 2:
+        raise ValueError("%s must be 2-D, got shape %s" % (name, tuple(t.shape)))
+    if t.shape[1] > 1 and t.stride(1) != 1:
+        raise ValueError("%s needs unit column stride" % name)
+    return t.data_ptr(), (t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1))
+
+
+def _vec(t, n, name, dtype=F32):
+    if t is None:
+        return None
+    if t.dtype != dtype or t.numel() != n or (n > 1 and not t.is_contiguous()):
+        raise ValueError("%s must be a contiguous %s vector of %d elements" % (name, dtype, n))
+    return t.data_ptr()
+
+
+# ---------------------------------------------------------------------------
+def rqs_coupling(x, params, up_in, up_out, z, *, lo_in=None, lo_out=None, logdet=None,
+                 logdet_mode=MODE_NONE, lad_out=None, K, left, right, bottom, top, tails=True,
+                 min_bin_width=1e-3, min_bin_height=1e-3, min_derivative=1e-3, param_mode=0,
+                 inverse=False, status=None):
+    """Spline coupling (nfk_rqs_coupling).  params: dense [B, n_up*(3K-1)] (or 3-D)."""
+    dev = _require_hip(x, params, up_in, z, logdet, lad_out, status)
+    B = x.shape[0]
+    n_up = up_in.numel()
+    n_lo = 0 if lo_in is None else lo_in.numel()
+    per = 3 * K + 1 if param_mode == 2 else 3 * K - 1
+    if params.dtype != F32 or not params.is_contiguous() or params.numel() != B * n_up * per:
+        raise ValueError("params must be a dense float32 [B, n_up, %d] tensor "
+                         "(got %s, %s)" % (per, tuple(params.shape), params.dtype))
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    if z.shape[0] != B:
+        raise ValueError("z batch mismatch")
+    lp, ldl = (None, 0) if lad_out is None else _mat(lad_out, "lad_out")
+    for m in (up_in, up_out, lo_in, lo_out):
+        if m is not None and (m.dtype != torch.int32 or not m.is_contiguous()):
+            raise ValueError("index maps must be contiguous int32")
+    _timed("nfk_rqs_coupling", dev, "nfk_rqs_coupling", xp, ldx, params.data_ptr(), up_in.data_ptr(),
+              up_out.data_ptr(), n_up, _ptr(lo_in), _ptr(lo_out), n_lo, zp, ldz,
+              _vec(logdet, B, "logdet"), logdet_mode, lp, ldl, B, K, float(left), float(right),
+              float(bottom), float(top), 1 if tails else 0, float(min_bin_width),
+              float(min_bin_height), float(min_derivative), param_mode, 1 if inverse else 0,
+              _vec(status, 1, "status", torch.int32), _stream(dev))
+
+
+def searchsorted(bin_locations, inputs, eps=1e-6):
+    dev = _require_hip(bin_locations, inputs)
+    if bin_locations.dtype != F32 or not bin_locations.is_contiguous():
+        raise ValueError("bin_locations must be contiguous float32")
+    n = bin_locations.shape[-1]
+    rows = bin_locations.numel() // n
+    if inputs.numel() != rows:
+        raise ValueError("inputs must have one value per bin row")
+    v = inputs.contiguous().to(F32)
+    idx = torch.empty(inputs.shape, dtype=torch.int64, device=dev)
+    _lib.call("nfk_searchsorted", bin_locations.data_ptr(), v.data_ptr(), idx.data_ptr(), rows,
+              n, float(eps), _stream(dev))
+    return idx
+
+
+def affine_coupling(x_in, s, t, x_out, *, logdet=None, logdet_mode=MODE_NONE, inverse=False):
+    dev = _require_hip(x_in, s, t, x_out, logdet)
+    B, n = x_in.shape
+    if s.shape != (B, n) or t.shape != (B, n) or x_out.shape != (B, n):
+        raise ValueError("affine coupling shape mismatch: in %s s %s t %s out %s"
+                         % (tuple(x_in.shape), tuple(s.shape), tuple(t.shape), tuple(x_out.shape)))
+    xp, ldi = _mat(x_in, "x_in")
+    sp, lds = _mat(s, "s")
+    tp, ldt = _mat(t, "t")
+    if ldt != lds:
+        if B > 1:
+            t = t.contiguous() if t.stride(0) != lds else t
+            s = s.contiguous()
+            sp, lds = _mat(s, "s")
+            tp, ldt = _mat(t, "t")
+        ldt = lds
+    op, ldo = _mat(x_out, "x_out")
+    _timed("nfk_affine_coupling", dev, "nfk_affine_coupling", xp, ldi, sp, tp, lds, op, ldo, _vec(logdet, B, "logdet"),
+              logdet_mode, B, n, 1 if inverse else 0, _stream(dev))
+
+
+PLANAR_NL = {"tanh": 0, "leaky_relu": 1, "elu": 2}
+
+
+def planar(x, w, u, b, z, *, logdet=None, logdet_mode=MODE_NONE, ld_out=None, nonlinearity=0):
+    dev = _require_hip(x, w, u, b, z, logdet, ld_out)
+    B, D = x.shape
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    _lib.call("nfk_planar", xp, ldx, _vec(w, D, "w"), _vec(u, D, "u"), _vec(b, 1, "b"), zp, ldz,
+              _vec(logdet, B, "logdet"), logdet_mode, _vec(ld_out, B, "ld_out"), B, D,
+              nonlinearity, _stream(dev))
+
+
+def radial_workspace_elems():
+    return int(_lib.load().nfk_radial_workspace_elems())
+
+
+def radial_sumsq(x, x0, workspace, sumsq):
+    dev = _require_hip(x, x0, workspace, sumsq)
+    B, D = x.shape
+    xp, ldx = _mat(x, "x")
+    _lib.call("nfk_radial_sumsq", xp, ldx, _vec(x0, D, "x0"),
+              B, D, _vec(workspace, radial_workspace_elems(), "workspace", torch.float64),
+              _vec(sumsq, 1, "sumsq", torch.float64), _stream(dev))
+
+
+def radial_apply(x, x0, log_alpha, beta, sumsq, z, ld_scalar, *, logdet=None,
+                 logdet_mode=MODE_NONE):
+    dev = _require_hip(x, x0, log_alpha, beta, sumsq, z, ld_scalar, logdet)
+    B, D = x.shape
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    _lib.call("nfk_radial_apply", xp, ldx, _vec(x0, D, "x0"), _vec(log_alpha, 1, "log_alpha"),
+              _vec(beta, 1, "beta"), _vec(sumsq, 1, "sumsq", torch.float64), zp, ldz,
+              _vec(ld_scalar, 1, "ld_scalar"), _vec(logdet, B, "logdet"), logdet_mode, B, D,
+              _stream(dev))
+
+
+def iso_normal_consts(var, dim):
+    """(scale, half_log_det) of MultivariateNormal(0, var*I) as torch evaluates
+    them: scale = fp32 Cholesky diagonal, half_log_det = fp32 sum of its logs."""
+    cov = torch.eye(dim, dtype=torch.float32) * var
+    L = torch.linalg.cholesky(cov)
+    return float(L[0, 0]), float(L.diagonal().log().sum())
+
+
+def normal_logprob(z, out, *, scale=1.0, hld=0.0, logdet=None, sign=1):
+    dev = _require_hip(z, out, logdet)
+    B, D = z.shape
+    zp, ldz = _mat(z, "z")
+    _timed("nfk_normal_logprob", dev, "nfk_normal_logprob", zp, ldz, _vec(logdet, B, "logdet"), _vec(out, B, "out"), B, D,
+              float(scale), float(hld), int(sign), _stream(dev))
+
+
+def trig_features(x, feat, B):
+    dev = _require_hip(x, feat)
+    n_rows, n = x.shape
+    xp, ldx = _mat(x, "x")
+    fp, ldf = _mat(feat, "feat")
+    if feat.shape != (n_rows, 2 * n):
+        raise ValueError("feat must be [B, 2n]")
+    _lib.call("nfk_trig_features", xp, ldx, fp, ldf, n_rows, n, float(B), _stream(dev))
+
+
+# ---------------------------------------------------------------------------
+def fused_nsf_supported(n_lo, n_up, hidden, K):
+    return bool(_lib.load().nfk_fused_nsf_supported(n_lo, n_up, hidden, K))
+
+
+def fused_nsf_pack(w0, b0, w2, b2, w4, b4, n_lo, n_up, hidden, K):
+    dev = _require_hip(w0, b0, w2, b2, w4, b4)
+    n = int(_lib.load().nfk_fused_nsf_pack_elems(n_lo, n_up, hidden, K))
+    pack = torch.empty(n, dtype=F32, device=dev)
+    ws = [t.detach().contiguous() for t in (w0, b0, w2, b2, w4, b4)]
+    _lib.call("nfk_fused_nsf_pack", *[t.data_ptr() for t in ws], n_lo, n_up, hidden, K,
+              pack.data_ptr(), _stream(dev))
+    return pack
+
+
+def fused_nsf(x, wpack, up_in, up_out, lo_in, lo_out, hidden, z, *, logdet, logdet_mode, K,
+              tail_bound, inverse=False, status=None):
+    dev = _require_hip(x, wpack, up_in, z, logdet, status)
+    B = x.shape[0]
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    _timed("nfk_fused_nsf", dev, "nfk_fused_nsf", xp, ldx, wpack.data_ptr(), up_in.data_ptr(), up_out.data_ptr(),
+              up_in.numel(), lo_in.data_ptr(), lo_out.data_ptr(), lo_in.numel(), hidden, zp, ldz,
+              _vec(logdet, B, "logdet"), logdet_mode, B, K, float(tail_bound),
+              1 if inverse else 0, _vec(status, 1, "status", torch.int32), _stream(dev))

@@ -1,0 +1,125 @@
+"""NormalizingFlowModel with the reference's API (nf/models.py:5-40).
+
+forward(x)  -> (z, prior_logprob, log_det)      models.py:13-20
+inverse(z)  -> (x, log_det)                     models.py:22-29
+sample(n)   -> (x.data, log_px.data, z.data)    models.py:31-35
+evaluate(x) -> log_px.data                      models.py:37-40
+log_prob(x) == evaluate(x)   (the north-star name; NormalizingFlow is an alias)
+
+The layer loop enqueues one kernel chain per layer on the current HIP stream,
+accumulating log|det| in place (no per-layer temporaries, no host syncs); the
+reference's errors are raised after the chain from the kernels' status words
+(config.STRICT_CHECKS).  An isotropic-normal prior (the reference's "Normal"
+prior, applications/src/setup.py:25-30) is evaluated by the fused
+nfk_normal_logprob epilogue; any other prior object is called as is.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import config
+from . import kernels as K_
+from .flows import _HipFlow, _check_input, _grad_warning, raise_on_status
+
+__all__ = ["NormalizingFlowModel", "NormalizingFlow"]
+
+
+def _iso_normal(prior):
+    """(scale, half_log_det) if ``prior`` is MultivariateNormal(0, s^2 I), else None."""
+    if not isinstance(prior, torch.distributions.MultivariateNormal):
+        return None
+    loc = prior.loc
+    L = prior.scale_tril
+    if loc.dim() != 1 or L.dim() != 2 or L.dtype != torch.float32:
+        return None
+    d = L.diagonal()
+    off = L - torch.diag_embed(d)
+    ok = bool((loc == 0).all()) and bool((off == 0).all()) and bool((d == d[0]).all())
+    if not ok:
+        return None
+    hld = float(d.log().sum())  # MultivariateNormal's half_log_det, as torch evaluates it
+    return float(d[0]), hld
+
+
+class NormalizingFlowModel(nn.Module):
+
+    def __init__(self, prior, flows, device="cpu"):
+        super().__init__()
+        self.device = device
+        self.prior = prior
+        self.flows = nn.ModuleList(flows)
+        self._prior_key = None
+        self._prior_iso = None
+
+    # ------------------------------------------------------------------ prior
+    def _prior_consts(self):
+        p = self.prior
+        key = (id(p),) + tuple((t.data_ptr(), t._version) for t in (p.loc, p.scale_tril)) \
+            if isinstance(p, torch.distributions.MultivariateNormal) else (id(p),)
+        if key != self._prior_key:
+            self._prior_iso = _iso_normal(p)
+            self._prior_key = key
+        return self._prior_iso
+
+    def _prior_log_prob(self, z, logdet=None, sign=1):
+        iso = self._prior_consts()
+        if iso is not None and z.shape[1] == self.prior.loc.shape[0]:
+            out = torch.empty(z.shape[0], dtype=torch.float32, device=z.device)
+            K_.normal_logprob(z, out, scale=iso[0], hld=iso[1], logdet=logdet, sign=sign)
+            return out
+        lp = self.prior.log_prob(z)
+        if logdet is None:
+            return lp
+        return lp + logdet if sign >= 0 else lp - logdet
+
+    # ------------------------------------------------------------------ chain
+    def _status(self, device):
+        n = sum(f._n_status for f in self.flows if isinstance(f, _HipFlow))
+        return torch.zeros(max(n, 1), dtype=torch.int32, device=device), n
+
+    def _chain(self, x, inverse):
+        x = _check_input(x)
+        _grad_warning(self)
+        m = x.shape[0]
+        logdet = torch.zeros(m, dtype=torch.float32, device=x.device)
+        status, n_st = self._status(x.device)
+        off = 0
+        flows = self.flows[::-1] if inverse else self.flows
+        with torch.no_grad():
+            for flow in flows:
+                if isinstance(flow, _HipFlow):
+                    k = flow._n_status
+                    st = status[off:off + k] if k else None
+                    off += k
+                    x = flow._run(x, inverse, logdet, K_.MODE_ACC, st)
+                else:  # a user-defined layer: reference protocol
+                    x, ld = flow.inverse(x) if inverse else flow.forward(x)
+                    logdet += ld
+        if n_st and config.STRICT_CHECKS:
+            raise_on_status(status, n_st)
+        return x, logdet
+
+    # ------------------------------------------------------------------ API
+    def forward(self, x):
+        z, log_det = self._chain(x, False)
+        return z, self._prior_log_prob(z), log_det
+
+    def inverse(self, z):
+        return self._chain(z, True)
+
+    def sample(self, n_samples):
+        z = self.prior.sample((n_samples,))
+        x, log_det = self.inverse(z)
+        log_px = self._prior_log_prob(z, logdet=log_det, sign=-1)
+        return x.data, log_px.data, z.data
+
+    def evaluate(self, x):
+        z, log_det = self._chain(x, False)
+        return self._prior_log_prob(z, logdet=log_det, sign=1).data
+
+    def log_prob(self, x):
+        return self.evaluate(x)
+
+
+NormalizingFlow = NormalizingFlowModel

@@ -1,0 +1,98 @@
+"""Rational-quadratic spline functions with the reference's signatures
+(nf/utils.py:13-152), evaluated by nfk_rqs_coupling / nfk_searchsorted.
+
+Like the reference these raise on bad input (ValueError for the bin-size and
+domain checks, RuntimeError when no element is inside the tails interval,
+AssertionError on a negative discriminant); the data-dependent ones are read
+back from the kernel's status word once per call.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import config
+from . import kernels as K_
+from .flows import raise_on_status
+
+__all__ = ["DEFAULT_MIN_BIN_WIDTH", "DEFAULT_MIN_BIN_HEIGHT", "DEFAULT_MIN_DERIVATIVE",
+           "searchsorted", "unconstrained_RQS", "RQS"]
+
+DEFAULT_MIN_BIN_WIDTH = 1e-3
+DEFAULT_MIN_BIN_HEIGHT = 1e-3
+DEFAULT_MIN_DERIVATIVE = 1e-3
+
+_cols = {}
+
+
+def _col0(device):
+    c = _cols.get(str(device))
+    if c is None:
+        c = _cols[str(device)] = torch.zeros(1, dtype=torch.int32, device=device)
+    return c
+
+
+def searchsorted(bin_locations, inputs, eps=1e-6):
+    """utils.py:20-25 -- mutates ``bin_locations[..., -1] += eps`` in place, as
+    the reference does, and returns #(inputs >= bin_locations) - 1."""
+    return K_.searchsorted(bin_locations, inputs, eps)
+
+
+def _check_bins(nb, min_bin_width, min_bin_height):
+    if min_bin_width * nb > 1.0:
+        raise ValueError("Minimal bin width too large for the number of bins")
+    if min_bin_height * nb > 1.0:
+        raise ValueError("Minimal bin height too large for the number of bins")
+
+
+def _spline(inputs, w, h, d, inverse, left, right, bottom, top, tails, mode, mbw, mbh, mbd):
+    if not inputs.is_cuda:
+        raise RuntimeError("normalizingflow_amd runs on the ROCm device only; there is no CPU "
+                           "fallback (got a %s tensor)" % inputs.device)
+    K = w.shape[-1]
+    _check_bins(K, mbw, mbh)
+    n = inputs.numel()
+    flat = lambda t, c: t.reshape(n, c).to(torch.float32)
+    params = torch.cat([flat(w, K), flat(h, K), flat(d, d.shape[-1])], dim=1).contiguous()
+    x = inputs.reshape(n, 1).to(torch.float32)
+    out = torch.empty(n, 1, dtype=torch.float32, device=inputs.device)
+    lad = torch.empty(n, 1, dtype=torch.float32, device=inputs.device)
+    st = torch.zeros(1, dtype=torch.int32, device=inputs.device)
+    col = _col0(inputs.device)
+    K_.rqs_coupling(x, params, col, col, out, lad_out=lad, K=K, left=left, right=right,
+                    bottom=bottom, top=top, tails=tails, min_bin_width=mbw, min_bin_height=mbh,
+                    min_derivative=mbd, param_mode=mode, inverse=inverse, status=st)
+    if config.STRICT_CHECKS:
+        raise_on_status(st)
+    return out.reshape(inputs.shape), lad.reshape(inputs.shape)
+
+
+def unconstrained_RQS(inputs, unnormalized_widths, unnormalized_heights,
+                      unnormalized_derivatives, inverse=False, tail_bound=1.,
+                      min_bin_width=DEFAULT_MIN_BIN_WIDTH, min_bin_height=DEFAULT_MIN_BIN_HEIGHT,
+                      min_derivative=DEFAULT_MIN_DERIVATIVE):
+    """utils.py:27-56: spline on [-B, B] with identity tails; derivatives carry
+    K-1 interior logits (the two boundary ones are fixed so the slope is 1)."""
+    if unnormalized_derivatives.shape[-1] != unnormalized_widths.shape[-1] - 1:
+        raise ValueError("unnormalized_derivatives must have K-1 entries")
+    tb = float(tail_bound)
+    return _spline(inputs, unnormalized_widths, unnormalized_heights, unnormalized_derivatives,
+                   inverse, -tb, tb, -tb, tb, True, 1, min_bin_width, min_bin_height,
+                   min_derivative)
+
+
+def RQS(inputs, unnormalized_widths, unnormalized_heights, unnormalized_derivatives,
+        inverse=False, left=0., right=1., bottom=0., top=1.,
+        min_bin_width=DEFAULT_MIN_BIN_WIDTH, min_bin_height=DEFAULT_MIN_BIN_HEIGHT,
+        min_derivative=DEFAULT_MIN_DERIVATIVE):
+    """utils.py:58-152: spline on [left, right] x [bottom, top], all K+1
+    derivative logits given.  Raises ValueError("Input outside domain") like
+    the reference (one device->host read of min/max)."""
+    if torch.min(inputs) < left or torch.max(inputs) > right:
+        raise ValueError("Input outside domain")
+    if unnormalized_derivatives.shape[-1] != unnormalized_widths.shape[-1] + 1:
+        raise ValueError("unnormalized_derivatives must have K+1 entries")
+    out, lad = _spline(inputs, unnormalized_widths, unnormalized_heights,
+                       unnormalized_derivatives, inverse, float(left), float(right),
+                       float(bottom), float(top), False, 2, min_bin_width, min_bin_height,
+                       min_derivative)
+    return out, lad

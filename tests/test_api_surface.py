@@ -1,0 +1,99 @@
+"""CPU checks of the drop-in Python surface: names, constructor arguments,
+state_dict keys and parameter-initialisation order match the reference (the
+golden fixtures hold the reference's own state_dicts built under the same
+seed), and the product path refuses CPU tensors instead of falling back."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import golden_io as gio
+import nf.flows as nff
+import nf.models as nfm
+import nf.utils as nfu
+
+NL = {"tanh": torch.tanh, "leaky_relu": F.leaky_relu, "elu": F.elu}
+
+
+def build_layer(meta):
+    kw = dict(meta["kwargs"])
+    cls = getattr(nff, meta["type"])
+    if meta["type"] == "Planar":
+        kw["nonlinearity"] = NL[meta.get("nonlinearity", "tanh")]
+    return cls(**kw)
+
+
+LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar")]
+
+
+@pytest.mark.parametrize("name", LAYERS)
+def test_same_seed_same_weights_and_keys(name):
+    meta, _, sd = gio.load(name)
+    torch.manual_seed(meta["seed"])
+    layer = build_layer(meta)
+    ours = layer.state_dict()
+    assert list(ours.keys()) == list(sd.keys())
+    if meta["type"] == "Radial":
+        return  # the reference leaves Radial's parameters uninitialised (flows_1.py:72-83)
+    for k in sd:
+        torch.testing.assert_close(ours[k], sd[k], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("name", gio.names("model_"))
+def test_model_state_dict_round_trip(name):
+    meta, _, sd = gio.load(name)
+    torch.manual_seed(meta["seed"])
+    flows = []
+    for l in meta["layers"]:
+        flows.append(build_layer(dict(type=l["type"], kwargs=l["kwargs"])))
+    d = meta["dim"]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(d), meta["var"] * torch.eye(d))
+    model = nfm.NormalizingFlowModel(prior, flows)
+    assert list(model.state_dict().keys()) == list(sd.keys())
+    for k in sd:
+        torch.testing.assert_close(model.state_dict()[k], sd[k], rtol=0, atol=0)
+    model.load_state_dict(sd, strict=False)
+
+
+def test_exports():
+    for n in ("FCNN", "RealNVP", "NSF_AR", "NSF_CL", "Planar", "Radial"):
+        assert hasattr(nff, n)
+    assert nfm.NormalizingFlow is nfm.NormalizingFlowModel
+    assert hasattr(nfm.NormalizingFlowModel, "log_prob")
+    for n in ("unconstrained_RQS", "RQS", "searchsorted", "DEFAULT_MIN_BIN_WIDTH"):
+        assert hasattr(nfu, n)
+    # setup.py:55-62 instantiates layers by eval() of the class name after `from nf.flows import *`
+    ns = {}
+    exec("from nf.flows import *", ns)
+    for n in ("RealNVP", "NSF_AR", "NSF_CL"):
+        assert n in ns
+
+
+def test_no_cpu_fallback():
+    layer = nff.NSF_CL(size=4, dim=2, K=8, B=3, hidden_dim=8, mask=[0])
+    with pytest.raises(RuntimeError, match="ROCm device only"):
+        layer(torch.zeros(3, 8))
+    prior = torch.distributions.MultivariateNormal(torch.zeros(8), torch.eye(8))
+    model = nfm.NormalizingFlowModel(prior, [layer])
+    with pytest.raises(RuntimeError, match="ROCm device only"):
+        model.evaluate(torch.zeros(3, 8))
+    with pytest.raises(RuntimeError, match="ROCm device only"):
+        nfu.unconstrained_RQS(torch.zeros(4), torch.zeros(4, 8), torch.zeros(4, 8),
+                              torch.zeros(4, 7), tail_bound=3.0)
+
+
+def test_radial_and_planar_have_reference_inverse_behaviour():
+    with pytest.raises(NotImplementedError):
+        nff.Planar(4).inverse(torch.zeros(2, 4))
+    assert not hasattr(nff.Radial(4), "inverse")
+
+
+def test_nsf_cl_maps_follow_reference_layout():
+    # dim=3, mask [1,2] (non-prefix): lower = coords 1,2 of each particle,
+    # output puts them first in each group (flows.py:239)
+    layer = nff.NSF_CL(size=2, dim=3, K=4, B=3, hidden_dim=4, mask=[1, 2])
+    m = layer._maps.__func__  # no device use: call with a CPU device just to build lists
+    maps = m(layer, torch.device("cpu"))
+    assert maps.lo_in.tolist() == [1, 2, 4, 5]
+    assert maps.up_in.tolist() == [0, 3]
+    assert maps.lo_out.tolist() == [0, 1, 3, 4]
+    assert maps.up_out.tolist() == [2, 5]

@@ -1,0 +1,379 @@
+"""GPU parity: the HIP path vs (a) the reference's golden vectors and (b) the
+CPU oracle on the same seeded inputs and weights, plus size-independent
+properties at the BASELINE sizes.
+
+Tolerances (north star: log_prob within 1e-5 relative, fp32):
+  log_prob / prior_lp     rtol 1e-5 (+ atol 1e-5 for values near 0)
+  z (elementwise)         rtol 1e-5, atol 2e-5  -- the reference's own fp32 z
+                          is off its fp64 value by up to 6.5e-6
+  per-layer log|det|      rtol 1e-5, atol 5e-5  (sum of up to 32 terms)
+For the extreme-parameter spline fixture the bound is "no worse than the
+reference": |ours - fp64| <= 2*|reference_fp32 - fp64| + 1e-5.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import golden_io as gio
+import nf.flows as nff
+import nf.models as nfm
+import nf.utils as nfu
+from normalizingflow_amd import config
+from oracle import nf_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+Z_RTOL, Z_ATOL = 1e-5, 2e-5
+LD_RTOL, LD_ATOL = 1e-5, 5e-5
+LP_RTOL, LP_ATOL = 1e-5, 1e-5
+NL = {"tanh": torch.tanh, "leaky_relu": F.leaky_relu, "elu": F.elu}
+DEV = "cuda:0"
+
+
+def close(a, b, rtol, atol):
+    torch.testing.assert_close(a.detach().cpu(), b.detach().cpu(), rtol=rtol, atol=atol)
+
+
+def build_layer(meta):
+    kw = dict(meta["kwargs"])
+    if meta["type"] == "Planar":
+        kw["nonlinearity"] = NL[meta.get("nonlinearity", "tanh")]
+    return getattr(nff, meta["type"])(**kw)
+
+
+def spec_of(layer, prefix):
+    if isinstance(layer, nff.NSF_CL):
+        return dict(type="NSF_CL", prefix=prefix, size=layer.size, dim=layer.dim, K=layer.K,
+                    B=layer.B, mask=[int(m) for m in layer.mask])
+    if isinstance(layer, nff.RealNVP):
+        return dict(type="RealNVP", prefix=prefix, dim=layer.dim)
+    if isinstance(layer, nff.NSF_AR):
+        return dict(type="NSF_AR", prefix=prefix, dim=layer.dim, K=layer.K, B=layer.B)
+    if isinstance(layer, nff.Planar):
+        return dict(type="Planar", prefix=prefix, nonlinearity=layer.h.__name__)
+    if isinstance(layer, nff.Radial):
+        return dict(type="Radial", prefix=prefix)
+    raise TypeError(type(layer))
+
+
+def cpu_sd(module):
+    return {k: v.detach().cpu() for k, v in module.state_dict().items()}
+
+
+# --------------------------------------------------------------------------- golden
+LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar")]
+
+
+@pytest.mark.parametrize("name", LAYERS)
+def test_layer_vs_reference_golden(name, hip_device):
+    meta, d, sd = gio.load(name)
+    layer = build_layer(meta)
+    layer.load_state_dict(sd)
+    layer = layer.to(hip_device)
+    with torch.no_grad():
+        z, ld = layer(d["x"].to(hip_device))
+        close(z, d["z"], Z_RTOL, Z_ATOL)
+        close(ld, d["ld"], LD_RTOL, LD_ATOL)
+        if "rt_x" in d:
+            xi, ldi = layer.inverse(d["z"].to(hip_device))
+            close(xi, d["rt_x"], Z_RTOL, 5e-5)
+            close(ldi, d["rt_ld"], LD_RTOL, LD_ATOL)
+            xa, lda = layer.inverse(d["x"].to(hip_device))
+            close(xa, d["inv_x"], Z_RTOL, 5e-5)
+            close(lda, d["inv_ld"], LD_RTOL, LD_ATOL)
+
+
+def _golden_model(meta, sd, device):
+    flows = [build_layer(dict(type=l["type"], kwargs=l["kwargs"])) for l in meta["layers"]]
+    d = meta["dim"]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(d, device=device),
+                                                   meta["var"] * torch.eye(d, device=device))
+    model = nfm.NormalizingFlowModel(prior, flows)
+    model.load_state_dict(sd, strict=False)
+    return model.to(device)
+
+
+@pytest.mark.parametrize("name", gio.names("model_"))
+def test_model_vs_reference_golden(name, hip_device):
+    meta, d, sd = gio.load(name)
+    model = _golden_model(meta, sd, hip_device)
+    x = d["x"].to(hip_device)
+    with torch.no_grad():
+        z, plp, ld = model(x)
+        close(z, d["z"], Z_RTOL, Z_ATOL)
+        close(plp, d["prior_lp"], LP_RTOL, LP_ATOL)
+        close(ld, d["ld"], LD_RTOL, 1e-4)
+        close(model.evaluate(x), d["log_prob"], LP_RTOL, 1e-4)
+        close(model.log_prob(x), d["log_prob"], LP_RTOL, 1e-4)
+        if "rt_x" in d:
+            xi, ldi = model.inverse(d["z"].to(hip_device))
+            close(xi, d["rt_x"], Z_RTOL, 5e-5)
+            close(ldi, d["rt_ld"], LD_RTOL, 1e-4)
+            # sample(): the prior draws differ by device RNG, so feed the
+            # reference's draws through our inverse + prior epilogue
+            zs = d["sample_z"].to(hip_device)
+            xs, lds = model.inverse(zs)
+            lp = model._prior_log_prob(zs, logdet=lds, sign=-1)
+            close(xs, d["sample_x"], Z_RTOL, 5e-5)
+            close(lp, d["sample_log_px"], LP_RTOL, 1e-4)
+            xs2, lps2, zs2 = model.sample(64)
+            assert xs2.shape == (64, meta["dim"]) and lps2.shape == (64,)
+            assert bool(torch.isfinite(lps2).all())
+
+
+@pytest.mark.parametrize("name", gio.names("rqs_"))
+def test_unconstrained_rqs_vs_reference_golden(name, hip_device):
+    meta, d, _ = gio.load(name)
+    tb = meta["tail_bound"]
+    dv = lambda k: d[k].to(hip_device)
+    y, lad = nfu.unconstrained_RQS(dv("x"), dv("uw"), dv("uh"), dv("ud"), tail_bound=tb)
+    yi, ladi = nfu.unconstrained_RQS(dv("y"), dv("uw"), dv("uh"), dv("ud"), inverse=True,
+                                     tail_bound=tb)
+    if meta["scale"] <= 1.5:
+        close(y, d["y"], Z_RTOL, Z_ATOL)
+        close(lad, d["lad"], LD_RTOL, LD_ATOL)
+        close(yi, d["inv_y"], Z_RTOL, 5e-5)
+        close(ladi, d["inv_lad"], LD_RTOL, LD_ATOL)
+    # no worse than the reference against the fp64 truth
+    y64, l64 = d["y_f64"], d["lad_f64"]
+    err_ref_y = (d["y"].double() - y64).abs()
+    err_ref_l = (d["lad"].double() - l64).abs()
+    assert bool(((y.cpu().double() - y64).abs() <= 2 * err_ref_y + 1e-5).all())
+    assert bool(((lad.cpu().double() - l64).abs() <= 2 * err_ref_l + 1e-5).all())
+
+
+# --------------------------------------------------------------------------- oracle, random
+def _c3_model(n_layers=8, size=32, dim=2, K=8, hidden=100, seed=1234):
+    torch.manual_seed(seed)
+    flows = [nff.NSF_CL(size=size, dim=dim, K=K, B=3, hidden_dim=hidden, mask=[i % 2])
+             for i in range(n_layers)]
+    D = size * dim
+    prior = torch.distributions.MultivariateNormal(torch.zeros(D), torch.eye(D))
+    return nfm.NormalizingFlowModel(prior, flows)
+
+
+def _specs(model):
+    return [spec_of(f, "flows.%d." % i) for i, f in enumerate(model.flows)]
+
+
+def _to_dev(model, device):
+    D = model.prior.loc.shape[0]
+    var = float(model.prior.covariance_matrix[0, 0])
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(D, device=device),
+                                                        var * torch.eye(D, device=device))
+    return model.to(device)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_c3_log_prob_vs_oracle(fused, hip_device):
+    model = _c3_model()
+    sd, specs = cpu_sd(model), _specs(model)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(4096, 64, generator=g)
+    ref = orc.model_log_prob(specs, sd, x)
+    z_ref, _, ld_ref = orc.model_forward(specs, sd, x)
+    model = _to_dev(model, hip_device)
+    old = config.USE_FUSED
+    config.USE_FUSED = fused
+    try:
+        with torch.no_grad():
+            lp = model.log_prob(x.to(hip_device))
+            z, plp, ld = model(x.to(hip_device))
+    finally:
+        config.USE_FUSED = old
+    close(lp, ref, LP_RTOL, LP_ATOL)
+    close(z, z_ref, Z_RTOL, 5e-5)
+    close(ld, ld_ref, LD_RTOL, 2e-4)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_c3_inverse_vs_oracle(fused, hip_device):
+    model = _c3_model(n_layers=4)
+    sd, specs = cpu_sd(model), _specs(model)
+    g = torch.Generator().manual_seed(5)
+    z = torch.randn(2048, 64, generator=g)
+    x_ref, ld_ref = orc.model_inverse(specs, sd, z)
+    model = _to_dev(model, hip_device)
+    old = config.USE_FUSED
+    config.USE_FUSED = fused
+    try:
+        x, ld = model.inverse(z.to(hip_device))
+    finally:
+        config.USE_FUSED = old
+    close(x, x_ref, Z_RTOL, 1e-4)
+    close(ld, ld_ref, LD_RTOL, 2e-4)
+
+
+def test_realnvp_c2_vs_oracle(hip_device):
+    torch.manual_seed(1234)
+    flows = [nff.RealNVP(64, hidden_dim=100) for _ in range(8)]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(64), torch.eye(64))
+    model = nfm.NormalizingFlowModel(prior, flows)
+    sd, specs = cpu_sd(model), _specs(model)
+    x = torch.randn(2048, 64, generator=torch.Generator().manual_seed(1))
+    ref = orc.model_log_prob(specs, sd, x)
+    model = _to_dev(model, hip_device)
+    lp = model.log_prob(x.to(hip_device))
+    close(lp, ref, LP_RTOL, 1e-4)
+    xr, _ = model.inverse(model(x.to(hip_device))[0])
+    close(xr, x, 1e-4, 1e-4)
+
+
+@pytest.mark.parametrize("K", [2, 4, 5, 8, 10, 16, 32])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_unconstrained_rqs_random_vs_oracle(K, inverse, hip_device):
+    g = torch.Generator().manual_seed(100 + K)
+    n = 3000
+    x = torch.randn(n, generator=g) * 2.5
+    w, h, d = (torch.randn(n, K, generator=g), torch.randn(n, K, generator=g),
+               torch.randn(n, K - 1, generator=g))
+    y_ref, l_ref = orc.unconstrained_rq_spline(x, w, h, d, inverse=inverse, tail_bound=3.0)
+    y, l = nfu.unconstrained_RQS(*(t.to(hip_device) for t in (x, w, h, d)), inverse=inverse,
+                                 tail_bound=3.0)
+    close(y, y_ref, Z_RTOL, 5e-5)
+    close(l, l_ref, LD_RTOL, 5e-5)
+
+
+def test_rqs_bare_bounds_vs_oracle(hip_device):
+    g = torch.Generator().manual_seed(9)
+    n, K = 1000, 6
+    x = torch.rand(n, generator=g) * 0.98 + 0.01
+    w, h, d = (torch.randn(n, K, generator=g), torch.randn(n, K, generator=g),
+               torch.randn(n, K + 1, generator=g))
+    for inv in (False, True):
+        y_ref, l_ref, _ = orc.rq_spline(x, w, h, d, inverse=inv)
+        y, l = nfu.RQS(*(t.to(hip_device) for t in (x, w, h, d)), inverse=inv)
+        close(y, y_ref, Z_RTOL, 2e-5)
+        close(l, l_ref, LD_RTOL, 5e-5)
+    with pytest.raises(ValueError, match="outside domain"):
+        nfu.RQS((x + 2).to(hip_device), *(t.to(hip_device) for t in (w, h, d)))
+
+
+def test_searchsorted_side_effect(hip_device):
+    loc = torch.tensor([[0.0, 0.5, 1.0], [0.0, 0.25, 1.0]])
+    v = torch.tensor([1.0, 0.3])
+    ref_loc = loc.clone()
+    ref_loc[..., -1] += 1e-6
+    ref = (v[..., None] >= ref_loc).sum(-1) - 1
+    dl = loc.to(hip_device)
+    idx = nfu.searchsorted(dl, v.to(hip_device))
+    assert idx.cpu().tolist() == ref.tolist()
+    assert torch.equal(dl.cpu(), ref_loc)
+
+
+@pytest.mark.parametrize("nl", ["tanh", "leaky_relu", "elu"])
+def test_planar_random_vs_oracle(nl, hip_device):
+    torch.manual_seed(3)
+    layer = nff.Planar(37, nonlinearity=NL[nl])
+    x = torch.randn(999, 37)
+    z_ref, ld_ref = orc.planar(x, cpu_sd(layer), "", nl)
+    z, ld = layer.to(hip_device)(x.to(hip_device))
+    close(z, z_ref, Z_RTOL, Z_ATOL)
+    close(ld, ld_ref, LD_RTOL, LD_ATOL)
+
+
+def test_radial_random_vs_oracle(hip_device):
+    layer = nff.Radial(24)
+    torch.manual_seed(4)
+    layer.reset_parameters(24)
+    x = torch.randn(5000, 24)
+    z_ref, ld_ref = orc.radial(x, cpu_sd(layer), "")
+    z, ld = layer.to(hip_device)(x.to(hip_device))
+    assert ld.shape == (1,)
+    close(z, z_ref, Z_RTOL, Z_ATOL)
+    close(ld, ld_ref, LD_RTOL, LD_ATOL)
+
+
+def test_nsf_ar_random_vs_oracle(hip_device):
+    torch.manual_seed(8)
+    layer = nff.NSF_AR(dim=6, K=8, B=3, hidden_dim=32)
+    x = torch.randn(777, 6) * 1.5
+    sd = cpu_sd(layer)
+    for inv in (False, True):
+        z_ref, ld_ref = orc.nsf_ar(x, sd, "", 6, 8, 3, inverse=inv)
+        z, ld = (layer.to(hip_device).inverse if inv else layer.to(hip_device))(x.to(hip_device))
+        close(z, z_ref, Z_RTOL, 5e-5)
+        close(ld, ld_ref, LD_RTOL, LD_ATOL)
+
+
+# --------------------------------------------------------------------------- edge cases
+def test_all_outside_raises_like_reference(hip_device):
+    layer = nff.NSF_CL(size=4, dim=2, K=8, B=3, hidden_dim=8, mask=[0]).to(hip_device)
+    x = torch.full((16, 8), 10.0, device=hip_device)
+    with pytest.raises(RuntimeError):
+        layer(x)
+    with pytest.raises(RuntimeError):
+        layer(torch.zeros(0, 8, device=hip_device))  # empty batch: torch.min of empty
+    with pytest.raises(RuntimeError):
+        nfu.unconstrained_RQS(torch.full((4,), 9.0, device=hip_device),
+                              torch.zeros(4, 8, device=hip_device),
+                              torch.zeros(4, 8, device=hip_device),
+                              torch.zeros(4, 7, device=hip_device), tail_bound=3.0)
+
+
+def test_tails_identity_and_boundaries(hip_device):
+    n, K = 8, 8
+    x = torch.tensor([-3.0, 3.0, -3.0001, 3.0001, 100.0, -100.0, 0.0, 1e-7])
+    g = torch.Generator().manual_seed(2)
+    w, h, d = torch.randn(n, K, generator=g), torch.randn(n, K, generator=g), torch.randn(n, K - 1, generator=g)
+    y, l = nfu.unconstrained_RQS(*(t.to(hip_device) for t in (x, w, h, d)), tail_bound=3.0)
+    y_ref, l_ref = orc.unconstrained_rq_spline(x, w, h, d, tail_bound=3.0)
+    close(y, y_ref, 0, 2e-6)
+    close(l, l_ref, 0, 2e-5)
+    assert y.cpu()[2:6].tolist() == x[2:6].tolist() and l.cpu()[2:6].abs().sum() == 0
+
+
+def test_dim3_masks_and_ragged_batch(hip_device):
+    for mask in ([0], [1], [2], [0, 1], [1, 2], [0, 2]):
+        torch.manual_seed(11)
+        layer = nff.NSF_CL(size=5, dim=3, K=6, B=2.0, hidden_dim=24, mask=mask)
+        x = torch.randn(1001, 15)
+        z_ref, ld_ref = orc.nsf_cl(x, cpu_sd(layer), "", 5, 3, 6, 2.0, mask)
+        z, ld = layer.to(hip_device)(x.to(hip_device))
+        close(z, z_ref, Z_RTOL, Z_ATOL)
+        close(ld, ld_ref, LD_RTOL, LD_ATOL)
+
+
+def test_large_n_up_rounds(hip_device):
+    # n_up > 256 exercises the multi-round path of the streaming kernel
+    torch.manual_seed(12)
+    layer = nff.NSF_CL(size=300, dim=2, K=4, B=3, hidden_dim=16, mask=[1])
+    x = torch.randn(37, 600)
+    z_ref, ld_ref = orc.nsf_cl(x, cpu_sd(layer), "", 300, 2, 4, 3, [1])
+    old = config.USE_FUSED
+    config.USE_FUSED = False
+    try:
+        z, ld = layer.to(hip_device)(x.to(hip_device))
+    finally:
+        config.USE_FUSED = old
+    close(z, z_ref, Z_RTOL, Z_ATOL)
+    close(ld, ld_ref, LD_RTOL, 2e-4)
+
+
+# --------------------------------------------------------------------------- full size
+def test_c3_full_batch_properties(hip_device):
+    """BASELINE c3 at B = 2^20: row-subsample parity with the oracle (samples
+    are independent), inverse o forward round trip for the prefix-mask layers,
+    log-det antisymmetry, and run-to-run bitwise determinism."""
+    model = _c3_model()
+    sd, specs = cpu_sd(model), _specs(model)
+    B = 1 << 20
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B, 64, generator=g)
+    rows = torch.randperm(B, generator=g)[:1024]
+    ref = orc.model_log_prob(specs, sd, x[rows])
+    model = _to_dev(model, hip_device)
+    xd = x.to(hip_device)
+    lp1 = model.log_prob(xd)
+    lp2 = model.log_prob(xd)
+    assert torch.equal(lp1, lp2)
+    close(lp1[rows.to(hip_device)], ref, LP_RTOL, LP_ATOL)
+    # a prefix-mask stack is exactly invertible (flows.py:239 keeps the layout)
+    torch.manual_seed(7)
+    pre = nfm.NormalizingFlowModel(model.prior, [nff.NSF_CL(size=32, dim=2, K=8, B=3,
+                                                            hidden_dim=100, mask=[0])
+                                                 for _ in range(4)]).to(hip_device)
+    z, _, ld_f = pre(xd)
+    xr, ld_i = pre.inverse(z)
+    assert float((xr - xd).abs().max()) < 1e-3
+    assert float((ld_f + ld_i).abs().max()) < 1e-3
