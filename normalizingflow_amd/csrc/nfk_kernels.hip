@@ -249,13 +249,14 @@ extern "C" int nfk_rqs_coupling(const float* x, int64_t ldx, const float* params
                                 double min_derivative, int32_t param_mode, int32_t inverse,
                                 int32_t* status, nfk_stream_t stream) {
     if (batch < 0 || n_up <= 0 || n_lo < 0) return nfk_set_error("nfk_rqs_coupling: bad sizes");
+    if (min_bin_width * K > 1.0) return nfk_set_error("Minimal bin width too large for the number of bins");
+    if (min_bin_height * K > 1.0) return nfk_set_error("Minimal bin height too large for the number of bins");
+    if (batch == 0) return 0;  // nothing inside: status stays 0 (reference: RuntimeError)
     if (x == nullptr || params == nullptr || z == nullptr || up_in == nullptr || up_out == nullptr)
         return nfk_set_error("nfk_rqs_coupling: null pointer");
     if (n_lo > 0 && (lo_in == nullptr || lo_out == nullptr))
         return nfk_set_error("nfk_rqs_coupling: null lower index map");
     if (logdet_mode != 0 && logdet == nullptr) return nfk_set_error("nfk_rqs_coupling: null logdet");
-    if (min_bin_width * K > 1.0) return nfk_set_error("Minimal bin width too large for the number of bins");
-    if (min_bin_height * K > 1.0) return nfk_set_error("Minimal bin height too large for the number of bins");
     RqsArgs a{x, ldx, params, up_in, up_out, n_up, lo_in, lo_out, n_lo, z, ldz, logdet,
               logdet_mode, lad_out, ld_lad, batch, 1, status,
               nfk_make_const(K, left, right, bottom, top, tails, min_bin_width, min_bin_height,
@@ -293,6 +294,7 @@ __global__ __launch_bounds__(256) void k_searchsorted(float* loc, const float* _
 extern "C" int nfk_searchsorted(float* bin_locations, const float* inputs, int64_t* idx,
                                 int64_t rows, int32_t n_loc, double eps, nfk_stream_t stream) {
     if (rows < 0 || n_loc <= 0) return nfk_set_error("nfk_searchsorted: bad sizes");
+    if (rows == 0) return 0;
     if (!bin_locations || !inputs || !idx) return nfk_set_error("nfk_searchsorted: null pointer");
     if (rows == 0) return 0;
     int64_t g = (rows + 255) / 256;
@@ -374,6 +376,7 @@ extern "C" int nfk_affine_coupling(const float* x_in, int64_t ld_in, const float
                                    float* logdet, int32_t logdet_mode, int64_t batch, int32_t n,
                                    int32_t inverse, nfk_stream_t stream) {
     if (batch < 0 || n <= 0) return nfk_set_error("nfk_affine_coupling: bad sizes");
+    if (batch == 0) return 0;
     if (!x_in || !s || !t || !x_out) return nfk_set_error("nfk_affine_coupling: null pointer");
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_affine_coupling: null logdet");
     if (batch == 0) return 0;
@@ -478,6 +481,7 @@ extern "C" int nfk_planar(const float* x, int64_t ldx, const float* w, const flo
                           int32_t logdet_mode, float* ld_out, int64_t batch, int32_t dim,
                           int32_t nonlinearity, nfk_stream_t stream) {
     if (batch < 0 || dim <= 0 || dim > 16384) return nfk_set_error("nfk_planar: bad sizes");
+    if (batch == 0) return 0;
     if (!x || !w || !u || !b || !z) return nfk_set_error("nfk_planar: null pointer");
     if (nonlinearity < 0 || nonlinearity > 2) return nfk_set_error("nfk_planar: bad nonlinearity");
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_planar: null logdet");
@@ -615,6 +619,7 @@ extern "C" int nfk_normal_logprob(const float* z, int64_t ldz, const float* logd
                                   int64_t batch, int32_t dim, float scale, float half_log_det,
                                   int32_t sign, nfk_stream_t stream) {
     if (batch < 0 || dim <= 0 || !(scale > 0.0f)) return nfk_set_error("nfk_normal_logprob: bad args");
+    if (batch == 0) return 0;
     if (!z || !out) return nfk_set_error("nfk_normal_logprob: null pointer");
     if (batch == 0) return 0;
     const int w = lanes_for(dim);
@@ -650,6 +655,7 @@ __global__ __launch_bounds__(256) void k_trig(const float* __restrict__ x, int64
 extern "C" int nfk_trig_features(const float* x, int64_t ldx, float* feat, int64_t ldf,
                                  int64_t batch, int32_t n, double B, nfk_stream_t stream) {
     if (batch < 0 || n <= 0) return nfk_set_error("nfk_trig_features: bad sizes");
+    if (batch == 0) return 0;
     if (!x || !feat) return nfk_set_error("nfk_trig_features: null pointer");
     if (batch == 0) return 0;
     int64_t g = (batch * n + 255) / 256;

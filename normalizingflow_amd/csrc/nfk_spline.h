@@ -33,17 +33,38 @@ __device__ __forceinline__ float nfk_softplus(float v) {
     return v > 20.0f ? v : log1pf(expf(v));
 }
 
-// softmax over K logits, in place (K compile-time so the arrays stay in VGPRs)
+// softmax over K logits, in place (K compile-time so the arrays stay in VGPRs).
+// Summation order of ATen's CPU kernel (vec::reduce_all, AVX-512 build the
+// golden vectors come from): sequential for K < 16; for K >= 16 the K values
+// are folded onto 16 lanes (lane i += x[i + 16m]) and reduced by the
+// xor-8/4/2/1 butterfly.  Output = e * (1/sum).
 template <int K>
 __device__ __forceinline__ void nfk_softmax(float (&u)[K]) {
     float m = u[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) m = fmaxf(m, u[i]);
-    float s = 0.0f;
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        u[i] = expf(u[i] - m);
-        s = s + u[i];
+    for (int i = 0; i < K; ++i) u[i] = expf(u[i] - m);
+    float s;
+    if constexpr (K < 16) {
+        s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < K; ++i) s = s + u[i];
+    } else {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            v[i] = u[i];
+#pragma unroll
+            for (int j = i + 16; j < K; j += 16) v[i] = v[i] + u[j];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = v[i] + v[i + 8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] + v[i + 4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) v[i] = v[i] + v[i + 2];
+        s = v[0] + v[1];
     }
     const float r = 1.0f / s;
 #pragma unroll
