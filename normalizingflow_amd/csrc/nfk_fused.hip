@@ -1,22 +1,205 @@
-// nfk_fused.hip -- fused NSF coupling layer (MLP conditioner on fp32 MFMA +
-// spline epilogue).  Placeholder until the MFMA kernel lands: reports every
-// shape as unsupported so the host layer takes the streaming path.
+// nfk_fused.hip -- one launch per NSF coupling layer: conditioner MLP
+// (FCNN, nf/flows.py:20-35) on fp32 MFMA + rational-quadratic spline epilogue
+// (nf/flows.py:227-253, nf/utils.py:27-152).  The [B, n_up, 3K-1] conditioner
+// output never leaves registers.
+//
+// Work decomposition: one wave owns ST tiles of 16 samples.  All products
+// are computed transposed, h^T[feature][sample] = W . act^T, with
+// v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fmaf chain):
+//   A operand = weights   (lane l: W[row l&15][k l>>4]),
+//   B operand = activations (lane l: act[k l>>4][sample l&15]),
+//   D: lane l, register r = output row 4*(l>>4)+r of sample l&15.
+// Hidden feature f of tile t sits in row 4*r+q... precisely: row i = 4q + r of
+// tile t holds feature 16t + 4r + q, so register r of tile t IS the B
+// fragment of k-step 4t + r (features 4ks + q) of the next product -- no LDS
+// transpose between layers.
+//
+// Output layer: per chunk of 16 coordinates the 3K-1 parameter tiles are
+// produced in three phases (W logits, H logits, D logits; H first when
+// inverting).  Row i of a parameter tile is coordinate jbase + i, so lane l
+// holds, for sample l&15, all K logits of coordinates jbase + 4q + r in
+// registers and evaluates the spline there (same fp32 op order as
+// nfk_spline.h).  Per-sample log|det| is reduced across the four lane groups
+// with xor-16/32 shuffles.
+//
+// Weights are packed once per weight version (nfk_fused_nsf_pack) in MFMA
+// fragment order, 4 tiles per float4, so every A fragment is one coalesced
+// 16-B load that feeds 4 x ST MFMAs.  The x tile and the output z tile are
+// staged through a per-wave LDS region so HBM sees only full-row accesses.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 #include "../../include/nfk.h"
+#include "nfk_spline.h"
 
 int nfk_set_error(const char* msg);
+NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, double top,
+                              int tails, double min_w, double min_h, double min_d);
 
-extern "C" int nfk_fused_nsf_supported(int32_t, int32_t, int32_t, int32_t) { return 0; }
-extern "C" int64_t nfk_fused_nsf_pack_elems(int32_t, int32_t, int32_t, int32_t) { return 0; }
-extern "C" int nfk_fused_nsf_pack(const float*, const float*, const float*, const float*,
-                                  const float*, const float*, int32_t, int32_t, int32_t, int32_t,
-                                  float*, nfk_stream_t) {
-    return nfk_set_error("nfk_fused_nsf_pack: shape not supported");
+#include "nfk_fused_impl.h"
+
+using namespace nfk_fused;
+
+namespace nfk_fused {
+#define NFK_X(h) NFK_FUSED_K(NFK_FUSED_EXTERN, h)
+NFK_FUSED_HT(NFK_X)
+#undef NFK_X
+}  // namespace nfk_fused
+
+namespace {
+
+struct PackArgs {
+    const float *w0, *b0, *w2, *b2, *w4, *b4;
+    float* out;
+    Layout L;
+};
+
+__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+    const Layout& L = a.L;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < L.total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.0f;
+        if (g < L.o_b1) {  // W1 [KS1][TGH][64][4]
+            const int64_t r = g - L.o_w1;
+            const int e = r & 3, lane = (r >> 2) & 63;
+            const int64_t blk = r >> 8;
+            const int tg = (int)(blk % L.TGH), ks = (int)(blk / L.TGH);
+            const int t = 4 * tg + e, f = hid_row(t, lane & 15), k = 4 * ks + (lane >> 4);
+            if (t < L.HT && f < L.H && k < L.n_lo) v = a.w0[(int64_t)f * L.n_lo + k];
+        } else if (g < L.o_w2) {  // b1 padded
+            const int f = (int)(g - L.o_b1);
+            if (f < L.H) v = a.b0[f];
+        } else if (g < L.o_b2) {  // W2 [KSH][TGH][64][4]
+            const int64_t r = g - L.o_w2;
+            const int e = r & 3, lane = (r >> 2) & 63;
+            const int64_t blk = r >> 8;
+            const int tg = (int)(blk % L.TGH), ks = (int)(blk / L.TGH);
+            const int t = 4 * tg + e, f = hid_row(t, lane & 15), k = 4 * ks + (lane >> 4);
+            if (t < L.HT && f < L.H && k < L.H) v = a.w2[(int64_t)f * L.H + k];
+        } else if (g < L.o_w3) {  // b2 padded
+            const int f = (int)(g - L.o_b2);
+            if (f < L.H) v = a.b2[f];
+        } else if (g < L.o_b3) {  // W3 [NCH][phase-major: KSH][tiles][64][4]
+            const int64_t r0 = g - L.o_w3;
+            const int c = (int)(r0 / L.w3_chunk);
+            int64_t r = r0 - (int64_t)c * L.w3_chunk;
+            // phases 0 (W, TGK groups), 1 (H, TGK), 2 (D, TGD), each [KSH][groups][64][4]
+            const int64_t s0 = (int64_t)L.KSH * L.TGK * 256;
+            int ph = 0, ng = L.TGK, pbase = 0, nt = L.K;
+            if (r >= s0) {
+                r -= s0;
+                ph = 1;
+                pbase = L.K;
+                if (r >= s0) {
+                    r -= s0;
+                    ph = 2;
+                    ng = L.TGD;
+                    pbase = 2 * L.K;
+                    nt = L.K - 1;
+                }
+            }
+            (void)ph;
+            const int e = r & 3, lane = (r >> 2) & 63;
+            const int64_t blk = r >> 8;
+            const int tg = (int)(blk % ng), ks = (int)(blk / ng);
+            const int t = 4 * tg + e, j = 16 * c + (lane & 15), k = 4 * ks + (lane >> 4);
+            if (t < nt && j < L.n_up && k < L.H)
+                v = a.w4[((int64_t)j * L.P + pbase + t) * L.H + k];
+        } else if (g < L.o_b3 + (int64_t)L.n_up * L.P) {  // b3 as is
+            v = a.b4[g - L.o_b3];
+        }
+        a.out[g] = v;
+    }
 }
-extern "C" int nfk_fused_nsf(const float*, int64_t, const float*, const int32_t*, const int32_t*,
-                             int32_t, const int32_t*, const int32_t*, int32_t, int32_t, float*,
-                             int64_t, float*, int32_t, int64_t, int32_t, double, int32_t, int32_t*,
-                             nfk_stream_t) {
-    return nfk_set_error("nfk_fused_nsf: shape not supported");
+
+// ---------------------------------------------------------------------------
+// instantiation table: hidden tiles (H = 16*HT rounded) x bins
+bool shape_ok(int n_lo, int n_up, int H, int K) {
+    if (n_lo < 1 || n_up < 1 || n_lo + n_up > kMaxD || H < 1) return false;
+    const int HT = (H + 15) / 16;
+    bool ht = false, kk = false;
+#define CHK_HT(h) ht |= (HT == h);
+    NFK_FUSED_HT(CHK_HT)
+#undef CHK_HT
+#define CHK_K(h, k) kk |= (K == k);
+    NFK_FUSED_K(CHK_K, 0)
+#undef CHK_K
+    return ht && kk;
+}
+
+}  // namespace
+
+extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
+    return shape_ok(n_lo, n_up, hidden, K) ? 1 : 0;
+}
+
+extern "C" int64_t nfk_fused_nsf_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
+    if (!shape_ok(n_lo, n_up, hidden, K)) return 0;
+    return make_layout(n_lo, n_up, hidden, K).total;
+}
+
+extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float* w2, const float* b2,
+                                  const float* w4, const float* b4, int32_t n_lo, int32_t n_up,
+                                  int32_t hidden, int32_t K, float* wpack, nfk_stream_t stream) {
+    if (!shape_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_pack: shape not supported");
+    if (!w0 || !b0 || !w2 || !b2 || !w4 || !b4 || !wpack)
+        return nfk_set_error("nfk_fused_nsf_pack: null pointer");
+    PackArgs a{w0, b0, w2, b2, w4, b4, wpack, make_layout(n_lo, n_up, hidden, K)};
+    int64_t g = (a.L.total + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
+                             const int32_t* up_out, int32_t n_up, const int32_t* lo_in,
+                             const int32_t* lo_out, int32_t n_lo, int32_t hidden, float* z,
+                             int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
+                             int32_t K, double tail_bound, int32_t inverse, int32_t* status,
+                             nfk_stream_t stream) {
+    if (!shape_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
+    if (batch < 0) return nfk_set_error("nfk_fused_nsf: bad batch");
+    if (batch == 0) return 0;
+    if (!x || !wpack || !up_in || !up_out || !lo_in || !lo_out || !z)
+        return nfk_set_error("nfk_fused_nsf: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf: null logdet");
+    const Layout L = make_layout(n_lo, n_up, hidden, K);
+    FusedArgs a;
+    a.x = x;
+    a.ldx = ldx;
+    a.w1 = wpack + L.o_w1;
+    a.b1 = wpack + L.o_b1;
+    a.w2 = wpack + L.o_w2;
+    a.b2 = wpack + L.o_b2;
+    a.w3 = wpack + L.o_w3;
+    a.b3 = wpack + L.o_b3;
+    a.w3_chunk = (int32_t)L.w3_chunk;
+    a.n_lo = n_lo;
+    a.n_up = n_up;
+    a.KS1 = L.KS1;
+    a.KSH = L.KSH;
+    a.NCH = L.NCH;
+    a.up_in = up_in;
+    a.up_out = up_out;
+    a.lo_in = lo_in;
+    a.lo_out = lo_out;
+    a.z = z;
+    a.ldz = ldz;
+    a.logdet = logdet;
+    a.mode = logdet_mode;
+    a.batch = batch;
+    a.status = status;
+    a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+    const int HT = L.HT;
+    hipStream_t st = (hipStream_t)stream;
+    const bool inv = inverse != 0;
+#define DISPATCH(h, k) \
+    if (HT == h && K == k) return launch_fused<h, k>(a, inv, st);
+#define DISPATCH_HT(h) NFK_FUSED_K(DISPATCH, h)
+    NFK_FUSED_HT(DISPATCH_HT)
+#undef DISPATCH_HT
+#undef DISPATCH
+    return nfk_set_error("nfk_fused_nsf: no kernel instance");
 }

@@ -22,4 +22,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     > "$OUT/prof.log" 2>&1; rc=$?
 echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"; fatal $rc rocprof
 find "$OUT/prof" -name "*stats*" | head
+if [ -n "${EXTRA_BENCH:-}" ]; then
+  timeout -k 10 300 python bench.py $EXTRA_BENCH > "$OUT/bench_extra.json" 2> "$OUT/bench_extra.err"; rc=$?
+  echo "bench_extra rc=$rc"; cat "$OUT/bench_extra.json"; fatal $rc bench_extra
+fi
 exit 0
