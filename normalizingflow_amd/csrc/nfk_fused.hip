@@ -24,7 +24,9 @@
 //
 // Weights are packed once per weight version (nfk_fused_nsf_pack) in MFMA
 // fragment order, 4 tiles per float4, so every A fragment is one coalesced
-// 16-B load that feeds 4 x ST MFMAs.  The x tile and the output z tile are
+// 16-B load that feeds 4 x ST MFMAs; a register ring keeps kPF k-steps of
+// weights in flight.  The hidden k-step count is a template parameter, so the
+// whole chain is branch-free straight-line code the scheduler can pipeline.  The x tile and the output z tile are
 // staged through a per-wave LDS region so HBM sees only full-row accesses.
 #include <hip/hip_runtime.h>
 
@@ -43,7 +45,7 @@ using namespace nfk_fused;
 
 namespace nfk_fused {
 #define NFK_X(h) NFK_FUSED_K(NFK_FUSED_EXTERN, h)
-NFK_FUSED_HT(NFK_X)
+NFK_FUSED_KSH(NFK_X)
 #undef NFK_X
 }  // namespace nfk_fused
 
@@ -55,6 +57,7 @@ struct PackArgs {
     Layout L;
 };
 
+// one thread per packed float; the layout is described at make_layout()
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     const Layout& L = a.L;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < L.total;
@@ -80,52 +83,51 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
         } else if (g < L.o_w3) {  // b2 padded
             const int f = (int)(g - L.o_b2);
             if (f < L.H) v = a.b2[f];
-        } else if (g < L.o_b3) {  // W3 [NCH][phase-major: KSH][tiles][64][4]
+        } else if (g < L.o_b3) {  // W3 [NCH][phases W,H,D: KSH][groups][64][4]
             const int64_t r0 = g - L.o_w3;
             const int c = (int)(r0 / L.w3_chunk);
             int64_t r = r0 - (int64_t)c * L.w3_chunk;
-            // phases 0 (W, TGK groups), 1 (H, TGK), 2 (D, TGD), each [KSH][groups][64][4]
             const int64_t s0 = (int64_t)L.KSH * L.TGK * 256;
-            int ph = 0, ng = L.TGK, pbase = 0, nt = L.K;
+            int ng = L.TGK, pbase = 0, nt = L.K;
             if (r >= s0) {
                 r -= s0;
-                ph = 1;
                 pbase = L.K;
                 if (r >= s0) {
                     r -= s0;
-                    ph = 2;
                     ng = L.TGD;
                     pbase = 2 * L.K;
                     nt = L.K - 1;
                 }
             }
-            (void)ph;
             const int e = r & 3, lane = (r >> 2) & 63;
             const int64_t blk = r >> 8;
             const int tg = (int)(blk % ng), ks = (int)(blk / ng);
             const int t = 4 * tg + e, j = 16 * c + (lane & 15), k = 4 * ks + (lane >> 4);
             if (t < nt && j < L.n_up && k < L.H)
                 v = a.w4[((int64_t)j * L.P + pbase + t) * L.H + k];
-        } else if (g < L.o_b3 + (int64_t)L.n_up * L.P) {  // b3 as is
-            v = a.b4[g - L.o_b3];
+        } else {  // b3 [NCH][P][64][4]: lane l, register r of tile p = coordinate 16c + 4(l>>4) + r
+            const int64_t r0 = g - L.o_b3;
+            const int c = (int)(r0 / L.b3_chunk);
+            const int64_t r = r0 - (int64_t)c * L.b3_chunk;
+            const int reg = r & 3, lane = (r >> 2) & 63, p = (int)(r >> 8);
+            const int j = 16 * c + 4 * (lane >> 4) + reg;
+            if (j < L.n_up) v = a.b4[(int64_t)j * L.P + p];
         }
         a.out[g] = v;
     }
 }
 
-// ---------------------------------------------------------------------------
-// instantiation table: hidden tiles (H = 16*HT rounded) x bins
 bool shape_ok(int n_lo, int n_up, int H, int K) {
     if (n_lo < 1 || n_up < 1 || n_lo + n_up > kMaxD || H < 1) return false;
-    const int HT = (H + 15) / 16;
-    bool ht = false, kk = false;
-#define CHK_HT(h) ht |= (HT == h);
-    NFK_FUSED_HT(CHK_HT)
-#undef CHK_HT
+    const int KSH = (H + 3) / 4;
+    bool ks = false, kk = false;
+#define CHK_KSH(h) ks |= (KSH == h);
+    NFK_FUSED_KSH(CHK_KSH)
+#undef CHK_KSH
 #define CHK_K(h, k) kk |= (K == k);
     NFK_FUSED_K(CHK_K, 0)
 #undef CHK_K
-    return ht && kk;
+    return ks && kk;
 }
 
 }  // namespace
@@ -168,38 +170,38 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     const Layout L = make_layout(n_lo, n_up, hidden, K);
     FusedArgs a;
     a.x = x;
-    a.ldx = ldx;
     a.w1 = wpack + L.o_w1;
     a.b1 = wpack + L.o_b1;
     a.w2 = wpack + L.o_w2;
     a.b2 = wpack + L.o_b2;
     a.w3 = wpack + L.o_w3;
     a.b3 = wpack + L.o_b3;
-    a.w3_chunk = (int32_t)L.w3_chunk;
-    a.n_lo = n_lo;
-    a.n_up = n_up;
-    a.KS1 = L.KS1;
-    a.KSH = L.KSH;
-    a.NCH = L.NCH;
     a.up_in = up_in;
     a.up_out = up_out;
     a.lo_in = lo_in;
     a.lo_out = lo_out;
     a.z = z;
-    a.ldz = ldz;
     a.logdet = logdet;
-    a.mode = logdet_mode;
-    a.batch = batch;
     a.status = status;
+    a.ldx = ldx;
+    a.ldz = ldz;
+    a.batch = batch;
+    a.w3_chunk = (int32_t)L.w3_chunk;
+    a.b3_chunk = (int32_t)L.b3_chunk;
+    a.n_lo = n_lo;
+    a.n_up = n_up;
+    a.KS1 = L.KS1;
+    a.NCH = L.NCH;
+    a.mode = logdet_mode;
     a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
-    const int HT = L.HT;
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
+    const int KSH = L.KSH;
 #define DISPATCH(h, k) \
-    if (HT == h && K == k) return launch_fused<h, k>(a, inv, st);
-#define DISPATCH_HT(h) NFK_FUSED_K(DISPATCH, h)
-    NFK_FUSED_HT(DISPATCH_HT)
-#undef DISPATCH_HT
+    if (KSH == h && K == k) return launch_fused<h, k>(a, inv, st);
+#define DISPATCH_KSH(h) NFK_FUSED_K(DISPATCH, h)
+    NFK_FUSED_KSH(DISPATCH_KSH)
+#undef DISPATCH_KSH
 #undef DISPATCH
     return nfk_set_error("nfk_fused_nsf: no kernel instance");
 }

@@ -7,10 +7,6 @@
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
 
-int nfk_set_error(const char* msg);
-NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, double top,
-                              int tails, double min_w, double min_h, double min_d);
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace nfk_fused {
@@ -20,13 +16,16 @@ constexpr int kWaves = 4;  // waves per workgroup
 #define NFK_FUSED_ST 1
 #endif
 constexpr int kST = NFK_FUSED_ST;  // 16-sample tiles per wave
-constexpr int kMaxD = 256; // n_lo + n_up staged in LDS
+constexpr int kMaxD = 256;         // n_lo + n_up staged in LDS
+constexpr int kPF = 4;             // weight prefetch distance (k-steps)
 
 struct Layout {  // packed-weight layout, all offsets in floats
     int n_lo, n_up, H, K, P, HT, KS1, KSH, NCH, TGH, TGK, TGD;
-    int64_t o_w1, o_b1, o_w2, o_b2, o_w3, o_b3, total, w3_chunk;
+    int64_t o_w1, o_b1, o_w2, o_b2, o_w3, o_b3, total, w3_chunk, b3_chunk;
 };
 
+// W1 [KS1][TGH][64][4] | b1 [HT*16] | W2 [KSH][TGH][64][4] | b2 [HT*16] |
+// W3 [NCH][phase W,H,D][KSH][groups][64][4] | b3 [NCH][P][64][4]
 inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     Layout L;
     L.n_lo = n_lo;
@@ -53,9 +52,9 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     L.w3_chunk = (int64_t)L.KSH * (2 * L.TGK + L.TGD) * 256;
     L.o_w3 = o;
     o += L.NCH * L.w3_chunk;
+    L.b3_chunk = (int64_t)L.P * 256;
     L.o_b3 = o;
-    o += (int64_t)n_up * L.P;
-    o = (o + 3) & ~(int64_t)3;
+    o += L.NCH * L.b3_chunk;
     L.total = o;
     return L;
 }
@@ -71,8 +70,8 @@ struct FusedArgs {
     float* logdet;
     int32_t* status;
     int64_t ldx, ldz, batch;
-    int32_t w3_chunk;  // floats per coordinate chunk of W3
-    int32_t n_lo, n_up, KS1, KSH, NCH, mode;
+    int32_t w3_chunk, b3_chunk;  // floats per coordinate chunk
+    int32_t n_lo, n_up, KS1, NCH, mode;
     NfkSplineConst c;
 };
 
@@ -80,55 +79,72 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// One output phase: NT parameter tiles (first `pbase`) for one chunk.
-// acc[st][t] accumulates rows = coordinates jbase + i, cols = samples.
-template <int HT, int NT, int NG, int ST>
-__device__ __forceinline__ void phase_gemm(const f32x4 (&h2)[ST][HT], const float4* __restrict__ wp,
-                                           const float* __restrict__ b3, int P, int pbase,
-                                           int jbase, int n_up, int KSH, int lane,
-                                           f32x4 (&acc)[ST][NT]) {
-    const int q = lane >> 4;
+__device__ __forceinline__ float pick4(const float4& w, int e) {
+    return e == 0 ? w.x : e == 1 ? w.y : e == 2 ? w.z : w.w;
+}
+
+// acc[st][t] += W[tile t] . act^T over KS k-steps; A fragments streamed from
+// the packed weights (4 tiles per float4, NG groups per k-step) with a
+// register ring kPF k-steps deep; B fragment of k-step ks = act[st][ks>>2][ks&3].
+template <int KS, int NT, int NG, int ST, int HTA>
+__device__ __forceinline__ void gemm_stream(const f32x4 (&act)[ST][HTA], const float4* __restrict__ wp,
+                                            int lane, f32x4 (&acc)[ST][NT]) {
+    constexpr int PF = KS < kPF ? KS : kPF;
+    float4 ring[PF][NG];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        f32x4 bv;
+    for (int p = 0; p < PF; ++p)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int j = jbase + 4 * q + r;
-            bv[r] = (j < n_up) ? b3[j * P + pbase + t] : 0.0f;
+        for (int g = 0; g < NG; ++g) ring[p][g] = wp[(p * NG + g) * 64 + lane];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        float4 cur[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) cur[g] = ring[ks % PF][g];
+        if (ks + PF < KS) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) ring[ks % PF][g] = wp[((ks + PF) * NG + g) * 64 + lane];
         }
+        // keep the prefetch of k-step ks+PF ahead of k-step ks's MFMAs (the
+        // scheduler otherwise sinks the loads next to their use)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int st = 0; st < ST; ++st) acc[st][t] = bv;
-    }
+        for (int g = 0; g < NG; ++g) {
 #pragma unroll
-    for (int ks = 0; ks < 4 * HT; ++ks) {
-        if (ks < KSH) {
-            float4 w[NG];
+            for (int e = 0; e < 4; ++e) {
+                const int t = 4 * g + e;
+                if (t < NT) {
+                    const float av = pick4(cur[g], e);
 #pragma unroll
-            for (int g = 0; g < NG; ++g) w[g] = wp[(ks * NG + g) * 64 + lane];
-#pragma unroll
-            for (int g = 0; g < NG; ++g) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int t = 4 * g + e;
-                    if (t < NT) {
-                        const float a = e == 0 ? w[g].x : e == 1 ? w[g].y : e == 2 ? w[g].z : w[g].w;
-#pragma unroll
-                        for (int st = 0; st < ST; ++st)
-                            acc[st][t] = mfma(a, h2[st][ks >> 2][ks & 3], acc[st][t]);
-                    }
+                    for (int st = 0; st < ST; ++st) acc[st][t] = mfma(av, act[st][ks >> 2][ks & 3], acc[st][t]);
                 }
             }
         }
     }
 }
 
-template <int HT, int K, bool INV, int ST>
+// bias-initialised accumulators of NT parameter tiles (packed b3: one float4 per tile)
+template <int NT, int ST>
+__device__ __forceinline__ void bias_init(const float4* __restrict__ bp, int lane, f32x4 (&acc)[ST][NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const float4 b = bp[t * 64 + lane];
+        f32x4 v;
+        v[0] = b.x;
+        v[1] = b.y;
+        v[2] = b.z;
+        v[3] = b.w;
+#pragma unroll
+        for (int st = 0; st < ST; ++st) acc[st][t] = v;
+    }
+}
+
+template <int KSH, int K, bool INV, int ST>
 __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
+    constexpr int HT = (KSH + 3) / 4;
     constexpr int TGH = (HT + 3) / 4;
     constexpr int TGK = (K + 3) / 4;
     constexpr int TGD = (K - 1 + 3) / 4;
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
-    constexpr int P = 3 * K - 1;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int q = lane >> 4, sl = lane & 15;
     const int D = a.n_lo + a.n_up;
@@ -171,9 +187,8 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
                 for (int e = 0; e < 4; ++e) {
                     const int t = 4 * g + e;
                     if (t < HT) {
-                        const float av = e == 0 ? w.x : e == 1 ? w.y : e == 2 ? w.z : w.w;
 #pragma unroll
-                        for (int st = 0; st < ST; ++st) h1[st][t] = mfma(av, bf[st], h1[st][t]);
+                        for (int st = 0; st < ST; ++st) h1[st][t] = mfma(pick4(w, e), bf[st], h1[st][t]);
                     }
                 }
             }
@@ -196,28 +211,7 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
         for (int st = 0; st < ST; ++st) h2[st][t] = bv;
     }
-    {
-        const float4* wp = reinterpret_cast<const float4*>(a.w2);
-#pragma unroll
-        for (int ks = 0; ks < 4 * HT; ++ks) {
-            if (ks < a.KSH) {
-#pragma unroll
-                for (int g = 0; g < TGH; ++g) {
-                    const float4 w = wp[(ks * TGH + g) * 64 + lane];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int t = 4 * g + e;
-                        if (t < HT) {
-                            const float av = e == 0 ? w.x : e == 1 ? w.y : e == 2 ? w.z : w.w;
-#pragma unroll
-                            for (int st = 0; st < ST; ++st)
-                                h2[st][t] = mfma(av, h1[st][ks >> 2][ks & 3], h2[st][t]);
-                        }
-                    }
-                }
-            }
-        }
-    }
+    gemm_stream<KSH, HT, TGH, ST, HT>(h1, reinterpret_cast<const float4*>(a.w2), lane, h2);
 #pragma unroll
     for (int st = 0; st < ST; ++st)
 #pragma unroll
@@ -225,9 +219,8 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) h2[st][t][r] = tanhf(h2[st][t][r]);
 
-    // ---- output layer + spline, chunk by chunk
+    // ---- output layer + spline, chunk by chunk of 16 coordinates
     const NfkSplineConst& c = a.c;
-    const float* b3 = a.b3;
     float ldsum[ST];
 #pragma unroll
     for (int st = 0; st < ST; ++st) ldsum[st] = 0.0f;
@@ -237,16 +230,17 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
         const int jbase = 16 * ch;
         const float4* w3 = reinterpret_cast<const float4*>(a.w3 + (int64_t)ch * a.w3_chunk);
         const float4* wW = w3;
-        const float4* wH = w3 + a.KSH * TGK * 64;
-        const float4* wD = w3 + 2 * a.KSH * TGK * 64;
+        const float4* wH = w3 + KSH * TGK * 64;
+        const float4* wD = w3 + 2 * KSH * TGK * 64;
+        const float4* b3 = reinterpret_cast<const float4*>(a.b3 + (int64_t)ch * a.b3_chunk);
         int kb[ST][4];
         float e0[ST][4], e1[ST][4], e2[ST][4], e3[ST][4];  // (cw_k, w_k, ch_k, h_k)
 
         // phase 1: the searched knots (widths forward, heights inverse)
         {
             f32x4 acc[ST][K];
-            phase_gemm<HT, K, TGK, ST>(h2, INV ? wH : wW, b3, P, INV ? K : 0, jbase, a.n_up,
-                                       a.KSH, lane, acc);
+            bias_init<K, ST>(b3 + (INV ? K : 0) * 64, lane, acc);
+            gemm_stream<KSH, K, TGK, ST, HT>(h2, INV ? wH : wW, lane, acc);
 #pragma unroll
             for (int st = 0; st < ST; ++st) {
 #pragma unroll
@@ -285,8 +279,8 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
         // phase 2: the other knots, selected at the bin found above
         {
             f32x4 acc[ST][K];
-            phase_gemm<HT, K, TGK, ST>(h2, INV ? wW : wH, b3, P, INV ? 0 : K, jbase, a.n_up,
-                                       a.KSH, lane, acc);
+            bias_init<K, ST>(b3 + (INV ? 0 : K) * 64, lane, acc);
+            gemm_stream<KSH, K, TGK, ST, HT>(h2, INV ? wW : wH, lane, acc);
 #pragma unroll
             for (int st = 0; st < ST; ++st) {
 #pragma unroll
@@ -322,7 +316,8 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
         // phase 3: derivative logits -> the two derivatives of the bin -> evaluate
         {
             f32x4 acc[ST][DN];
-            phase_gemm<HT, DN, TGD, ST>(h2, wD, b3, P, 2 * K, jbase, a.n_up, a.KSH, lane, acc);
+            bias_init<DN, ST>(b3 + 2 * K * 64, lane, acc);
+            gemm_stream<KSH, DN, TGD, ST, HT>(h2, wD, lane, acc);
 #pragma unroll
             for (int st = 0; st < ST; ++st) {
 #pragma unroll
@@ -422,7 +417,7 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
     }
 }
 
-template <int HT, int K>
+template <int KSH, int K>
 int launch_fused(const FusedArgs& a, bool inv, hipStream_t st) {
     const int D = a.n_lo + a.n_up;
     const size_t lds = (size_t)kWaves * (kST * 16) * (2 * D + 1) * sizeof(float);
@@ -430,29 +425,25 @@ int launch_fused(const FusedArgs& a, bool inv, hipStream_t st) {
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
     if (inv)
-        hipLaunchKernelGGL((k_fused_nsf<HT, K, true, kST>), dim3((unsigned)blocks), dim3(64 * kWaves),
+        hipLaunchKernelGGL((k_fused_nsf<KSH, K, true, kST>), dim3((unsigned)blocks), dim3(64 * kWaves),
                            lds, st, a);
     else
-        hipLaunchKernelGGL((k_fused_nsf<HT, K, false, kST>), dim3((unsigned)blocks),
+        hipLaunchKernelGGL((k_fused_nsf<KSH, K, false, kST>), dim3((unsigned)blocks),
                            dim3(64 * kWaves), lds, st, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 
-// explicit instantiation: definitions live in nfk_fused_ht<HT>.hip (one TU per
-// hidden-tile count so make -j compiles them in parallel); nfk_fused.hip sees
-// only the extern declarations.
-#define NFK_FUSED_INSTANCE(HT, K) \
-    template int launch_fused<HT, K>(const FusedArgs& a, bool inv, hipStream_t st);
-#define NFK_FUSED_EXTERN(HT, K) \
-    extern template int launch_fused<HT, K>(const FusedArgs& a, bool inv, hipStream_t st);
+// explicit instantiation: definitions live in nfk_fused_ksh<KSH>.hip (one TU
+// per hidden k-step count so make -j compiles them in parallel); nfk_fused.hip
+// sees only the extern declarations.
+#define NFK_FUSED_INSTANCE(KSH, K) \
+    template int launch_fused<KSH, K>(const FusedArgs& a, bool inv, hipStream_t st);
+#define NFK_FUSED_EXTERN(KSH, K) \
+    extern template int launch_fused<KSH, K>(const FusedArgs& a, bool inv, hipStream_t st);
 
-#ifdef NFK_FUSED_DEV
-#define NFK_FUSED_HT(X) X(7)
-#define NFK_FUSED_K(X, HT) X(HT, 8)
-#else
-#define NFK_FUSED_HT(X) X(1) X(2) X(4) X(7) X(8)
-#define NFK_FUSED_K(X, HT) X(HT, 4) X(HT, 5) X(HT, 6) X(HT, 8) X(HT, 10)
-#endif
+// supported hidden sizes: KSH = ceil(H/4) k-steps of 4 (H = 12, 16, 32, 64, 100, 128)
+#define NFK_FUSED_KSH(X) X(3) X(4) X(8) X(16) X(25) X(32)
+#define NFK_FUSED_K(X, KSH) X(KSH, 4) X(KSH, 5) X(KSH, 6) X(KSH, 8) X(KSH, 10)
 
 }  // namespace nfk_fused
