@@ -11,12 +11,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace nfk_fused {
 
-constexpr int kWaves = 4;  // waves per workgroup
-#ifndef NFK_FUSED_ST
-#define NFK_FUSED_ST 1
-#endif
-constexpr int kST = NFK_FUSED_ST;  // 16-sample tiles per wave
-constexpr int kMaxD = 256;         // n_lo + n_up staged in LDS
+constexpr int kWaves = 8;  // waves per workgroup: two per SIMD, ping-pong pairs (w, w+4)
+constexpr int kMaxD = 256; // n_lo + n_up staged in LDS (8 waves x 16 rows x (2D+1) floats)
 constexpr int kPF = 4;             // weight prefetch distance (k-steps)
 
 struct Layout {  // packed-weight layout, all offsets in floats
@@ -83,18 +79,26 @@ __device__ __forceinline__ float pick4(const float4& w, int e) {
     return e == 0 ? w.x : e == 1 ? w.y : e == 2 ? w.z : w.w;
 }
 
-// acc[st][t] += W[tile t] . act^T over KS k-steps; A fragments streamed from
-// the packed weights (4 tiles per float4, NG groups per k-step) with a
-// register ring kPF k-steps deep; B fragment of k-step ks = act[st][ks>>2][ks&3].
-template <int KS, int NT, int NG, int ST, int HTA>
-__device__ __forceinline__ void gemm_stream(const f32x4 (&act)[ST][HTA], const float4* __restrict__ wp,
-                                            int lane, f32x4 (&acc)[ST][NT]) {
+// ---------------------------------------------------------------------------
+// weight streaming: A fragments of KS k-steps (NG float4 groups = 4 tiles
+// each per k-step) flow through a register ring kPF k-steps deep.
+// ring_fill issues the first k-steps (called one segment ahead, so the loads
+// land while the wave runs VALU work); gemm_ring consumes the ring and keeps
+// it topped up.  B fragment of k-step ks = act[ks>>2][ks&3].
+template <int KS, int NG, int NGR>
+__device__ __forceinline__ void ring_fill(const float4* __restrict__ wp, int lane,
+                                          float4 (&ring)[kPF][NGR]) {
     constexpr int PF = KS < kPF ? KS : kPF;
-    float4 ring[PF][NG];
 #pragma unroll
     for (int p = 0; p < PF; ++p)
 #pragma unroll
         for (int g = 0; g < NG; ++g) ring[p][g] = wp[(p * NG + g) * 64 + lane];
+}
+
+template <int KS, int NT, int NG, int NGR, int HTA>
+__device__ __forceinline__ void gemm_ring(const f32x4 (&act)[HTA], const float4* __restrict__ wp,
+                                          int lane, float4 (&ring)[kPF][NGR], f32x4 (&acc)[NT]) {
+    constexpr int PF = KS < kPF ? KS : kPF;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
         float4 cur[NG];
@@ -104,7 +108,7 @@ __device__ __forceinline__ void gemm_stream(const f32x4 (&act)[ST][HTA], const f
 #pragma unroll
             for (int g = 0; g < NG; ++g) ring[ks % PF][g] = wp[((ks + PF) * NG + g) * 64 + lane];
         }
-        // keep the prefetch of k-step ks+PF ahead of k-step ks's MFMAs (the
+        // keep the refill of k-step ks+PF ahead of k-step ks's MFMAs (the
         // scheduler otherwise sinks the loads next to their use)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -112,299 +116,279 @@ __device__ __forceinline__ void gemm_stream(const f32x4 (&act)[ST][HTA], const f
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int t = 4 * g + e;
-                if (t < NT) {
-                    const float av = pick4(cur[g], e);
-#pragma unroll
-                    for (int st = 0; st < ST; ++st) acc[st][t] = mfma(av, act[st][ks >> 2][ks & 3], acc[st][t]);
-                }
+                if (t < NT) acc[t] = mfma(pick4(cur[g], e), act[ks >> 2][ks & 3], acc[t]);
             }
         }
     }
 }
 
-// bias-initialised accumulators of NT parameter tiles (packed b3: one float4 per tile)
-template <int NT, int ST>
-__device__ __forceinline__ void bias_init(const float4* __restrict__ bp, int lane, f32x4 (&acc)[ST][NT]) {
+template <int NT>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+// acc += packed bias (one float4 per tile and lane), at the start of a VALU segment
+template <int NT>
+__device__ __forceinline__ void add_bias(const float4* __restrict__ bp, int lane, f32x4 (&acc)[NT]) {
+    float4 b[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[t] = bp[t * 64 + lane];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const float4 b = bp[t * 64 + lane];
-        f32x4 v;
-        v[0] = b.x;
-        v[1] = b.y;
-        v[2] = b.z;
-        v[3] = b.w;
-#pragma unroll
-        for (int st = 0; st < ST; ++st) acc[st][t] = v;
+        acc[t][0] = acc[t][0] + b[t].x;
+        acc[t][1] = acc[t][1] + b[t].y;
+        acc[t][2] = acc[t][2] + b[t].z;
+        acc[t][3] = acc[t][3] + b[t].w;
     }
 }
 
-template <int KSH, int K, bool INV, int ST>
-__global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
+// Knot phase epilogue: for the 4 coordinates of this lane, normalise the K
+// logits of register r (NSF_CL's 2B*softmax, then RQS's own softmax + floor +
+// cumsum), optionally search the bin of x, and keep (edge_k, size_k).
+template <int K, bool SEARCH, bool Y>
+__device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
+                                           const NfkSplineConst& c, int (&kb)[4], float (&ek)[4],
+                                           float (&sk)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float u[K], edge[K + 1];
+#pragma unroll
+        for (int t = 0; t < K; ++t) u[t] = acc[t][r];
+        nfk_softmax<K>(u);
+#pragma unroll
+        for (int t = 0; t < K; ++t) u[t] = c.scale2b * u[t];
+        if (Y)
+            nfk_knots<K>(u, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, edge);
+        else
+            nfk_knots<K>(u, c.lo, c.hi, c.span, c.min_w, c.fw, edge);
+        if (SEARCH) kb[r] = nfk_bin<K>(edge, xv[r], c.knot_eps);
+        const int k = kb[r];
+        float e = edge[0], w = edge[1] - edge[0];
+#pragma unroll
+        for (int jj = 1; jj < K; ++jj)
+            if (k == jj) {
+                e = edge[jj];
+                w = edge[jj + 1] - edge[jj];
+            }
+        ek[r] = e;
+        sk[r] = w;
+    }
+}
+
+// Ping-pong structure: a workgroup = 8 waves, two per SIMD; every wave owns 16
+// samples and runs the same sequence of segments, alternating MFMA-heavy
+// (a phase's GEMM) and VALU-heavy (that phase's spline epilogue) work,
+// separated by workgroup barriers.  Waves 4..7 run exactly one segment behind
+// waves 0..3, so on each SIMD one wave feeds the matrix pipe while its
+// partner runs VALU (the partner of wave w is w+4: MI355X_MICROARCH.md,
+// "split roles between SIMD partners by wave number >= 4").
+template <int KSH, int K, bool INV>
+__global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     constexpr int HT = (KSH + 3) / 4;
     constexpr int TGH = (HT + 3) / 4;
     constexpr int TGK = (K + 3) / 4;
     constexpr int TGD = (K - 1 + 3) / 4;
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool lag = wid >= kWaves / 2;
     const int q = lane >> 4, sl = lane & 15;
     const int D = a.n_lo + a.n_up;
     const int XS = D + 1;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* xt = lds + wid * (ST * 16) * (XS + D);
-    float* zt = xt + (ST * 16) * XS;
-    const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * (16 * ST);
+    float* xt = lds + wid * 16 * (XS + D);
+    float* zt = xt + 16 * XS;
+    const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
-    const int nrows = rem <= 0 ? 0 : (rem < 16 * ST ? (int)rem : 16 * ST);
+    const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
+    const NfkSplineConst& c = a.c;
 
     // ---- stage this wave's x rows (full-row coalesced loads)
-    for (int r = 0; r < 16 * ST; ++r)
-        for (int c = lane; c < D; c += 64)
-            xt[r * XS + c] = (r < nrows) ? a.x[(b0 + r) * a.ldx + c] : 0.0f;
+    for (int r = 0; r < 16; ++r)
+        for (int cc = lane; cc < D; cc += 64) xt[r * XS + cc] = (r < nrows) ? a.x[(b0 + r) * a.ldx + cc] : 0.0f;
     __syncthreads();
+    if (lag) __syncthreads();
 
-    // ---- layer 1: h1^T = tanh(W1 . lower^T + b1)
-    f32x4 h1[ST][HT];
+    // ==== M segment 0: hidden layers, then the first phase of chunk 0
+    f32x4 h1[HT];
 #pragma unroll
     for (int t = 0; t < HT; ++t) {
-        f32x4 bv;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = a.b1[16 * t + 4 * r + q];
-#pragma unroll
-        for (int st = 0; st < ST; ++st) h1[st][t] = bv;
+        for (int r = 0; r < 4; ++r) h1[t][r] = a.b1[16 * t + 4 * r + q];
     }
     {
         const float4* wp = reinterpret_cast<const float4*>(a.w1);
         for (int ks = 0; ks < a.KS1; ++ks) {
             const int k = 4 * ks + q;
             const int col = (k < a.n_lo) ? a.lo_in[k] : -1;
-            float bf[ST];
-#pragma unroll
-            for (int st = 0; st < ST; ++st) bf[st] = (col >= 0) ? xt[(st * 16 + sl) * XS + col] : 0.0f;
+            const float bf = (col >= 0) ? xt[sl * XS + col] : 0.0f;
 #pragma unroll
             for (int g = 0; g < TGH; ++g) {
                 const float4 w = wp[(ks * TGH + g) * 64 + lane];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int t = 4 * g + e;
-                    if (t < HT) {
-#pragma unroll
-                        for (int st = 0; st < ST; ++st) h1[st][t] = mfma(pick4(w, e), bf[st], h1[st][t]);
-                    }
+                    if (t < HT) h1[t] = mfma(pick4(w, e), bf, h1[t]);
                 }
             }
         }
     }
 #pragma unroll
-    for (int st = 0; st < ST; ++st)
+    for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) h1[st][t][r] = tanhf(h1[st][t][r]);
-
-    // ---- layer 2: h2^T = tanh(W2 . h1^T + b2); register r of tile t = k-step 4t+r
-    f32x4 h2[ST][HT];
+        for (int r = 0; r < 4; ++r) h1[t][r] = tanhf(h1[t][r]);
+    f32x4 h2[HT];
 #pragma unroll
     for (int t = 0; t < HT; ++t) {
-        f32x4 bv;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = a.b2[16 * t + 4 * r + q];
-#pragma unroll
-        for (int st = 0; st < ST; ++st) h2[st][t] = bv;
+        for (int r = 0; r < 4; ++r) h2[t][r] = a.b2[16 * t + 4 * r + q];
     }
-    gemm_stream<KSH, HT, TGH, ST, HT>(h1, reinterpret_cast<const float4*>(a.w2), lane, h2);
+    {
+        float4 ring2[kPF][TGH];
+        ring_fill<KSH, TGH, TGH>(reinterpret_cast<const float4*>(a.w2), lane, ring2);
+        gemm_ring<KSH, HT, TGH, TGH, HT>(h1, reinterpret_cast<const float4*>(a.w2), lane, ring2, h2);
+    }
 #pragma unroll
-    for (int st = 0; st < ST; ++st)
+    for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) h2[st][t][r] = tanhf(h2[st][t][r]);
+        for (int r = 0; r < 4; ++r) h2[t][r] = tanhf(h2[t][r]);
 
-    // ---- output layer + spline, chunk by chunk of 16 coordinates
-    const NfkSplineConst& c = a.c;
-    float ldsum[ST];
-#pragma unroll
-    for (int st = 0; st < ST; ++st) ldsum[st] = 0.0f;
+    const int w3_phase = KSH * TGK * 64;  // float4s per W/H phase
+    float4 ring[kPF][TGK];
+    {
+        const float4* w3 = reinterpret_cast<const float4*>(a.w3);
+        ring_fill<KSH, TGK, TGK>(INV ? w3 + w3_phase : w3, lane, ring);
+    }
+
+    float ldsum = 0.0f;
     bool any_in = false, any_nd = false;
-
     for (int ch = 0; ch < a.NCH; ++ch) {
         const int jbase = 16 * ch;
         const float4* w3 = reinterpret_cast<const float4*>(a.w3 + (int64_t)ch * a.w3_chunk);
         const float4* wW = w3;
-        const float4* wH = w3 + KSH * TGK * 64;
-        const float4* wD = w3 + 2 * KSH * TGK * 64;
+        const float4* wH = w3 + w3_phase;
+        const float4* wD = w3 + 2 * w3_phase;
         const float4* b3 = reinterpret_cast<const float4*>(a.b3 + (int64_t)ch * a.b3_chunk);
-        int kb[ST][4];
-        float e0[ST][4], e1[ST][4], e2[ST][4], e3[ST][4];  // (cw_k, w_k, ch_k, h_k)
+        int jj4[4];
+        float xv[4];
+        int kb[4];
+        float cw_k[4], w_k[4], ch_k[4], h_k[4];
 
-        // phase 1: the searched knots (widths forward, heights inverse)
-        {
-            f32x4 acc[ST][K];
-            bias_init<K, ST>(b3 + (INV ? K : 0) * 64, lane, acc);
-            gemm_stream<KSH, K, TGK, ST, HT>(h2, INV ? wH : wW, lane, acc);
+        // ---- M: searched knots' GEMM (widths forward / heights inverse)
+        f32x4 acc[K];
+        zero_acc<K>(acc);
+        gemm_ring<KSH, K, TGK, TGK, HT>(h2, INV ? wH : wW, lane, ring, acc);
+        ring_fill<KSH, TGK, TGK>(INV ? wW : wH, lane, ring);
+        __syncthreads();
+        // ---- V: bin search
+        add_bias<K>(b3 + (INV ? K : 0) * 64, lane, acc);
 #pragma unroll
-            for (int st = 0; st < ST; ++st) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int j = jbase + 4 * q + r;
-                    const float xv = (j < a.n_up) ? xt[(st * 16 + sl) * XS + a.up_in[j]] : 0.0f;
-                    float u[K], edge[K + 1];
-#pragma unroll
-                    for (int t = 0; t < K; ++t) u[t] = acc[st][t][r];
-                    nfk_softmax<K>(u);
-#pragma unroll
-                    for (int t = 0; t < K; ++t) u[t] = c.scale2b * u[t];
-                    if (INV)
-                        nfk_knots<K>(u, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, edge);
-                    else
-                        nfk_knots<K>(u, c.lo, c.hi, c.span, c.min_w, c.fw, edge);
-                    const int k = nfk_bin<K>(edge, xv, c.knot_eps);
-                    float ek = edge[0], sk = edge[1] - edge[0];
-#pragma unroll
-                    for (int jj = 1; jj < K; ++jj)
-                        if (k == jj) {
-                            ek = edge[jj];
-                            sk = edge[jj + 1] - edge[jj];
-                        }
-                    kb[st][r] = k;
-                    if (INV) {
-                        e2[st][r] = ek;
-                        e3[st][r] = sk;
-                    } else {
-                        e0[st][r] = ek;
-                        e1[st][r] = sk;
-                    }
-                }
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int j = jbase + 4 * q + r;
+            jj4[r] = j;
+            xv[r] = (j < a.n_up) ? xt[sl * XS + a.up_in[j]] : 0.0f;
         }
-        // phase 2: the other knots, selected at the bin found above
-        {
-            f32x4 acc[ST][K];
-            bias_init<K, ST>(b3 + (INV ? 0 : K) * 64, lane, acc);
-            gemm_stream<KSH, K, TGK, ST, HT>(h2, INV ? wW : wH, lane, acc);
-#pragma unroll
-            for (int st = 0; st < ST; ++st) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float u[K], edge[K + 1];
-#pragma unroll
-                    for (int t = 0; t < K; ++t) u[t] = acc[st][t][r];
-                    nfk_softmax<K>(u);
-#pragma unroll
-                    for (int t = 0; t < K; ++t) u[t] = c.scale2b * u[t];
-                    if (INV)
-                        nfk_knots<K>(u, c.lo, c.hi, c.span, c.min_w, c.fw, edge);
-                    else
-                        nfk_knots<K>(u, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, edge);
-                    const int k = kb[st][r];
-                    float ek = edge[0], sk = edge[1] - edge[0];
-#pragma unroll
-                    for (int jj = 1; jj < K; ++jj)
-                        if (k == jj) {
-                            ek = edge[jj];
-                            sk = edge[jj + 1] - edge[jj];
-                        }
-                    if (INV) {
-                        e0[st][r] = ek;
-                        e1[st][r] = sk;
-                    } else {
-                        e2[st][r] = ek;
-                        e3[st][r] = sk;
-                    }
-                }
-            }
+        if (INV)
+            knot_phase<K, true, true>(acc, xv, c, kb, ch_k, h_k);
+        else
+            knot_phase<K, true, false>(acc, xv, c, kb, cw_k, w_k);
+        __syncthreads();
+
+        // ---- M: the other knots' GEMM
+        zero_acc<K>(acc);
+        gemm_ring<KSH, K, TGK, TGK, HT>(h2, INV ? wW : wH, lane, ring, acc);
+        ring_fill<KSH, TGD, TGK>(wD, lane, ring);
+        __syncthreads();
+        // ---- V: select the other knots at the bin
+        add_bias<K>(b3 + (INV ? 0 : K) * 64, lane, acc);
+        if (INV)
+            knot_phase<K, false, false>(acc, xv, c, kb, cw_k, w_k);
+        else
+            knot_phase<K, false, true>(acc, xv, c, kb, ch_k, h_k);
+        __syncthreads();
+
+        // ---- M: derivative logits' GEMM
+        f32x4 accd[DN];
+        zero_acc<DN>(accd);
+        gemm_ring<KSH, DN, TGD, TGK, HT>(h2, wD, lane, ring, accd);
+        if (ch + 1 < a.NCH) {
+            const float4* nx = reinterpret_cast<const float4*>(a.w3 + (int64_t)(ch + 1) * a.w3_chunk);
+            ring_fill<KSH, TGK, TGK>(INV ? nx + w3_phase : nx, lane, ring);
         }
-        // phase 3: derivative logits -> the two derivatives of the bin -> evaluate
-        {
-            f32x4 acc[ST][DN];
-            bias_init<DN, ST>(b3 + 2 * K * 64, lane, acc);
-            gemm_stream<KSH, DN, TGD, ST, HT>(h2, wD, lane, acc);
+        __syncthreads();
+        // ---- V: derivatives of the bin, evaluate the spline, log|det|
+        add_bias<DN>(b3 + 2 * K * 64, lane, accd);
 #pragma unroll
-            for (int st = 0; st < ST; ++st) {
+        for (int r = 0; r < 4; ++r) {
+            const int k = kb[r];
+            float raw_k = 0.0f, raw_k1 = 0.0f;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int j = jbase + 4 * q + r;
-                    const bool valid = j < a.n_up;
-                    const int row = st * 16 + sl;
-                    const float xv = valid ? xt[row * XS + a.up_in[j]] : 0.0f;
-                    const int k = kb[st][r];
-                    float raw_k = 0.0f, raw_k1 = 0.0f;
-#pragma unroll
-                    for (int t = 0; t < K - 1; ++t) {
-                        if (k == t + 1) raw_k = acc[st][t][r];
-                        if (k == t) raw_k1 = acc[st][t][r];
-                    }
-                    raw_k = nfk_softplus(raw_k);  // NSF_CL's D <- softplus(D)
-                    raw_k1 = nfk_softplus(raw_k1);
-                    raw_k = (k == 0) ? c.dpad : raw_k;
-                    raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
-                    const float d_k = c.min_d + nfk_softplus(raw_k);
-                    const float d_k1 = c.min_d + nfk_softplus(raw_k1);
-                    const float cw_k = e0[st][r], w_k = e1[st][r];
-                    const float ch_k = e2[st][r], h_k = e3[st][r];
-                    const float delta = h_k / w_k;
-                    const float gap = (d_k + d_k1) - 2.0f * delta;
-                    float out, th;
-                    bool nd = false;
-                    if (INV) {
-                        const float y = xv - ch_k;
-                        const float qa = y * gap + h_k * (delta - d_k);
-                        const float qb = h_k * d_k - y * gap;
-                        const float qc = (-delta) * y;
-                        const float disc = qb * qb - (4.0f * qa) * qc;
-                        nd = !(disc >= 0.0f);
-                        const float root = (2.0f * qc) / (-qb - sqrtf(disc));
-                        out = root * w_k + cw_k;
-                        th = root;
-                    } else {
-                        th = (xv - cw_k) / w_k;
-                    }
-                    const float t1mt = th * (1.0f - th);
-                    const float den = delta + gap * t1mt;
-                    if (!INV) {
-                        const float num = h_k * (delta * (th * th) + d_k * t1mt);
-                        out = ch_k + num / den;
-                    }
-                    const float omt = 1.0f - th;
-                    const float dnum = (delta * delta) *
-                                       ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
-                    float lad = logf(dnum) - 2.0f * logf(den);
-                    lad = INV ? -lad : lad;
-                    const bool inside = (xv >= c.lo) && (xv <= c.hi);
-                    if (!inside) {
-                        out = xv;
-                        lad = 0.0f;
-                        nd = false;
-                    }
-                    if (valid) {
-                        zt[row * D + a.up_out[j]] = out;
-                        if (row < nrows) {
-                            ldsum[st] += lad;
-                            any_in |= inside;
-                            any_nd |= nd;
-                        }
-                    }
-                }
+            for (int t = 0; t < K - 1; ++t) {
+                if (k == t + 1) raw_k = accd[t][r];
+                if (k == t) raw_k1 = accd[t][r];
             }
+            raw_k = nfk_softplus(raw_k);  // NSF_CL's D <- softplus(D)
+            raw_k1 = nfk_softplus(raw_k1);
+            raw_k = (k == 0) ? c.dpad : raw_k;
+            raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
+            const float d_k = c.min_d + nfk_softplus(raw_k);
+            const float d_k1 = c.min_d + nfk_softplus(raw_k1);
+            const float x = xv[r];
+            const float delta = h_k[r] / w_k[r];
+            const float gap = (d_k + d_k1) - 2.0f * delta;
+            float out, th;
+            bool nd = false;
+            if (INV) {
+                const float y = x - ch_k[r];
+                const float qa = y * gap + h_k[r] * (delta - d_k);
+                const float qb = h_k[r] * d_k - y * gap;
+                const float qc = (-delta) * y;
+                const float disc = qb * qb - (4.0f * qa) * qc;
+                nd = !(disc >= 0.0f);
+                const float root = (2.0f * qc) / (-qb - sqrtf(disc));
+                out = root * w_k[r] + cw_k[r];
+                th = root;
+            } else {
+                th = (x - cw_k[r]) / w_k[r];
+            }
+            const float t1mt = th * (1.0f - th);
+            const float den = delta + gap * t1mt;
+            if (!INV) {
+                const float num = h_k[r] * (delta * (th * th) + d_k * t1mt);
+                out = ch_k[r] + num / den;
+            }
+            const float omt = 1.0f - th;
+            const float dnum = (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+            float lad = logf(dnum) - 2.0f * logf(den);
+            lad = INV ? -lad : lad;
+            const bool inside = (x >= c.lo) && (x <= c.hi);
+            const bool valid = jj4[r] < a.n_up;
+            out = inside ? out : x;
+            lad = (inside && valid && sl < nrows) ? lad : 0.0f;
+            if (valid) zt[sl * D + a.up_out[jj4[r]]] = out;
+            ldsum += lad;
+            any_in |= inside && valid && sl < nrows;
+            any_nd |= nd && inside && valid && sl < nrows;
         }
+        __syncthreads();
     }
+    if (!lag) __syncthreads();
 
-    // ---- identity-copied coordinates, then full-row stores of z
-    for (int i = lane; i < 16 * ST * a.n_lo; i += 64) {
+    // ---- identity-copied coordinates, per-sample log|det|, full-row stores of z
+    for (int i = lane; i < 16 * a.n_lo; i += 64) {
         const int row = i / a.n_lo, qq = i - row * a.n_lo;
         zt[row * D + a.lo_out[qq]] = xt[row * XS + a.lo_in[qq]];
     }
-#pragma unroll
-    for (int st = 0; st < ST; ++st) {
-        float v = ldsum[st];
+    {
+        float v = ldsum;
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        const int row = st * 16 + sl;
-        if (q == 0 && row < nrows && a.mode != 0) {
-            float* dst = a.logdet + b0 + row;
+        if (q == 0 && sl < nrows && a.mode != 0) {
+            float* dst = a.logdet + b0 + sl;
             *dst = (a.mode == 2) ? (*dst + v) : v;
         }
     }
-    __syncthreads();
     for (int r = 0; r < nrows; ++r)
         for (int cc = lane; cc < D; cc += 64) a.z[(b0 + r) * a.ldz + cc] = zt[r * D + cc];
 
@@ -420,16 +404,16 @@ __global__ __launch_bounds__(256, 2) void k_fused_nsf(FusedArgs a) {
 template <int KSH, int K>
 int launch_fused(const FusedArgs& a, bool inv, hipStream_t st) {
     const int D = a.n_lo + a.n_up;
-    const size_t lds = (size_t)kWaves * (kST * 16) * (2 * D + 1) * sizeof(float);
-    const int64_t per_block = (int64_t)kWaves * 16 * kST;
+    const size_t lds = (size_t)kWaves * 16 * (2 * D + 1) * sizeof(float);
+    const int64_t per_block = (int64_t)kWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
     if (inv)
-        hipLaunchKernelGGL((k_fused_nsf<KSH, K, true, kST>), dim3((unsigned)blocks), dim3(64 * kWaves),
-                           lds, st, a);
+        hipLaunchKernelGGL((k_fused_nsf<KSH, K, true>), dim3((unsigned)blocks), dim3(64 * kWaves), lds,
+                           st, a);
     else
-        hipLaunchKernelGGL((k_fused_nsf<KSH, K, false, kST>), dim3((unsigned)blocks),
-                           dim3(64 * kWaves), lds, st, a);
+        hipLaunchKernelGGL((k_fused_nsf<KSH, K, false>), dim3((unsigned)blocks), dim3(64 * kWaves),
+                           lds, st, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
