@@ -33,18 +33,65 @@ __device__ __forceinline__ float nfk_softplus(float v) {
     return v > 20.0f ? v : log1pf(expf(v));
 }
 
+// ---------------------------------------------------------------------------
+// Short-sequence transcendentals for the fused kernel's epilogue, where fp32
+// MFMA and VALU share one datapath and every VALU instruction costs MFMA time.
+// exp: 2^(x*log2e) with the product's rounding error carried (hi/lo split of
+//      log2e + exact fma residual) and folded back with one fma: ~1-2 ulp.
+// rcp/div: v_rcp_f32 + one Newton step (+ residual correction for a/b):
+//      correctly rounded except in rare near-tie cases.
+// log: v_log_f32 (log2) times ln2 split hi/lo.
+// No special-value handling: inputs are finite by construction here.
+__device__ __forceinline__ float nfk_exp_fast(float x) {
+    const float L2E = 1.44269502e+00f, L2E_LO = 1.92596299e-08f;  // log2(e) = L2E + L2E_LO
+    const float t = x * L2E;
+    const float r = __builtin_fmaf(x, L2E_LO, __builtin_fmaf(x, L2E, -t));
+    const float e = __builtin_amdgcn_exp2f(t);
+    return __builtin_fmaf(e, r * 0.693147182f, e);
+}
+
+__device__ __forceinline__ float nfk_rcp_fast(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(r, __builtin_fmaf(-b, r, 1.0f), r);
+}
+
+__device__ __forceinline__ float nfk_div_fast(float a, float b) {
+    const float r = nfk_rcp_fast(b);
+    const float q = a * r;
+    return __builtin_fmaf(r, __builtin_fmaf(-b, q, a), q);
+}
+
+__device__ __forceinline__ float nfk_log_fast(float x) {
+    const float LN2 = 6.93147182e-01f, LN2_LO = -1.90465421e-09f;
+    const float l2 = __builtin_amdgcn_logf(x);
+    return __builtin_fmaf(l2, LN2_LO, l2 * LN2);
+}
+
+__device__ __forceinline__ float nfk_softplus_fast(float v) {
+    return v > 20.0f ? v : nfk_log_fast(1.0f + nfk_exp_fast(v));
+}
+
+template <bool FAST>
+__device__ __forceinline__ float nfk_exp(float x) { return FAST ? nfk_exp_fast(x) : expf(x); }
+template <bool FAST>
+__device__ __forceinline__ float nfk_log(float x) { return FAST ? nfk_log_fast(x) : logf(x); }
+template <bool FAST>
+__device__ __forceinline__ float nfk_div(float a, float b) { return FAST ? nfk_div_fast(a, b) : a / b; }
+template <bool FAST>
+__device__ __forceinline__ float nfk_splus(float v) { return FAST ? nfk_softplus_fast(v) : nfk_softplus(v); }
+
 // softmax over K logits, in place (K compile-time so the arrays stay in VGPRs).
 // Summation order of ATen's CPU kernel (vec::reduce_all, AVX-512 build the
 // golden vectors come from): sequential for K < 16; for K >= 16 the K values
 // are folded onto 16 lanes (lane i += x[i + 16m]) and reduced by the
 // xor-8/4/2/1 butterfly.  Output = e * (1/sum).
-template <int K>
+template <int K, bool FAST = false>
 __device__ __forceinline__ void nfk_softmax(float (&u)[K]) {
     float m = u[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) m = fmaxf(m, u[i]);
 #pragma unroll
-    for (int i = 0; i < K; ++i) u[i] = expf(u[i] - m);
+    for (int i = 0; i < K; ++i) u[i] = nfk_exp<FAST>(u[i] - m);
     float s;
     if constexpr (K < 16) {
         s = 0.0f;
@@ -66,17 +113,17 @@ __device__ __forceinline__ void nfk_softmax(float (&u)[K]) {
         for (int i = 0; i < 2; ++i) v[i] = v[i] + v[i + 2];
         s = v[0] + v[1];
     }
-    const float r = 1.0f / s;
+    const float r = FAST ? nfk_rcp_fast(s) : 1.0f / s;
 #pragma unroll
     for (int i = 0; i < K; ++i) u[i] = u[i] * r;
 }
 
 // Knot positions from unnormalised logits (utils.py:73-80 / 84-91):
 // edge[0..K]; edge[0] = lo, edge[K] = hi pinned.
-template <int K>
+template <int K, bool FAST = false>
 __device__ __forceinline__ void nfk_knots(float (&u)[K], float lo, float hi, float span,
                                           float min_b, float fb, float (&edge)[K + 1]) {
-    nfk_softmax<K>(u);
+    nfk_softmax<K, FAST>(u);
     double acc = 0.0;
     edge[0] = lo;
 #pragma unroll
