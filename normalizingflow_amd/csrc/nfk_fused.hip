@@ -57,68 +57,60 @@ struct PackArgs {
     Layout L;
 };
 
-// one thread per packed float; the layout is described at make_layout()
+// One thread per packed float (layout described at make_layout()).
+__device__ float pack_hidden(const float* W, const float* bias, int KS, int kin, int H, int TGH, int HT,
+                             int blk, int lane, int e) {
+    if (blk < KS * TGH) {
+        const int ks = blk / TGH, g = blk - ks * TGH, t = 4 * g + e;
+        const int f = hid_row(t, lane & 15), k = 4 * ks + (lane >> 4);
+        return (t < HT && f < H && k < kin) ? W[(int64_t)f * kin + k] : 0.0f;
+    }
+    const int t = blk - KS * TGH, f = 16 * t + 4 * e + (lane >> 4);  // bias: register e of tile t
+    return f < H ? bias[f] : 0.0f;
+}
+
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     const Layout& L = a.L;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < L.total;
          g += (int64_t)gridDim.x * blockDim.x) {
-        float v = 0.0f;
-        if (g < L.o_b1) {  // W1 [KS1][TGH][64][4]
-            const int64_t r = g - L.o_w1;
-            const int e = r & 3, lane = (r >> 2) & 63;
-            const int64_t blk = r >> 8;
-            const int tg = (int)(blk % L.TGH), ks = (int)(blk / L.TGH);
-            const int t = 4 * tg + e, f = hid_row(t, lane & 15), k = 4 * ks + (lane >> 4);
-            if (t < L.HT && f < L.H && k < L.n_lo) v = a.w0[(int64_t)f * L.n_lo + k];
-        } else if (g < L.o_w2) {  // b1 padded
-            const int f = (int)(g - L.o_b1);
-            if (f < L.H) v = a.b0[f];
-        } else if (g < L.o_b2) {  // W2 [KSH][TGH][64][4]
-            const int64_t r = g - L.o_w2;
-            const int e = r & 3, lane = (r >> 2) & 63;
-            const int64_t blk = r >> 8;
-            const int tg = (int)(blk % L.TGH), ks = (int)(blk / L.TGH);
-            const int t = 4 * tg + e, f = hid_row(t, lane & 15), k = 4 * ks + (lane >> 4);
-            if (t < L.HT && f < L.H && k < L.H) v = a.w2[(int64_t)f * L.H + k];
-        } else if (g < L.o_w3) {  // b2 padded
-            const int f = (int)(g - L.o_b2);
-            if (f < L.H) v = a.b2[f];
-        } else if (g < L.o_b3) {  // W3 [NCH][phases W,H,D: KSH][groups][64][4]
-            const int64_t r0 = g - L.o_w3;
-            const int c = (int)(r0 / L.w3_chunk);
-            int64_t r = r0 - (int64_t)c * L.w3_chunk;
-            const int64_t s0 = (int64_t)L.KSH * L.TGK * 256;
-            int ng = L.TGK, pbase = 0, nt = L.K;
-            if (r >= s0) {
-                r -= s0;
+        const int e = (int)(g & 3), lane = (int)((g >> 2) & 63);
+        float v;
+        if (g < L.o_h2) {
+            v = pack_hidden(a.w0, a.b0, L.KS1, L.n_lo, L.H, L.TGH, L.HT, (int)(g >> 8), lane, e);
+        } else if (g < L.o_w3) {
+            v = pack_hidden(a.w2, a.b2, L.KSH, L.H, L.H, L.TGH, L.HT, (int)((g - L.o_h2) >> 8), lane, e);
+        } else {
+            const int64_t bl = (g - L.o_w3) >> 8;
+            const int c = (int)(bl / L.blk_chunk);
+            int b = (int)(bl - (int64_t)c * L.blk_chunk);
+            int ng = L.TGK, nt = L.K, pbase = 0;
+            if (b >= L.blk_w) {
+                b -= L.blk_w;
                 pbase = L.K;
-                if (r >= s0) {
-                    r -= s0;
-                    ng = L.TGD;
+                if (b >= L.blk_w) {
+                    b -= L.blk_w;
                     pbase = 2 * L.K;
+                    ng = L.TGD;
                     nt = L.K - 1;
                 }
             }
-            const int e = r & 3, lane = (r >> 2) & 63;
-            const int64_t blk = r >> 8;
-            const int tg = (int)(blk % ng), ks = (int)(blk / ng);
-            const int t = 4 * tg + e, j = 16 * c + (lane & 15), k = 4 * ks + (lane >> 4);
-            if (t < nt && j < L.n_up && k < L.H)
-                v = a.w4[((int64_t)j * L.P + pbase + t) * L.H + k];
-        } else {  // b3 [NCH][P][64][4]: lane l, register r of tile p = coordinate 16c + 4(l>>4) + r
-            const int64_t r0 = g - L.o_b3;
-            const int c = (int)(r0 / L.b3_chunk);
-            const int64_t r = r0 - (int64_t)c * L.b3_chunk;
-            const int reg = r & 3, lane = (r >> 2) & 63, p = (int)(r >> 8);
-            const int j = 16 * c + 4 * (lane >> 4) + reg;
-            if (j < L.n_up) v = a.b4[(int64_t)j * L.P + p];
+            v = 0.0f;
+            if (b < L.KSH * ng) {
+                const int ks = b / ng, gg = b - ks * ng, t = 4 * gg + e;
+                const int j = 16 * c + (lane & 15), k = 4 * ks + (lane >> 4);
+                if (t < nt && j < L.n_up && k < L.H) v = a.w4[((int64_t)j * L.P + pbase + t) * L.H + k];
+            } else {
+                const int t = b - L.KSH * ng, j = 16 * c + 4 * (lane >> 4) + e;
+                if (t < nt && j < L.n_up) v = a.b4[(int64_t)j * L.P + pbase + t];
+            }
         }
         a.out[g] = v;
     }
 }
 
 bool shape_ok(int n_lo, int n_up, int H, int K) {
-    if (n_lo < 1 || n_up < 1 || n_lo + n_up > kMaxD || H < 1) return false;
+    if (n_lo < 1 || n_up < 1 || n_lo + n_up > kMaxD || H < 1 || K < 2) return false;
+    if (lds_bytes(make_layout(n_lo, n_up, H, K)) > (size_t)kLdsBytes) return false;
     const int KSH = (H + 3) / 4;
     bool ks = false, kk = false;
 #define CHK_KSH(h) ks |= (KSH == h);
@@ -170,12 +162,7 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     const Layout L = make_layout(n_lo, n_up, hidden, K);
     FusedArgs a;
     a.x = x;
-    a.w1 = wpack + L.o_w1;
-    a.b1 = wpack + L.o_b1;
-    a.w2 = wpack + L.o_w2;
-    a.b2 = wpack + L.o_b2;
-    a.w3 = wpack + L.o_w3;
-    a.b3 = wpack + L.o_b3;
+    a.pack = wpack;
     a.up_in = up_in;
     a.up_out = up_out;
     a.lo_in = lo_in;
@@ -186,19 +173,26 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     a.ldx = ldx;
     a.ldz = ldz;
     a.batch = batch;
-    a.w3_chunk = (int32_t)L.w3_chunk;
-    a.b3_chunk = (int32_t)L.b3_chunk;
     a.n_lo = n_lo;
     a.n_up = n_up;
     a.KS1 = L.KS1;
     a.NCH = L.NCH;
     a.mode = logdet_mode;
+    a.slot_blocks = L.slot_blocks;
+    a.blk_h1 = L.blk_h1;
+    a.blk_h2 = L.blk_h2;
+    a.blk_w = L.blk_w;
+    a.blk_d = L.blk_d;
+    a.blk_chunk = L.blk_chunk;
+    a.o_h2 = (int32_t)L.o_h2;
+    a.o_w3 = (int32_t)L.o_w3;
     a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+    const size_t lds = lds_bytes(L);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
     const int KSH = L.KSH;
 #define DISPATCH(h, k) \
-    if (KSH == h && K == k) return launch_fused<h, k>(a, inv, st);
+    if (KSH == h && K == k) return launch_fused<h, k>(a, lds, inv, st);
 #define DISPATCH_KSH(h) NFK_FUSED_K(DISPATCH, h)
     NFK_FUSED_KSH(DISPATCH_KSH)
 #undef DISPATCH_KSH

@@ -11,17 +11,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace nfk_fused {
 
-constexpr int kWaves = 4;  // waves per workgroup (one per SIMD; two workgroups per CU)
-constexpr int kMaxD = 256; // n_lo + n_up staged in LDS (4 waves x 16 rows x (2D+1) floats)
-constexpr int kPF = 2;             // weight prefetch distance (k-steps)
+constexpr int kWaves = 8;         // waves per workgroup (two per SIMD), 16 samples each
+constexpr int kMaxD = 128;        // n_lo + n_up staged in LDS
+constexpr int kLdsBytes = 160 * 1024;
 
-struct Layout {  // packed-weight layout, all offsets in floats
+// Packed weights: a stream of "phase records", each a run of 1-KiB blocks
+// (64 lanes x float4) in MFMA fragment order: the weight blocks of the
+// phase's KS k-steps x NG tile groups ([ks][g], 4 tiles per float4), then NT
+// bias blocks (lane l, register r of tile t = bias of the row that lane holds).
+//   hidden 1: KS1*TGH + HT blocks      hidden 2: KSH*TGH + HT blocks
+//   per 16-coordinate chunk: W logits KSH*TGK + K, H logits KSH*TGK + K,
+//                            D logits KSH*TGD + (K-1)
+// The workgroup copies one record at a time into an LDS slot with
+// global_load_lds (one wave-instruction per block), double-buffered.
+struct Layout {
     int n_lo, n_up, H, K, P, HT, KS1, KSH, NCH, TGH, TGK, TGD;
-    int64_t o_w1, o_b1, o_w2, o_b2, o_w3, o_b3, total, w3_chunk, b3_chunk;
+    int blk_h1, blk_h2, blk_w, blk_d, blk_chunk, slot_blocks;
+    int64_t o_h1, o_h2, o_w3, total;  // offsets / size in floats
 };
 
-// W1 [KS1][TGH][64][4] | b1 [HT*16] | W2 [KSH][TGH][64][4] | b2 [HT*16] |
-// W3 [NCH][phase W,H,D][KSH][groups][64][4] | b3 [NCH][P][64][4]
 inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     Layout L;
     L.n_lo = n_lo;
@@ -36,23 +44,27 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     L.TGH = (L.HT + 3) / 4;
     L.TGK = (K + 3) / 4;
     L.TGD = (K - 1 + 3) / 4;
-    int64_t o = 0;
-    L.o_w1 = o;
-    o += (int64_t)L.KS1 * L.TGH * 256;
-    L.o_b1 = o;
-    o += L.HT * 16;
-    L.o_w2 = o;
-    o += (int64_t)L.KSH * L.TGH * 256;
-    L.o_b2 = o;
-    o += L.HT * 16;
-    L.w3_chunk = (int64_t)L.KSH * (2 * L.TGK + L.TGD) * 256;
-    L.o_w3 = o;
-    o += L.NCH * L.w3_chunk;
-    L.b3_chunk = (int64_t)L.P * 256;
-    L.o_b3 = o;
-    o += L.NCH * L.b3_chunk;
-    L.total = o;
+    L.blk_h1 = L.KS1 * L.TGH + L.HT;
+    L.blk_h2 = L.KSH * L.TGH + L.HT;
+    L.blk_w = L.KSH * L.TGK + K;
+    L.blk_d = L.KSH * L.TGD + (K - 1);
+    L.blk_chunk = 2 * L.blk_w + L.blk_d;
+    L.slot_blocks = L.blk_h1;
+    if (L.blk_h2 > L.slot_blocks) L.slot_blocks = L.blk_h2;
+    if (L.blk_w > L.slot_blocks) L.slot_blocks = L.blk_w;
+    if (L.blk_d > L.slot_blocks) L.slot_blocks = L.blk_d;
+    L.o_h1 = 0;
+    L.o_h2 = (int64_t)L.blk_h1 * 256;
+    L.o_w3 = L.o_h2 + (int64_t)L.blk_h2 * 256;
+    L.total = L.o_w3 + (int64_t)L.NCH * L.blk_chunk * 256;
     return L;
+}
+
+// dynamic LDS bytes: two weight slots, the index maps, one x tile per wave
+inline size_t lds_bytes(const Layout& L) {
+    const int D = L.n_lo + L.n_up;
+    const size_t maps = ((size_t)(2 * D) * sizeof(int32_t) + 15) & ~(size_t)15;
+    return 2 * (size_t)L.slot_blocks * 1024 + maps + (size_t)kWaves * 16 * (D + 1) * sizeof(float);
 }
 
 // hidden feature held by MFMA row i (0..15) of tile t
@@ -60,14 +72,15 @@ __host__ __device__ inline int hid_row(int t, int i) { return 16 * t + 4 * (i & 
 
 struct FusedArgs {
     const float* x;
-    const float *w1, *b1, *w2, *b2, *w3, *b3;
+    const float* pack;
     const int32_t *up_in, *up_out, *lo_in, *lo_out;
     float* z;
     float* logdet;
     int32_t* status;
     int64_t ldx, ldz, batch;
-    int32_t w3_chunk, b3_chunk;  // floats per coordinate chunk
-    int32_t n_lo, n_up, KS1, NCH, mode;
+    int32_t n_lo, n_up, KS1, NCH, mode, slot_blocks;
+    int32_t blk_h1, blk_h2, blk_w, blk_d, blk_chunk;
+    int32_t o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
     NfkSplineConst c;
 };
 
@@ -79,67 +92,45 @@ __device__ __forceinline__ float pick4(const float4& w, int e) {
     return e == 0 ? w.x : e == 1 ? w.y : e == 2 ? w.z : w.w;
 }
 
-// ---------------------------------------------------------------------------
-// weight streaming: A fragments of KS k-steps (NG float4 groups = 4 tiles
-// each per k-step) flow through a register ring kPF k-steps deep.
-// ring_fill issues the first k-steps (called one segment ahead, so the loads
-// land while the wave runs VALU work); gemm_ring consumes the ring and keeps
-// it topped up.  B fragment of k-step ks = act[ks>>2][ks&3].
-template <int KS, int NG, int NGR>
-__device__ __forceinline__ void ring_fill(const float4* __restrict__ wp, int lane,
-                                          float4 (&ring)[kPF][NGR]) {
-    constexpr int PF = KS < kPF ? KS : kPF;
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) ring[p][g] = wp[(p * NG + g) * 64 + lane];
+__device__ __forceinline__ f32x4 as_f32x4(const float4& v) {
+    f32x4 r;
+    r[0] = v.x;
+    r[1] = v.y;
+    r[2] = v.z;
+    r[3] = v.w;
+    return r;
 }
 
-template <int KS, int NT, int NG, int NGR, int HTA>
-__device__ __forceinline__ void gemm_ring(const f32x4 (&act)[HTA], const float4* __restrict__ wp,
-                                          int lane, float4 (&ring)[kPF][NGR], f32x4 (&acc)[NT]) {
-    constexpr int PF = KS < kPF ? KS : kPF;
+// Copy one phase record (nblk 1-KiB blocks at src) into an LDS slot: block i
+// goes by wave i % kWaves as one global_load_lds_dwordx4 (LDS destination =
+// wave-uniform base + 16 B x lane).  Completion is waited for by the
+// workgroup barrier that precedes the slot's first read (vmcnt(0) + s_barrier).
+__device__ __forceinline__ void stage_record(const float* __restrict__ src, int nblk, float4* slot,
+                                             int wid, int lane) {
+    for (int i = wid; i < nblk; i += kWaves)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + (int64_t)i * 256 + lane * 4),
+            (__attribute__((address_space(3))) void*)(slot + i * 64), 16, 0, 0);
+}
+
+// acc[t] = bias + W[tile t] . act^T over KS k-steps, A fragments and bias from
+// an LDS slot; B fragment of k-step ks = act[ks>>2][ks&3].
+template <int KS, int NT, int NG, int HTA>
+__device__ __forceinline__ void gemm_lds(const f32x4 (&act)[HTA], const float4* slot, int lane,
+                                         f32x4 (&acc)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = as_f32x4(slot[(KS * NG + t) * 64 + lane]);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-        float4 cur[NG];
-#pragma unroll
-        for (int g = 0; g < NG; ++g) cur[g] = ring[ks % PF][g];
-        if (ks + PF < KS) {
-#pragma unroll
-            for (int g = 0; g < NG; ++g) ring[ks % PF][g] = wp[((ks + PF) * NG + g) * 64 + lane];
-        }
-        // keep the refill of k-step ks+PF ahead of k-step ks's MFMAs (the
-        // scheduler otherwise sinks the loads next to their use)
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
+            const float4 w = slot[(ks * NG + g) * 64 + lane];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int t = 4 * g + e;
-                if (t < NT) acc[t] = mfma(pick4(cur[g], e), act[ks >> 2][ks & 3], acc[t]);
+                if (t < NT) acc[t] = mfma(pick4(w, e), act[ks >> 2][ks & 3], acc[t]);
             }
         }
-    }
-}
-
-template <int NT>
-__device__ __forceinline__ void zero_acc(f32x4 (&acc)[NT]) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-}
-
-// acc += packed bias (one float4 per tile and lane), at the start of a VALU segment
-template <int NT>
-__device__ __forceinline__ void add_bias(const float4* __restrict__ bp, int lane, f32x4 (&acc)[NT]) {
-    float4 b[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) b[t] = bp[t * 64 + lane];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        acc[t][0] = acc[t][0] + b[t].x;
-        acc[t][1] = acc[t][1] + b[t].y;
-        acc[t][2] = acc[t][2] + b[t].z;
-        acc[t][3] = acc[t][3] + b[t].w;
     }
 }
 
@@ -173,20 +164,18 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
             }
         ek[r] = e;
         sk[r] = w;
-#ifdef NFK_PAIR_FENCE
-        __builtin_amdgcn_sched_barrier(0);  // one pair at a time: bounds live registers
-#endif
     }
 }
 
-// One wave = 16 samples, free-running (no inter-wave synchronisation after
-// the x tile is staged).  Measured on gfx950 (tools/ubench_coexec.hip): fp32
-// MFMA and VALU instructions of two waves on one SIMD do NOT co-execute (the
-// f32 MFMA runs at the vector datapath's rate), so layer time ~ MFMA cycles +
-// epilogue VALU cycles; the epilogue therefore uses the short-sequence
-// transcendentals of nfk_spline.h.
+// One workgroup = kWaves waves x 16 samples.  Phase records stream through
+// two LDS slots: while phase p computes from slot p&1, the record of phase
+// p+1 is already in the other slot and phase p+2's copy is issued right after
+// the barrier that ends phase p.  One barrier per phase; everything else is
+// wave-local.  (fp32 MFMA and VALU share the vector datapath on gfx950 --
+// tools/ubench_coexec.hip -- so the epilogue uses the short-sequence
+// transcendentals of nfk_spline.h.)
 template <int KSH, int K, bool INV>
-__global__ __launch_bounds__(64 * kWaves, 2) void k_fused_nsf(FusedArgs a) {
+__global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     constexpr int HT = (KSH + 3) / 4;
     constexpr int TGH = (HT + 3) / 4;
     constexpr int TGK = (K + 3) / 4;
@@ -197,35 +186,49 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_fused_nsf(FusedArgs a) {
     const int q = lane >> 4, sl = lane & 15;
     const int D = a.n_lo + a.n_up;
     const int XS = D + 1;
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* xt = lds + wid * 16 * (XS + D);
-    float* zt = xt + 16 * XS;
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    float4* slot0 = lds4;
+    float4* slot1 = lds4 + a.slot_blocks * 64;
+    int32_t* m_up_in = reinterpret_cast<int32_t*>(lds4 + 2 * a.slot_blocks * 64);
+    int32_t* m_up_out = m_up_in + a.n_up;
+    int32_t* m_lo_in = m_up_out + a.n_up;
+    int32_t* m_lo_out = m_lo_in + a.n_lo;
+    float* xt = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + ((2 * D + 3) / 4)) +
+                wid * 16 * XS;
     const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const NfkSplineConst& c = a.c;
+    const float* pk = a.pack;
 
-    // ---- stage this wave's x rows (full-row coalesced loads)
+    // ---- prologue: x rows, index maps, first two phase records
     for (int r = 0; r < 16; ++r)
         for (int cc = lane; cc < D; cc += 64) xt[r * XS + cc] = (r < nrows) ? a.x[(b0 + r) * a.ldx + cc] : 0.0f;
-    __syncthreads();
-
-    // ---- hidden layers
-    f32x4 h1[HT];
-#pragma unroll
-    for (int t = 0; t < HT; ++t) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h1[t][r] = a.b1[16 * t + 4 * r + q];
+    for (int i = threadIdx.x; i < a.n_up; i += 64 * kWaves) {
+        m_up_in[i] = a.up_in[i];
+        m_up_out[i] = a.up_out[i];
     }
+    for (int i = threadIdx.x; i < a.n_lo; i += 64 * kWaves) {
+        m_lo_in[i] = a.lo_in[i];
+        m_lo_out[i] = a.lo_out[i];
+    }
+    stage_record(pk, a.blk_h1, slot0, wid, lane);
+    __syncthreads();
+    stage_record(pk + a.o_h2, a.blk_h2, slot1, wid, lane);
+
+    // ---- layer 1 (slot 0): h1^T = tanh(W1 . lower^T + b1)
+    f32x4 h1[HT];
     {
-        const float4* wp = reinterpret_cast<const float4*>(a.w1);
+        const float4* s = slot0;
+#pragma unroll
+        for (int t = 0; t < HT; ++t) h1[t] = as_f32x4(s[(a.KS1 * TGH + t) * 64 + lane]);
         for (int ks = 0; ks < a.KS1; ++ks) {
             const int k = 4 * ks + q;
-            const int col = (k < a.n_lo) ? a.lo_in[k] : -1;
+            const int col = (k < a.n_lo) ? m_lo_in[k] : -1;
             const float bf = (col >= 0) ? xt[sl * XS + col] : 0.0f;
 #pragma unroll
             for (int g = 0; g < TGH; ++g) {
-                const float4 w = wp[(ks * TGH + g) * 64 + lane];
+                const float4 w = s[(ks * TGH + g) * 64 + lane];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int t = 4 * g + e;
@@ -238,161 +241,147 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_fused_nsf(FusedArgs a) {
     for (int t = 0; t < HT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) h1[t][r] = tanhf(h1[t][r]);
+    __syncthreads();  // slot 0 free, hidden-2 record landed
+    const float* w3 = pk + a.o_w3;
+    // execution order of the three records of a chunk: searched knots, other knots, derivatives
+    const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
+    stage_record(w3 + offA * 256, a.blk_w, slot0, wid, lane);
+
+    // ---- layer 2 (slot 1): h2^T = tanh(W2 . h1^T + b2); register r of tile t = k-step 4t+r
     f32x4 h2[HT];
-#pragma unroll
-    for (int t = 0; t < HT; ++t) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h2[t][r] = a.b2[16 * t + 4 * r + q];
-    }
-    {
-        float4 ring2[kPF][TGH];
-        ring_fill<KSH, TGH, TGH>(reinterpret_cast<const float4*>(a.w2), lane, ring2);
-        gemm_ring<KSH, HT, TGH, TGH, HT>(h1, reinterpret_cast<const float4*>(a.w2), lane, ring2, h2);
-    }
+    gemm_lds<KSH, HT, TGH, HT>(h1, slot1, lane, h2);
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) h2[t][r] = tanhf(h2[t][r]);
-
-    const int w3_phase = KSH * TGK * 64;  // float4s per W/H phase
-    float4 ring[kPF][TGK];
-    {
-        const float4* w3 = reinterpret_cast<const float4*>(a.w3);
-        ring_fill<KSH, TGK, TGK>(INV ? w3 + w3_phase : w3, lane, ring);
-    }
+    __syncthreads();  // slot 1 free, chunk-0 record A landed
+    stage_record(w3 + offB * 256, a.blk_w, slot1, wid, lane);
 
     float ldsum = 0.0f;
     bool any_in = false, any_nd = false;
+    float* zrow = a.z + (b0 + sl) * a.ldz;
+    // record A and C of a chunk use slot sA, record B slot sB; the next chunk's
+    // A is staged into sB once B is consumed, so the roles swap every chunk
+    float4* sA = slot0;
+    float4* sB = slot1;
+    const bool row_ok = sl < nrows;
     for (int ch = 0; ch < a.NCH; ++ch) {
         const int jbase = 16 * ch;
-        const float4* w3 = reinterpret_cast<const float4*>(a.w3 + (int64_t)ch * a.w3_chunk);
-        const float4* wW = w3;
-        const float4* wH = w3 + w3_phase;
-        const float4* wD = w3 + 2 * w3_phase;
-        const float4* b3 = reinterpret_cast<const float4*>(a.b3 + (int64_t)ch * a.b3_chunk);
+        const float* wc = w3 + (int64_t)ch * a.blk_chunk * 256;
+        const float* wn = wc + (int64_t)a.blk_chunk * 256;  // next chunk
         int jj4[4];
         float xv[4];
         int kb[4];
         float cw_k[4], w_k[4], ch_k[4], h_k[4];
-
-        // ---- searched knots' GEMM (widths forward / heights inverse)
-        f32x4 acc[K];
-        zero_acc<K>(acc);
-        gemm_ring<KSH, K, TGK, TGK, HT>(h2, INV ? wH : wW, lane, ring, acc);
-        ring_fill<KSH, TGK, TGK>(INV ? wW : wH, lane, ring);
-        __builtin_amdgcn_sched_barrier(0);  // phase fence: keeps register pressure per phase
-        // ---- bin search
-        add_bias<K>(b3 + (INV ? K : 0) * 64, lane, acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int j = jbase + 4 * q + r;
             jj4[r] = j;
-            xv[r] = (j < a.n_up) ? xt[sl * XS + a.up_in[j]] : 0.0f;
+            xv[r] = (j < a.n_up) ? xt[sl * XS + m_up_in[j]] : 0.0f;
         }
-        if (INV)
-            knot_phase<K, true, true>(acc, xv, c, kb, ch_k, h_k);
-        else
-            knot_phase<K, true, false>(acc, xv, c, kb, cw_k, w_k);
-        __builtin_amdgcn_sched_barrier(0);
 
-        // ---- the other knots' GEMM
-        zero_acc<K>(acc);
-        gemm_ring<KSH, K, TGK, TGK, HT>(h2, INV ? wW : wH, lane, ring, acc);
-        ring_fill<KSH, TGD, TGK>(wD, lane, ring);
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- select the other knots at the bin
-        add_bias<K>(b3 + (INV ? 0 : K) * 64, lane, acc);
-        if (INV)
-            knot_phase<K, false, false>(acc, xv, c, kb, cw_k, w_k);
-        else
-            knot_phase<K, false, true>(acc, xv, c, kb, ch_k, h_k);
-        __builtin_amdgcn_sched_barrier(0);
+        // ---- record A (slot sA): searched knots (widths forward / heights inverse)
+        {
+            f32x4 acc[K];
+            gemm_lds<KSH, K, TGK, HT>(h2, sA, lane, acc);
+            if (INV)
+                knot_phase<K, true, true>(acc, xv, c, kb, ch_k, h_k);
+            else
+                knot_phase<K, true, false>(acc, xv, c, kb, cw_k, w_k);
+        }
+        __syncthreads();
+        stage_record(wc + offC * 256, a.blk_d, sA, wid, lane);
 
-        // ---- derivative logits' GEMM
-        f32x4 accd[DN];
-        zero_acc<DN>(accd);
-        gemm_ring<KSH, DN, TGD, TGK, HT>(h2, wD, lane, ring, accd);
-        if (ch + 1 < a.NCH) {
-            const float4* nx = reinterpret_cast<const float4*>(a.w3 + (int64_t)(ch + 1) * a.w3_chunk);
-            ring_fill<KSH, TGK, TGK>(INV ? nx + w3_phase : nx, lane, ring);
+        // ---- record B (slot sB): the other knots, selected at the bin
+        {
+            f32x4 acc[K];
+            gemm_lds<KSH, K, TGK, HT>(h2, sB, lane, acc);
+            if (INV)
+                knot_phase<K, false, false>(acc, xv, c, kb, cw_k, w_k);
+            else
+                knot_phase<K, false, true>(acc, xv, c, kb, ch_k, h_k);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- derivatives of the bin, evaluate the spline, log|det|
-        add_bias<DN>(b3 + 2 * K * 64, lane, accd);
+        __syncthreads();
+        if (ch + 1 < a.NCH) stage_record(wn + offA * 256, a.blk_w, sB, wid, lane);
+
+        // ---- record C (slot sA): derivatives of the bin, evaluate, log|det|
+        {
+            f32x4 accd[DN];
+            gemm_lds<KSH, DN, TGD, HT>(h2, sA, lane, accd);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int k = kb[r];
-            float raw_k = 0.0f, raw_k1 = 0.0f;
+            for (int r = 0; r < 4; ++r) {
+                const int k = kb[r];
+                float raw_k = 0.0f, raw_k1 = 0.0f;
 #pragma unroll
-            for (int t = 0; t < K - 1; ++t) {
-                if (k == t + 1) raw_k = accd[t][r];
-                if (k == t) raw_k1 = accd[t][r];
+                for (int t = 0; t < K - 1; ++t) {
+                    if (k == t + 1) raw_k = accd[t][r];
+                    if (k == t) raw_k1 = accd[t][r];
+                }
+                raw_k = nfk_splus<true>(raw_k);  // NSF_CL's D <- softplus(D)
+                raw_k1 = nfk_splus<true>(raw_k1);
+                raw_k = (k == 0) ? c.dpad : raw_k;
+                raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
+                const float d_k = c.min_d + nfk_splus<true>(raw_k);
+                const float d_k1 = c.min_d + nfk_splus<true>(raw_k1);
+                const float x = xv[r];
+                const float delta = nfk_div<true>(h_k[r], w_k[r]);
+                const float gap = (d_k + d_k1) - 2.0f * delta;
+                float out, th;
+                bool nd = false;
+                if (INV) {
+                    const float y = x - ch_k[r];
+                    const float qa = y * gap + h_k[r] * (delta - d_k);
+                    const float qb = h_k[r] * d_k - y * gap;
+                    const float qc = (-delta) * y;
+                    const float disc = qb * qb - (4.0f * qa) * qc;
+                    nd = !(disc >= 0.0f);
+                    const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
+                    out = root * w_k[r] + cw_k[r];
+                    th = root;
+                } else {
+                    th = nfk_div<true>(x - cw_k[r], w_k[r]);
+                }
+                const float t1mt = th * (1.0f - th);
+                const float den = delta + gap * t1mt;
+                if (!INV) {
+                    const float num = h_k[r] * (delta * (th * th) + d_k * t1mt);
+                    out = ch_k[r] + nfk_div<true>(num, den);
+                }
+                const float omt = 1.0f - th;
+                const float dnum =
+                    (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+                float lad = nfk_log<true>(dnum) - 2.0f * nfk_log<true>(den);
+                lad = INV ? -lad : lad;
+                const bool inside = (x >= c.lo) && (x <= c.hi);
+                const bool live = jj4[r] < a.n_up && row_ok;
+                out = inside ? out : x;
+                if (live) zrow[m_up_out[jj4[r]]] = out;
+                ldsum += (inside && live) ? lad : 0.0f;
+                any_in |= inside && live;
+                any_nd |= nd && inside && live;
             }
-            raw_k = nfk_splus<true>(raw_k);  // NSF_CL's D <- softplus(D)
-            raw_k1 = nfk_splus<true>(raw_k1);
-            raw_k = (k == 0) ? c.dpad : raw_k;
-            raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
-            const float d_k = c.min_d + nfk_splus<true>(raw_k);
-            const float d_k1 = c.min_d + nfk_splus<true>(raw_k1);
-            const float x = xv[r];
-            const float delta = nfk_div<true>(h_k[r], w_k[r]);
-            const float gap = (d_k + d_k1) - 2.0f * delta;
-            float out, th;
-            bool nd = false;
-            if (INV) {
-                const float y = x - ch_k[r];
-                const float qa = y * gap + h_k[r] * (delta - d_k);
-                const float qb = h_k[r] * d_k - y * gap;
-                const float qc = (-delta) * y;
-                const float disc = qb * qb - (4.0f * qa) * qc;
-                nd = !(disc >= 0.0f);
-                const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
-                out = root * w_k[r] + cw_k[r];
-                th = root;
-            } else {
-                th = nfk_div<true>(x - cw_k[r], w_k[r]);
-            }
-            const float t1mt = th * (1.0f - th);
-            const float den = delta + gap * t1mt;
-            if (!INV) {
-                const float num = h_k[r] * (delta * (th * th) + d_k * t1mt);
-                out = ch_k[r] + nfk_div<true>(num, den);
-            }
-            const float omt = 1.0f - th;
-            const float dnum = (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
-            float lad = nfk_log<true>(dnum) - 2.0f * nfk_log<true>(den);
-            lad = INV ? -lad : lad;
-            const bool inside = (x >= c.lo) && (x <= c.hi);
-            const bool valid = jj4[r] < a.n_up;
-            out = inside ? out : x;
-            lad = (inside && valid && sl < nrows) ? lad : 0.0f;
-            if (valid) zt[sl * D + a.up_out[jj4[r]]] = out;
-            ldsum += lad;
-            any_in |= inside && valid && sl < nrows;
-            any_nd |= nd && inside && valid && sl < nrows;
-#ifdef NFK_PAIR_FENCE
-            __builtin_amdgcn_sched_barrier(0);
-#endif
         }
+        __syncthreads();
+        if (ch + 1 < a.NCH) stage_record(wn + offB * 256, a.blk_w, sA, wid, lane);
+        float4* t = sA;
+        sA = sB;
+        sB = t;
     }
 
-    // ---- identity-copied coordinates, per-sample log|det|, full-row stores of z
+    // ---- identity-copied coordinates, per-sample log|det|
     for (int i = lane; i < 16 * a.n_lo; i += 64) {
         const int row = i / a.n_lo, qq = i - row * a.n_lo;
-        zt[row * D + a.lo_out[qq]] = xt[row * XS + a.lo_in[qq]];
+        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xt[row * XS + m_lo_in[qq]];
     }
     {
         float v = ldsum;
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        if (q == 0 && sl < nrows && a.mode != 0) {
+        if (q == 0 && row_ok && a.mode != 0) {
             float* dst = a.logdet + b0 + sl;
             *dst = (a.mode == 2) ? (*dst + v) : v;
         }
     }
-    for (int r = 0; r < nrows; ++r)
-        for (int cc = lane; cc < D; cc += 64) a.z[(b0 + r) * a.ldz + cc] = zt[r * D + cc];
-
     if (a.status != nullptr) {
         const int bits = (__any(any_in) ? NFK_ST_INSIDE_SEEN : 0) | (__any(any_nd) ? NFK_ST_NEG_DISC : 0);
         if (lane == 0 && bits != 0) {
@@ -403,9 +392,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_fused_nsf(FusedArgs a) {
 }
 
 template <int KSH, int K>
-int launch_fused(const FusedArgs& a, bool inv, hipStream_t st) {
-    const int D = a.n_lo + a.n_up;
-    const size_t lds = (size_t)kWaves * 16 * (2 * D + 1) * sizeof(float);
+int launch_fused(const FusedArgs& a, size_t lds, bool inv, hipStream_t st) {
     const int64_t per_block = (int64_t)kWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
@@ -423,9 +410,9 @@ int launch_fused(const FusedArgs& a, bool inv, hipStream_t st) {
 // per hidden k-step count so make -j compiles them in parallel); nfk_fused.hip
 // sees only the extern declarations.
 #define NFK_FUSED_INSTANCE(KSH, K) \
-    template int launch_fused<KSH, K>(const FusedArgs& a, bool inv, hipStream_t st);
+    template int launch_fused<KSH, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
 #define NFK_FUSED_EXTERN(KSH, K) \
-    extern template int launch_fused<KSH, K>(const FusedArgs& a, bool inv, hipStream_t st);
+    extern template int launch_fused<KSH, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
 
 // supported hidden sizes: KSH = ceil(H/4) k-steps of 4 (H = 12, 16, 32, 64, 100, 128)
 #define NFK_FUSED_KSH(X) X(3) X(4) X(8) X(16) X(25) X(32)
