@@ -118,18 +118,30 @@ __device__ __forceinline__ void stage_record(const float* __restrict__ src, int 
 template <int KS, int NT, int NG, int HTA>
 __device__ __forceinline__ void gemm_lds(const f32x4 (&act)[HTA], const float4* slot, int lane,
                                          f32x4 (&acc)[NT]) {
+    float4 cur[NG], nxt[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) cur[g] = slot[g * 64 + lane];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = as_f32x4(slot[(KS * NG + t) * 64 + lane]);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+        // A fragments of k-step ks+1 are read while k-step ks's MFMAs run
+        if (ks + 1 < KS) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) nxt[g] = slot[((ks + 1) * NG + g) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
-            const float4 w = slot[(ks * NG + g) * 64 + lane];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int t = 4 * g + e;
-                if (t < NT) acc[t] = mfma(pick4(w, e), act[ks >> 2][ks & 3], acc[t]);
+                if (t < NT) acc[t] = mfma(pick4(cur[g], e), act[ks >> 2][ks & 3], acc[t]);
             }
+        }
+        if (ks + 1 < KS) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) cur[g] = nxt[g];
         }
     }
 }
