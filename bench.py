@@ -137,9 +137,10 @@ def load_traffic(kernel):
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get(kernel)
+            rec = json.load(f).get(kernel)
     except (OSError, ValueError):
         return None
+    return None if rec is None else rec.get("bytes_per_launch")
 
 
 def main():
