@@ -146,9 +146,12 @@ __device__ __forceinline__ void gemm_lds(const f32x4 (&act)[HTA], const float4* 
     }
 }
 
-// Knot phase epilogue: for the 4 coordinates of this lane, normalise the K
-// logits of register r (NSF_CL's 2B*softmax, then RQS's own softmax + floor +
-// cumsum), optionally search the bin of x, and keep (edge_k, size_k).
+// Knot phase epilogue: for the 4 coordinates of this lane, turn the K logits
+// of register r into knots (NSF_CL's 2B softmax, then RQS's softmax, floor and
+// cumsum: nfk_knots_nsf_lean) and keep (edge_k, size_k) of the bin.  The
+// searched phase finds the bin by a running select over the interior edges
+// (edges are strictly increasing, so the last edge <= x is the bin of
+// utils.py:20-25 for every x inside the tails); the other phase selects by k.
 template <int K, bool SEARCH, bool Y>
 __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
                                            const NfkSplineConst& c, int (&kb)[4], float (&ek)[4],
@@ -158,24 +161,22 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
         float u[K], edge[K + 1];
 #pragma unroll
         for (int t = 0; t < K; ++t) u[t] = acc[t][r];
-        nfk_softmax<K, true>(u);
-#pragma unroll
-        for (int t = 0; t < K; ++t) u[t] = c.scale2b * u[t];
         if (Y)
-            nfk_knots<K, true>(u, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, edge);
+            nfk_knots_nsf_lean<K>(u, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, c.m2b, edge);
         else
-            nfk_knots<K, true>(u, c.lo, c.hi, c.span, c.min_w, c.fw, edge);
-        if (SEARCH) kb[r] = nfk_bin<K>(edge, xv[r], c.knot_eps);
-        const int k = kb[r];
-        float e = edge[0], w = edge[1] - edge[0];
+            nfk_knots_nsf_lean<K>(u, c.lo, c.hi, c.span, c.min_w, c.fw, c.m2b, edge);
+        float e = edge[0], e1 = edge[1];
+        int k = 0;
 #pragma unroll
-        for (int jj = 1; jj < K; ++jj)
-            if (k == jj) {
-                e = edge[jj];
-                w = edge[jj + 1] - edge[jj];
-            }
+        for (int j = 1; j < K; ++j) {
+            const bool ge = SEARCH ? (xv[r] >= edge[j]) : (kb[r] >= j);
+            e = ge ? edge[j] : e;
+            e1 = ge ? edge[j + 1] : e1;
+            if (SEARCH) k += ge ? 1 : 0;
+        }
+        if (SEARCH) kb[r] = k;
         ek[r] = e;
-        sk[r] = w;
+        sk[r] = e1 - e;
     }
 }
 
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h1[t][r] = tanhf(h1[t][r]);
+        for (int r = 0; r < 4; ++r) h1[t][r] = nfk_tanh_lean(h1[t][r]);
     __syncthreads();  // slot 0 free, hidden-2 record landed
     const float* w3 = pk + a.o_w3;
     // execution order of the three records of a chunk: searched knots, other knots, derivatives
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h2[t][r] = tanhf(h2[t][r]);
+        for (int r = 0; r < 4; ++r) h2[t][r] = nfk_tanh_lean(h2[t][r]);
     __syncthreads();  // slot 1 free, chunk-0 record A landed
     stage_record(w3 + offB * 256, a.blk_w, slot1, wid, lane);
 
@@ -322,19 +323,22 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
             gemm_lds<KSH, DN, TGD, HT>(h2, sA, lane, accd);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
+                // padded derivative index j+1 holds logit j (utils.py:36-39):
+                // raw_k = logit k-1, raw_k1 = logit k, by running select on k >= j
                 const int k = kb[r];
-                float raw_k = 0.0f, raw_k1 = 0.0f;
+                float raw_k = accd[0][r], raw_k1 = accd[0][r];
 #pragma unroll
-                for (int t = 0; t < K - 1; ++t) {
-                    if (k == t + 1) raw_k = accd[t][r];
-                    if (k == t) raw_k1 = accd[t][r];
+                for (int j = 1; j < K - 1; ++j) {
+                    const bool ge = k >= j;
+                    raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
+                    raw_k1 = ge ? accd[j][r] : raw_k1;
                 }
-                raw_k = nfk_splus<true>(raw_k);  // NSF_CL's D <- softplus(D)
-                raw_k1 = nfk_splus<true>(raw_k1);
+                raw_k = nfk_softplus_lean(raw_k);  // NSF_CL's D <- softplus(D) (flows.py:235)
+                raw_k1 = nfk_softplus_lean(raw_k1);
                 raw_k = (k == 0) ? c.dpad : raw_k;
                 raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
-                const float d_k = c.min_d + nfk_splus<true>(raw_k);
-                const float d_k1 = c.min_d + nfk_splus<true>(raw_k1);
+                const float d_k = c.min_d + nfk_softplus_lean(raw_k);
+                const float d_k1 = c.min_d + nfk_softplus_lean(raw_k1);
                 const float x = xv[r];
                 const float delta = nfk_div<true>(h_k[r], w_k[r]);
                 const float gap = (d_k + d_k1) - 2.0f * delta;
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                 const float omt = 1.0f - th;
                 const float dnum =
                     (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
-                float lad = nfk_log<true>(dnum) - 2.0f * nfk_log<true>(den);
+                float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
                 lad = INV ? -lad : lad;
                 const bool inside = (x >= c.lo) && (x <= c.hi);
                 const bool live = jj4[r] < a.n_up && row_ok;

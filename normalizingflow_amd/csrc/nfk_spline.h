@@ -26,6 +26,7 @@ struct NfkSplineConst {
     float min_d;     // (float)min_derivative
     float dpad;      // (float)log(exp(1 - min_derivative) - 1) (utils.py:37)
     float knot_eps;  // 1e-6f (utils.py:20)
+    float m2b;       // (float)((right-left) * log2(e)): lean knots' second-softmax multiplier
 };
 
 __device__ __forceinline__ float nfk_softplus(float v) {
@@ -69,6 +70,72 @@ __device__ __forceinline__ float nfk_log_fast(float x) {
 
 __device__ __forceinline__ float nfk_softplus_fast(float v) {
     return v > 20.0f ? v : nfk_log_fast(1.0f + nfk_exp_fast(v));
+}
+
+// ---------------------------------------------------------------------------
+// Lean epilogue math for the fused layer kernel.  Every VALU instruction there
+// costs MFMA time, so these trade the reference's exact operation order for
+// short sequences whose ABSOLUTE error stays at the few-ulp level that the
+// downstream consumers (linear layers, cumulative knots) are sensitive to.
+constexpr float kL2E = 1.44269502e+00f;  // log2(e)
+constexpr float kLN2 = 6.93147182e-01f;
+
+// tanh(x) = sign(x) (1 - t) / (1 + t), t = 2^(-2|x| log2e) in (0, 1]: branch
+// free, no overflow; absolute error ~1e-7 (the hidden activations only feed
+// the next linear layer, where absolute error is what propagates).
+__device__ __forceinline__ float nfk_tanh_lean(float x) {
+    const float t = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * (-2.0f * kL2E));
+    const float r = (1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t);
+    return __builtin_copysignf(r, x);
+}
+
+// softplus (threshold 20, like torch) as log2(1 + 2^(v log2e)) ln2.
+__device__ __forceinline__ float nfk_softplus_lean(float v) {
+    const float s = __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(v * kL2E)) * kLN2;
+    return v > 20.0f ? v : s;
+}
+
+// Knots of one element from its K raw NSF_CL conditioner logits:
+//   W <- 2B softmax(raw)                 (flows.py:233-234)
+//   w <- softmax(W); w <- min + (1 - min K) w; cw <- span cumsum(w) + lo
+//                                        (utils.py:73-80, 84-91)
+// Both softmaxes are evaluated as 2^(fma(u, log2e, -shift)): softmax is
+// shift-invariant, so the rounding of the shift cancels.  The first uses the
+// max logit as shift; the second the known bound 2B of its inputs (2B softmax
+// lies in [0, 2B]) with the 1/sum folded into the exponent's multiplier,
+// m2b = 2B log2e.  The cumsum is still accumulated in double.
+// edge[0] = lo, edge[K] = hi are pinned like utils.py:78-79.
+template <int K>
+__device__ __forceinline__ void nfk_knots_nsf_lean(const float (&raw)[K], float lo, float hi, float span,
+                                                   float min_b, float fb, float m2b,
+                                                   float (&edge)[K + 1]) {
+    float m = raw[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) m = fmaxf(m, raw[i]);
+    const float mL = m * kL2E;
+    float e[K];
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(raw[i], kL2E, -mL));
+        s = i == 0 ? e[0] : s + e[i];
+    }
+    const float q = m2b * __builtin_amdgcn_rcpf(s);
+    float s2 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(e[i], q, -m2b));
+        s2 = i == 0 ? e[0] : s2 + e[i];
+    }
+    const float f = fb * __builtin_amdgcn_rcpf(s2);
+    double acc = 0.0;
+    edge[0] = lo;
+#pragma unroll
+    for (int i = 0; i < K - 1; ++i) {
+        acc += (double)__builtin_fmaf(e[i], f, min_b);
+        edge[i + 1] = __builtin_fmaf(span, (float)acc, lo);
+    }
+    edge[K] = hi;
 }
 
 template <bool FAST>
