@@ -1,33 +1,35 @@
 // nfk_fused.hip -- one launch per NSF coupling layer: conditioner MLP
-// (FCNN, nf/flows.py:20-35) on fp32 MFMA + rational-quadratic spline epilogue
+// (FCNN, nf/flows.py:20-35) on MFMA + rational-quadratic spline epilogue
 // (nf/flows.py:227-253, nf/utils.py:27-152).  The [B, n_up, 3K-1] conditioner
 // output never leaves registers.
 //
-// Work decomposition: one wave owns ST tiles of 16 samples.  All products
-// are computed transposed, h^T[feature][sample] = W . act^T, with
-// v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fmaf chain):
-//   A operand = weights   (lane l: W[row l&15][k l>>4]),
-//   B operand = activations (lane l: act[k l>>4][sample l&15]),
+// Work decomposition: one wave owns a tile of 16 samples.  All products are
+// computed transposed, h^T[feature][sample] = W . act^T:
+//   A operand = weights (from an LDS slot), B operand = activations (registers),
 //   D: lane l, register r = output row 4*(l>>4)+r of sample l&15.
-// Hidden feature f of tile t sits in row 4*r+q... precisely: row i = 4q + r of
-// tile t holds feature 16t + 4r + q, so register r of tile t IS the B
-// fragment of k-step 4t + r (features 4ks + q) of the next product -- no LDS
-// transpose between layers.
+// Layer 1 (inputs x, any magnitude) runs on v_mfma_f32_16x16x4_f32, an exact
+// fp32 fma chain.  Layer 2 and the output layer run as a two-way fp16 split on
+// v_mfma_f32_16x16x32_f16: v = hi + lo with hi = f16(v), lo = f16(v - hi)
+// (22 significant bits), product = lo.hi + hi.lo + hi.hi accumulated in fp32,
+// dropping lo.lo (2^-22 relative).  Weights are pre-scaled by a power of two
+// so that max|W| lies in [2^14, 2^15) and activations (tanh outputs) by 2^14,
+// which keeps both parts in fp16's normal range; the exact power-of-two scale
+// is undone inside the consumers (tanh constant, softmax log2e, softplus
+// argument).  Accuracy matches the fp32 chain (mean |err| ~1e-7 on the
+// logits); the fp16 form needs 3 x 16 MFMA cycles per 16x16x32 block where
+// fp32 needs 8 x 32 -- and on gfx950 fp32 MFMA and VALU share one issue port
+// (tools/ubench_coexec.hip), so MFMA cycles are paid in full.
 //
+// Hidden features are permuted (hid_feature in nfk_fused_impl.h) so that the
+// accumulators of one layer ARE the B fragments of the next: no LDS round trip.
 // Output layer: per chunk of 16 coordinates the 3K-1 parameter tiles are
 // produced in three phases (W logits, H logits, D logits; H first when
 // inverting).  Row i of a parameter tile is coordinate jbase + i, so lane l
 // holds, for sample l&15, all K logits of coordinates jbase + 4q + r in
-// registers and evaluates the spline there (same fp32 op order as
-// nfk_spline.h).  Per-sample log|det| is reduced across the four lane groups
-// with xor-16/32 shuffles.
-//
-// Weights are packed once per weight version (nfk_fused_nsf_pack) in MFMA
-// fragment order, 4 tiles per float4, so every A fragment is one coalesced
-// 16-B load that feeds 4 x ST MFMAs; a register ring keeps kPF k-steps of
-// weights in flight.  The hidden k-step count is a template parameter, so the
-// whole chain is branch-free straight-line code the scheduler can pipeline.  The x tile and the output z tile are
-// staged through a per-wave LDS region so HBM sees only full-row accesses.
+// registers and evaluates the spline there (nfk_spline.h lean forms).
+// Per-sample log|det| is reduced across the four lane groups with xor-16/32
+// shuffles.  Weights stream through two LDS slots (global_load_lds, one
+// barrier per phase); each record is read from L2 once per 128 samples.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -45,7 +47,7 @@ using namespace nfk_fused;
 
 namespace nfk_fused {
 #define NFK_X(h) NFK_FUSED_K(NFK_FUSED_EXTERN, h)
-NFK_FUSED_KSH(NFK_X)
+NFK_FUSED_KB(NFK_X)
 #undef NFK_X
 }  // namespace nfk_fused
 
@@ -57,69 +59,152 @@ struct PackArgs {
     Layout L;
 };
 
-// One thread per packed float (layout described at make_layout()).
-__device__ float pack_hidden(const float* W, const float* bias, int KS, int kin, int H, int TGH, int HT,
-                             int blk, int lane, int e) {
-    if (blk < KS * TGH) {
-        const int ks = blk / TGH, g = blk - ks * TGH, t = 4 * g + e;
-        const int f = hid_row(t, lane & 15), k = 4 * ks + (lane >> 4);
-        return (t < HT && f < H && k < kin) ? W[(int64_t)f * kin + k] : 0.0f;
+// max |W| of layer 2 (hdr[0]) and of the output layer (hdr[1]) as uint bits
+// (non-negative floats order like their bit patterns)
+__global__ __launch_bounds__(256) void k_pack_max(PackArgs a) {
+    const Layout& L = a.L;
+    const int64_t n2 = (int64_t)L.H * L.H, n3 = (int64_t)L.n_up * L.P * L.H;
+    float m2 = 0.0f, m3 = 0.0f;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n2 + n3;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        if (g < n2)
+            m2 = fmaxf(m2, fabsf(a.w2[g]));
+        else
+            m3 = fmaxf(m3, fabsf(a.w4[g - n2]));
     }
-    const int t = blk - KS * TGH, f = 16 * t + 4 * e + (lane >> 4);  // bias: register e of tile t
-    return f < H ? bias[f] : 0.0f;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+        m3 = fmaxf(m3, __shfl_xor(m3, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(reinterpret_cast<unsigned int*>(a.out), __float_as_uint(m2));
+        atomicMax(reinterpret_cast<unsigned int*>(a.out) + 1, __float_as_uint(m3));
+    }
 }
 
+// power-of-two exponent s with max|W| 2^s in [2^14, 2^15)
+__device__ int scale_exp(float maxw) {
+    if (!(maxw > 0.0f) || !(maxw < 3.0e38f)) return 0;
+    int e;
+    frexpf(maxw, &e);  // maxw = m 2^e, m in [0.5, 1)
+    return 15 - e;
+}
+
+__device__ uint32_t f16_part_pair(float v0, float v1, int part) {
+    const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+    const _Float16 r0 = part ? (_Float16)(v0 - (float)h0) : h0;
+    const _Float16 r1 = part ? (_Float16)(v1 - (float)h1) : h1;
+    return (uint32_t)__builtin_bit_cast(uint16_t, r0) | ((uint32_t)__builtin_bit_cast(uint16_t, r1) << 16);
+}
+
+// One thread per packed 32-bit word (layout described in nfk_fused_impl.h).
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     const Layout& L = a.L;
+    const unsigned int* hdr = reinterpret_cast<const unsigned int*>(a.out);
+    const int s2 = scale_exp(__uint_as_float(hdr[0])), s3 = scale_exp(__uint_as_float(hdr[1]));
+    const float sc2 = ldexpf(1.0f, s2), sc3 = ldexpf(1.0f, s3);
+    const float bs2 = ldexpf(1.0f, s2 + 14), bs3 = ldexpf(1.0f, s3 + 14);
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < L.total;
          g += (int64_t)gridDim.x * blockDim.x) {
-        const int e = (int)(g & 3), lane = (int)((g >> 2) & 63);
-        float v;
-        if (g < L.o_h2) {
-            v = pack_hidden(a.w0, a.b0, L.KS1, L.n_lo, L.H, L.TGH, L.HT, (int)(g >> 8), lane, e);
-        } else if (g < L.o_w3) {
-            v = pack_hidden(a.w2, a.b2, L.KSH, L.H, L.H, L.TGH, L.HT, (int)((g - L.o_h2) >> 8), lane, e);
+        if (g < L.o_h1) {  // header: the unscale factors (words 0, 1 hold the maxima)
+            if (g == 2) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
+            if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
+            if (g >= 4) out[g] = 0;
+            continue;
+        }
+        if (g < L.o_h2) {  // layer 1, fp32 fragments
+            const int64_t w = g - L.o_h1;
+            const int blk = (int)(w >> 8), wl = (int)(w & 255);
+            float v = 0.0f;
+            if (blk < L.KS1 * L.TG1) {
+                const int lane = wl >> 2, e = wl & 3;
+                const int ks = blk / L.TG1, gg = blk - ks * L.TG1, t = 4 * gg + e;
+                const int f = hid_feature(t, lane & 15), k = 4 * ks + (lane >> 4);
+                if (t < L.HT && f < L.H && k < L.n_lo) v = a.w0[(int64_t)f * L.n_lo + k];
+            } else {
+                const int t = wl >> 4, f = hid_feature(t, wl & 15);
+                if (t < L.HT && f < L.H) v = a.b0[f];
+            }
+            out[g] = __float_as_uint(v);
+            continue;
+        }
+        // fp16-split records: layer 2 or one output phase
+        int64_t w;
+        int NT, pbase = 0, chunk = -1;
+        if (g < L.o_w3) {
+            w = g - L.o_h2;
+            NT = L.HT;
         } else {
-            const int64_t bl = (g - L.o_w3) >> 8;
-            const int c = (int)(bl / L.blk_chunk);
-            int b = (int)(bl - (int64_t)c * L.blk_chunk);
-            int ng = L.TGK, nt = L.K, pbase = 0;
+            const int64_t w3 = g - L.o_w3;
+            const int64_t bl = w3 >> 8;
+            chunk = (int)(bl / L.blk_chunk);
+            int b = (int)(bl - (int64_t)chunk * L.blk_chunk);
+            NT = L.K;
             if (b >= L.blk_w) {
                 b -= L.blk_w;
                 pbase = L.K;
                 if (b >= L.blk_w) {
                     b -= L.blk_w;
                     pbase = 2 * L.K;
-                    ng = L.TGD;
-                    nt = L.K - 1;
+                    NT = L.K - 1;
                 }
             }
-            v = 0.0f;
-            if (b < L.KSH * ng) {
-                const int ks = b / ng, gg = b - ks * ng, t = 4 * gg + e;
-                const int j = 16 * c + (lane & 15), k = 4 * ks + (lane >> 4);
-                if (t < nt && j < L.n_up && k < L.H) v = a.w4[((int64_t)j * L.P + pbase + t) * L.H + k];
-            } else {
-                const int t = b - L.KSH * ng, j = 16 * c + 4 * (lane >> 4) + e;
-                if (t < nt && j < L.n_up) v = a.b4[(int64_t)j * L.P + pbase + t];
-            }
+            w = (int64_t)b * 256 + (w3 & 255);
         }
-        a.out[g] = v;
+        const int blk = (int)(w >> 8), wl = (int)(w & 255);
+        const bool hidden = chunk < 0;
+        if (blk < L.KB * NT * 2) {
+            const int part = blk & 1, idx = blk >> 1, kb = idx / NT, t = idx - kb * NT;
+            const int lane = wl >> 2, j = 2 * (wl & 3);
+            const int k0 = 32 * kb + 8 * (lane >> 4) + j;
+            float v0 = 0.0f, v1 = 0.0f;
+            if (hidden) {
+                const int f = hid_feature(t, lane & 15);
+                if (f < L.H) {
+                    if (k0 < L.H) v0 = a.w2[(int64_t)f * L.H + k0] * sc2;
+                    if (k0 + 1 < L.H) v1 = a.w2[(int64_t)f * L.H + k0 + 1] * sc2;
+                }
+            } else {
+                const int jc = 16 * chunk + (lane & 15);
+                if (jc < L.n_up) {
+                    const float* row = a.w4 + ((int64_t)jc * L.P + pbase + t) * L.H;
+                    if (k0 < L.H) v0 = row[k0] * sc3;
+                    if (k0 + 1 < L.H) v1 = row[k0 + 1] * sc3;
+                }
+            }
+            out[g] = f16_part_pair(v0, v1, part);
+        } else {  // bias block: [tile][row], pre-scaled like the products
+            const int t = wl >> 4, i = wl & 15;
+            float v = 0.0f;
+            if (t < NT) {
+                if (hidden) {
+                    const int f = hid_feature(t, i);
+                    if (f < L.H) v = a.b2[f] * bs2;
+                } else {
+                    const int jc = 16 * chunk + i;
+                    if (jc < L.n_up) v = a.b4[(int64_t)jc * L.P + pbase + t] * bs3;
+                }
+            }
+            out[g] = __float_as_uint(v);
+        }
     }
 }
 
 bool shape_ok(int n_lo, int n_up, int H, int K) {
     if (n_lo < 1 || n_up < 1 || n_lo + n_up > kMaxD || H < 1 || K < 2) return false;
-    if (lds_bytes(make_layout(n_lo, n_up, H, K)) > (size_t)kLdsBytes) return false;
-    const int KSH = (H + 3) / 4;
-    bool ks = false, kk = false;
-#define CHK_KSH(h) ks |= (KSH == h);
-    NFK_FUSED_KSH(CHK_KSH)
-#undef CHK_KSH
+    const Layout L = make_layout(n_lo, n_up, H, K);
+    if (lds_bytes(L) > (size_t)kLdsBytes) return false;
+    if (L.K > 16 || L.HT > 16) return false;  // one bias block per record
+    bool kb = false, kk = false;
+#define CHK_KB(h) kb |= (L.KB == h);
+    NFK_FUSED_KB(CHK_KB)
+#undef CHK_KB
 #define CHK_K(h, k) kk |= (K == k);
     NFK_FUSED_K(CHK_K, 0)
 #undef CHK_K
-    return ks && kk;
+    return kb && kk;
 }
 
 }  // namespace
@@ -140,10 +225,14 @@ extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float*
     if (!w0 || !b0 || !w2 || !b2 || !w4 || !b4 || !wpack)
         return nfk_set_error("nfk_fused_nsf_pack: null pointer");
     PackArgs a{w0, b0, w2, b2, w4, b4, wpack, make_layout(n_lo, n_up, hidden, K)};
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(wpack, 0, 2 * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_pack_max, dim3(64), dim3(256), 0, st, a);
     int64_t g = (a.L.total + 255) / 256;
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, a);
-    hipError_t e = hipGetLastError();
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, st, a);
+    e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 
@@ -179,23 +268,24 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     a.NCH = L.NCH;
     a.mode = logdet_mode;
     a.slot_blocks = L.slot_blocks;
+    a.xlo = xlo_floats(L);
     a.blk_h1 = L.blk_h1;
     a.blk_h2 = L.blk_h2;
     a.blk_w = L.blk_w;
     a.blk_d = L.blk_d;
     a.blk_chunk = L.blk_chunk;
+    a.o_h1 = (int32_t)L.o_h1;
     a.o_h2 = (int32_t)L.o_h2;
     a.o_w3 = (int32_t)L.o_w3;
     a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
     const size_t lds = lds_bytes(L);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
-    const int KSH = L.KSH;
 #define DISPATCH(h, k) \
-    if (KSH == h && K == k) return launch_fused<h, k>(a, lds, inv, st);
-#define DISPATCH_KSH(h) NFK_FUSED_K(DISPATCH, h)
-    NFK_FUSED_KSH(DISPATCH_KSH)
-#undef DISPATCH_KSH
+    if (L.KB == h && K == k) return launch_fused<h, k>(a, lds, inv, st);
+#define DISPATCH_KB(h) NFK_FUSED_K(DISPATCH, h)
+    NFK_FUSED_KB(DISPATCH_KB)
+#undef DISPATCH_KB
 #undef DISPATCH
     return nfk_set_error("nfk_fused_nsf: no kernel instance");
 }

@@ -8,24 +8,38 @@
 #include "nfk_spline.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 namespace nfk_fused {
 
-constexpr int kWaves = 8;         // waves per workgroup (two per SIMD), 16 samples each
-constexpr int kMaxD = 128;        // n_lo + n_up staged in LDS
+constexpr int kWaves = 8;  // waves per workgroup (two per SIMD), 16 samples each
+constexpr int kMaxD = 128;
 constexpr int kLdsBytes = 160 * 1024;
+constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 2^14 <= 2^14)
 
-// Packed weights: a stream of "phase records", each a run of 1-KiB blocks
-// (64 lanes x float4) in MFMA fragment order: the weight blocks of the
-// phase's KS k-steps x NG tile groups ([ks][g], 4 tiles per float4), then NT
-// bias blocks (lane l, register r of tile t = bias of the row that lane holds).
-//   hidden 1: KS1*TGH + HT blocks      hidden 2: KSH*TGH + HT blocks
-//   per 16-coordinate chunk: W logits KSH*TGK + K, H logits KSH*TGK + K,
-//                            D logits KSH*TGD + (K-1)
-// The workgroup copies one record at a time into an LDS slot with
-// global_load_lds (one wave-instruction per block), double-buffered.
+// ---------------------------------------------------------------------------
+// Packed weights ("pack"): a header block, then a stream of phase records.
+// A record is a run of 1-KiB blocks (64 lanes x 16 B, one wave-instruction of
+// global_load_lds each) followed by one bias block (float[16 tiles][16 rows]).
+//   header (1 block): hdr[0] = max|W2|, hdr[1] = max|W3| (uint bits, from the
+//            pack's reduction), float hdr[2] = 2^-(s2+14), hdr[3] = 2^-(s3+14):
+//            the factors that undo the fp16 pre-scaling of layer 2 / 3 products
+//   layer 1 (fp32, v_mfma_f32_16x16x4_f32): KS1 k-steps x TG1 groups of 4
+//            tiles: lane l of block (ks, g) holds W1[f(4g+e, l&15)][4ks + l>>4],
+//            e = 0..3 (the float4 components)
+//   layer 2 and the output phases (fp16 split, v_mfma_f32_16x16x32_f16): KB
+//            k-blocks x NT tiles x {hi, lo}: lane l of block (kb, t, p) holds
+//            part p of 2^s W[row(t, l&15)][32kb + 8(l>>4) + j], j = 0..7, where
+//            hi = f16(v), lo = f16(v - hi) and 2^s puts max|W| in [2^14, 2^15)
+//   per 16-coordinate chunk: W logits (K tiles), H logits (K tiles), D logits
+//            (K-1 tiles); row i of tile t = parameter t of coordinate 16c + i
+// Hidden feature permutation: row i of hidden tile t computes feature
+//   f(t, i) = 32(t>>1) + 8(i>>2) + 4(t&1) + (i&3),
+// so accumulator register r of tiles 2kb, 2kb+1 of lane l are exactly
+// elements j = r, 4 + r of the next product's B fragment for k-block kb
+// (k = 32kb + 8(l>>4) + j) -- activations never leave registers.
 struct Layout {
-    int n_lo, n_up, H, K, P, HT, KS1, KSH, NCH, TGH, TGK, TGD;
+    int n_lo, n_up, H, K, P, KB, HT, KS1, TG1, NCH;
     int blk_h1, blk_h2, blk_w, blk_d, blk_chunk, slot_blocks;
     int64_t o_h1, o_h2, o_w3, total;  // offsets / size in floats
 };
@@ -37,38 +51,41 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     L.H = H;
     L.K = K;
     L.P = 3 * K - 1;
-    L.HT = (H + 15) / 16;
+    L.KB = (H + 31) / 32;
+    L.HT = 2 * L.KB;
     L.KS1 = (n_lo + 3) / 4;
-    L.KSH = (H + 3) / 4;
+    L.TG1 = (L.HT + 3) / 4;
     L.NCH = (n_up + 15) / 16;
-    L.TGH = (L.HT + 3) / 4;
-    L.TGK = (K + 3) / 4;
-    L.TGD = (K - 1 + 3) / 4;
-    L.blk_h1 = L.KS1 * L.TGH + L.HT;
-    L.blk_h2 = L.KSH * L.TGH + L.HT;
-    L.blk_w = L.KSH * L.TGK + K;
-    L.blk_d = L.KSH * L.TGD + (K - 1);
+    L.blk_h1 = L.KS1 * L.TG1 + 1;
+    L.blk_h2 = L.KB * L.HT * 2 + 1;
+    L.blk_w = L.KB * K * 2 + 1;
+    L.blk_d = L.KB * (K - 1) * 2 + 1;
     L.blk_chunk = 2 * L.blk_w + L.blk_d;
     L.slot_blocks = L.blk_h1;
     if (L.blk_h2 > L.slot_blocks) L.slot_blocks = L.blk_h2;
     if (L.blk_w > L.slot_blocks) L.slot_blocks = L.blk_w;
     if (L.blk_d > L.slot_blocks) L.slot_blocks = L.blk_d;
-    L.o_h1 = 0;
-    L.o_h2 = (int64_t)L.blk_h1 * 256;
+    L.o_h1 = 256;  // after the header block
+    L.o_h2 = L.o_h1 + (int64_t)L.blk_h1 * 256;
     L.o_w3 = L.o_h2 + (int64_t)L.blk_h2 * 256;
     L.total = L.o_w3 + (int64_t)L.NCH * L.blk_chunk * 256;
     return L;
 }
 
-// dynamic LDS bytes: two weight slots, the index maps, one x tile per wave
+// floats of one wave's lower-x tile: 16 rows x 4*KS1 (16-B aligned)
+inline int xlo_floats(const Layout& L) { return (16 * 4 * L.KS1 + 3) & ~3; }
+
+// dynamic LDS bytes: two record slots, the index maps, one lower-x tile per wave
 inline size_t lds_bytes(const Layout& L) {
     const int D = L.n_lo + L.n_up;
-    const size_t maps = ((size_t)(2 * D) * sizeof(int32_t) + 15) & ~(size_t)15;
-    return 2 * (size_t)L.slot_blocks * 1024 + maps + (size_t)kWaves * 16 * (D + 1) * sizeof(float);
+    const size_t maps = (size_t)((2 * D + 3) / 4) * 16;
+    return 2 * (size_t)L.slot_blocks * 1024 + maps + (size_t)kWaves * xlo_floats(L) * sizeof(float);
 }
 
-// hidden feature held by MFMA row i (0..15) of tile t
-__host__ __device__ inline int hid_row(int t, int i) { return 16 * t + 4 * (i & 3) + (i >> 2); }
+// hidden feature computed by row i (0..15) of hidden tile t
+__host__ __device__ inline int hid_feature(int t, int i) {
+    return 32 * (t >> 1) + 8 * (i >> 2) + 4 * (t & 1) + (i & 3);
+}
 
 struct FusedArgs {
     const float* x;
@@ -78,14 +95,18 @@ struct FusedArgs {
     float* logdet;
     int32_t* status;
     int64_t ldx, ldz, batch;
-    int32_t n_lo, n_up, KS1, NCH, mode, slot_blocks;
+    int32_t n_lo, n_up, KS1, NCH, mode, slot_blocks, xlo;
     int32_t blk_h1, blk_h2, blk_w, blk_d, blk_chunk;
-    int32_t o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
+    int32_t o_h1, o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
     NfkSplineConst c;
 };
 
-__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+__device__ __forceinline__ f32x4 mfma32(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ float pick4(const float4& w, int e) {
@@ -113,58 +134,83 @@ __device__ __forceinline__ void stage_record(const float* __restrict__ src, int 
             (__attribute__((address_space(3))) void*)(slot + i * 64), 16, 0, 0);
 }
 
-// acc[t] = bias + W[tile t] . act^T over KS k-steps, A fragments and bias from
-// an LDS slot; B fragment of k-step ks = act[ks>>2][ks&3].
-template <int KS, int NT, int NG, int HTA>
-__device__ __forceinline__ void gemm_lds(const f32x4 (&act)[HTA], const float4* slot, int lane,
-                                         f32x4 (&acc)[NT]) {
-    float4 cur[NG], nxt[NG];
+// tanh of acc * unscale, returned times 2^14 (ready for the fp16 split):
+// sign(x) (1 - t) / (1 + t), t = 2^(-2|x| log2e) in (0, 1]; c2 = -2 log2e
+// unscale.  Branch free, no overflow; absolute error ~1e-7 of the activation
+// (which only feeds the next linear layer, where absolute error propagates).
+__device__ __forceinline__ float tanh_scaled(float acc, float c2) {
+    const float t = __builtin_amdgcn_exp2f(__builtin_fabsf(acc) * c2);
+    const float inv = 1.0f / kActScale;
+    const float r = (1.0f - t) * __builtin_amdgcn_rcpf(__builtin_fmaf(t, inv, inv));
+    return __builtin_copysignf(r, acc);
+}
+
+// B fragments (hi, lo) of k-block kb from the activations of tiles 2kb, 2kb+1
+template <int HT>
+__device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, h8& lo) {
 #pragma unroll
-    for (int g = 0; g < NG; ++g) cur[g] = slot[g * 64 + lane];
+    for (int j = 0; j < 8; ++j) {
+        const float v = a[2 * kb + (j >> 2)][j & 3];
+        const _Float16 h = (_Float16)v;
+        hi[j] = h;
+        lo[j] = (_Float16)(v - (float)h);
+    }
+}
+
+// acc[t] = bias + 2^s W[tile t] . act^T over KB k-blocks of 32 in the fp16
+// split: three MFMAs per (tile, k-block), small terms first.  A fragments
+// come from the LDS slot PF tiles ahead of their MFMAs.
+template <int KB, int NT>
+__device__ __forceinline__ void gemm_h(const h8 (&bh)[KB], const h8 (&bl)[KB], const float4* slot,
+                                       int lane, f32x4 (&acc)[NT]) {
+    constexpr int N = KB * NT;
+    constexpr int PF = 2;
+    const int q = lane >> 4;
+    const float4* bias = slot + N * 2 * 64;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = as_f32x4(slot[(KS * NG + t) * 64 + lane]);
+    for (int t = 0; t < NT; ++t) acc[t] = as_f32x4(bias[t * 4 + q]);
+    float4 ring[PF + 1][2];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-        // A fragments of k-step ks+1 are read while k-step ks's MFMAs run
-        if (ks + 1 < KS) {
+    for (int i = 0; i < PF && i < N; ++i) {
+        ring[i][0] = slot[(2 * i) * 64 + lane];
+        ring[i][1] = slot[(2 * i + 1) * 64 + lane];
+    }
 #pragma unroll
-            for (int g = 0; g < NG; ++g) nxt[g] = slot[((ks + 1) * NG + g) * 64 + lane];
+    for (int i = 0; i < N; ++i) {
+        if (i + PF < N) {
+            ring[(i + PF) % (PF + 1)][0] = slot[(2 * (i + PF)) * 64 + lane];
+            ring[(i + PF) % (PF + 1)][1] = slot[(2 * (i + PF) + 1) * 64 + lane];
         }
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int t = 4 * g + e;
-                if (t < NT) acc[t] = mfma(pick4(cur[g], e), act[ks >> 2][ks & 3], acc[t]);
-            }
-        }
-        if (ks + 1 < KS) {
-#pragma unroll
-            for (int g = 0; g < NG; ++g) cur[g] = nxt[g];
-        }
+        const int kb = i / NT, t = i - kb * NT;
+        const h8 ahi = __builtin_bit_cast(h8, ring[i % (PF + 1)][0]);
+        const h8 alo = __builtin_bit_cast(h8, ring[i % (PF + 1)][1]);
+        acc[t] = mfma16(alo, bh[kb], acc[t]);
+        acc[t] = mfma16(ahi, bl[kb], acc[t]);
+        acc[t] = mfma16(ahi, bh[kb], acc[t]);
     }
 }
 
 // Knot phase epilogue: for the 4 coordinates of this lane, turn the K logits
 // of register r into knots (NSF_CL's 2B softmax, then RQS's softmax, floor and
-// cumsum: nfk_knots_nsf_lean) and keep (edge_k, size_k) of the bin.  The
+// cumsum: nfk_knots_nsf_lean; the logits still carry the 2^(s3+14) product
+// scale, which l2e absorbs) and keep (edge_k, size_k) of the bin.  The
 // searched phase finds the bin by a running select over the interior edges
 // (edges are strictly increasing, so the last edge <= x is the bin of
 // utils.py:20-25 for every x inside the tails); the other phase selects by k.
 template <int K, bool SEARCH, bool Y>
 __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
-                                           const NfkSplineConst& c, int (&kb)[4], float (&ek)[4],
-                                           float (&sk)[4]) {
+                                           const NfkSplineConst& c, float l2e, int (&kb)[4],
+                                           float (&ek)[4], float (&sk)[4]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         float u[K], edge[K + 1];
 #pragma unroll
         for (int t = 0; t < K; ++t) u[t] = acc[t][r];
         if (Y)
-            nfk_knots_nsf_lean<K>(u, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, c.m2b, edge);
+            nfk_knots_nsf_lean<K>(u, l2e, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, c.m2b, edge);
         else
-            nfk_knots_nsf_lean<K>(u, c.lo, c.hi, c.span, c.min_w, c.fw, c.m2b, edge);
+            nfk_knots_nsf_lean<K>(u, l2e, c.lo, c.hi, c.span, c.min_w, c.fw, c.m2b, edge);
         float e = edge[0], e1 = edge[1];
         int k = 0;
 #pragma unroll
@@ -184,21 +230,16 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
 // two LDS slots: while phase p computes from slot p&1, the record of phase
 // p+1 is already in the other slot and phase p+2's copy is issued right after
 // the barrier that ends phase p.  One barrier per phase; everything else is
-// wave-local.  (fp32 MFMA and VALU share the vector datapath on gfx950 --
-// tools/ubench_coexec.hip -- so the epilogue uses the short-sequence
-// transcendentals of nfk_spline.h.)
-template <int KSH, int K, bool INV>
+// wave-local.
+template <int KB, int K, bool INV>
 __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
-    constexpr int HT = (KSH + 3) / 4;
-    constexpr int TGH = (HT + 3) / 4;
-    constexpr int TGK = (K + 3) / 4;
-    constexpr int TGD = (K - 1 + 3) / 4;
+    constexpr int HT = 2 * KB;
+    constexpr int TG1 = (HT + 3) / 4;
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4, sl = lane & 15;
     const int D = a.n_lo + a.n_up;
-    const int XS = D + 1;
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
     float4* slot0 = lds4;
     float4* slot1 = lds4 + a.slot_blocks * 64;
@@ -206,17 +247,17 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     int32_t* m_up_out = m_up_in + a.n_up;
     int32_t* m_lo_in = m_up_out + a.n_up;
     int32_t* m_lo_out = m_lo_in + a.n_lo;
-    float* xt = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + ((2 * D + 3) / 4)) +
-                wid * 16 * XS;
+    const int XL = 4 * a.KS1;  // lower-x tile row length (n_lo padded to the k-steps)
+    float* xl = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xlo;
     const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const NfkSplineConst& c = a.c;
     const float* pk = a.pack;
+    const bool row_ok = sl < nrows;
 
-    // ---- prologue: x rows, index maps, first two phase records
-    for (int r = 0; r < 16; ++r)
-        for (int cc = lane; cc < D; cc += 64) xt[r * XS + cc] = (r < nrows) ? a.x[(b0 + r) * a.ldx + cc] : 0.0f;
+    // ---- prologue: first record, index maps, lower-x tile, second record
+    stage_record(pk + a.o_h1, a.blk_h1, slot0, wid, lane);
     for (int i = threadIdx.x; i < a.n_up; i += 64 * kWaves) {
         m_up_in[i] = a.up_in[i];
         m_up_out[i] = a.up_out[i];
@@ -225,59 +266,82 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         m_lo_in[i] = a.lo_in[i];
         m_lo_out[i] = a.lo_out[i];
     }
-    stage_record(pk, a.blk_h1, slot0, wid, lane);
-    __syncthreads();
+    __syncthreads();  // maps visible
+    for (int i = lane; i < 16 * XL; i += 64) {
+        const int r = i / XL, k = i - r * XL;
+        xl[i] = (r < nrows && k < a.n_lo) ? a.x[(b0 + r) * a.ldx + m_lo_in[k]] : 0.0f;
+    }
+    // factors undoing the fp16 pre-scaling (pack header)
+    const float un2 = pk[2], un3 = pk[3];
+    __syncthreads();  // record 1 landed, lower-x tiles visible
     stage_record(pk + a.o_h2, a.blk_h2, slot1, wid, lane);
 
-    // ---- layer 1 (slot 0): h1^T = tanh(W1 . lower^T + b1)
+    // ---- layer 1 (slot 0, fp32 MFMA): h1^T = tanh(W1 . lower^T + b1)
     f32x4 h1[HT];
     {
         const float4* s = slot0;
+        const float4* bias = s + a.KS1 * TG1 * 64;
 #pragma unroll
-        for (int t = 0; t < HT; ++t) h1[t] = as_f32x4(s[(a.KS1 * TGH + t) * 64 + lane]);
+        for (int t = 0; t < HT; ++t) h1[t] = as_f32x4(bias[t * 4 + q]);
         for (int ks = 0; ks < a.KS1; ++ks) {
-            const int k = 4 * ks + q;
-            const int col = (k < a.n_lo) ? m_lo_in[k] : -1;
-            const float bf = (col >= 0) ? xt[sl * XS + col] : 0.0f;
+            const float bf = xl[sl * XL + 4 * ks + q];
 #pragma unroll
-            for (int g = 0; g < TGH; ++g) {
-                const float4 w = s[(ks * TGH + g) * 64 + lane];
+            for (int g = 0; g < TG1; ++g) {
+                const float4 w = s[(ks * TG1 + g) * 64 + lane];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int t = 4 * g + e;
-                    if (t < HT) h1[t] = mfma(pick4(w, e), bf, h1[t]);
+                    if (t < HT) h1[t] = mfma32(pick4(w, e), bf, h1[t]);
                 }
             }
         }
     }
+    h8 bh[KB], bl[KB];
+    {
+        const float c2 = -2.0f * kL2E;
 #pragma unroll
-    for (int t = 0; t < HT; ++t)
+        for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h1[t][r] = nfk_tanh_lean(h1[t][r]);
-    __syncthreads();  // slot 0 free, hidden-2 record landed
+            for (int r = 0; r < 4; ++r) h1[t][r] = tanh_scaled(h1[t][r], c2);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) split_act<HT>(h1, kb, bh[kb], bl[kb]);
+    }
+    __syncthreads();  // slot 0 free, layer-2 record landed
     const float* w3 = pk + a.o_w3;
     // execution order of the three records of a chunk: searched knots, other knots, derivatives
     const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
     stage_record(w3 + offA * 256, a.blk_w, slot0, wid, lane);
 
-    // ---- layer 2 (slot 1): h2^T = tanh(W2 . h1^T + b2); register r of tile t = k-step 4t+r
-    f32x4 h2[HT];
-    gemm_lds<KSH, HT, TGH, HT>(h1, slot1, lane, h2);
+    // ---- layer 2 (slot 1, fp16 split): h2^T = tanh(W2 . h1^T + b2)
+    {
+        f32x4 h2[HT];
+        gemm_h<KB, HT>(bh, bl, slot1, lane, h2);
+        const float c2 = -2.0f * kL2E * un2;
 #pragma unroll
-    for (int t = 0; t < HT; ++t)
+        for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h2[t][r] = nfk_tanh_lean(h2[t][r]);
+            for (int r = 0; r < 4; ++r) h2[t][r] = tanh_scaled(h2[t][r], c2);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) split_act<HT>(h2, kb, bh[kb], bl[kb]);
+    }
     __syncthreads();  // slot 1 free, chunk-0 record A landed
     stage_record(w3 + offB * 256, a.blk_w, slot1, wid, lane);
 
+    const float l2e3 = kL2E * un3;
     float ldsum = 0.0f;
     bool any_in = false, any_nd = false;
     float* zrow = a.z + (b0 + sl) * a.ldz;
+    const float* xrow = a.x + (b0 + (row_ok ? sl : 0)) * a.ldx;
     // record A and C of a chunk use slot sA, record B slot sB; the next chunk's
     // A is staged into sB once B is consumed, so the roles swap every chunk
     float4* sA = slot0;
     float4* sB = slot1;
-    const bool row_ok = sl < nrows;
+    float xn[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int j = 4 * q + r;
+        xn[r] = (j < a.n_up && row_ok) ? xrow[m_up_in[j]] : 0.0f;
+    }
     for (int ch = 0; ch < a.NCH; ++ch) {
         const int jbase = 16 * ch;
         const float* wc = w3 + (int64_t)ch * a.blk_chunk * 256;
@@ -288,19 +352,20 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         float cw_k[4], w_k[4], ch_k[4], h_k[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int j = jbase + 4 * q + r;
-            jj4[r] = j;
-            xv[r] = (j < a.n_up) ? xt[sl * XS + m_up_in[j]] : 0.0f;
+            jj4[r] = jbase + 4 * q + r;
+            xv[r] = xn[r];
+            const int jn = jj4[r] + 16;  // prefetch the next chunk's x
+            xn[r] = (jn < a.n_up && row_ok) ? xrow[m_up_in[jn]] : 0.0f;
         }
 
         // ---- record A (slot sA): searched knots (widths forward / heights inverse)
         {
             f32x4 acc[K];
-            gemm_lds<KSH, K, TGK, HT>(h2, sA, lane, acc);
+            gemm_h<KB, K>(bh, bl, sA, lane, acc);
             if (INV)
-                knot_phase<K, true, true>(acc, xv, c, kb, ch_k, h_k);
+                knot_phase<K, true, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
             else
-                knot_phase<K, true, false>(acc, xv, c, kb, cw_k, w_k);
+                knot_phase<K, true, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
         }
         __syncthreads();
         stage_record(wc + offC * 256, a.blk_d, sA, wid, lane);
@@ -308,11 +373,11 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         // ---- record B (slot sB): the other knots, selected at the bin
         {
             f32x4 acc[K];
-            gemm_lds<KSH, K, TGK, HT>(h2, sB, lane, acc);
+            gemm_h<KB, K>(bh, bl, sB, lane, acc);
             if (INV)
-                knot_phase<K, false, false>(acc, xv, c, kb, cw_k, w_k);
+                knot_phase<K, false, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
             else
-                knot_phase<K, false, true>(acc, xv, c, kb, ch_k, h_k);
+                knot_phase<K, false, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
         }
         __syncthreads();
         if (ch + 1 < a.NCH) stage_record(wn + offA * 256, a.blk_w, sB, wid, lane);
@@ -320,7 +385,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         // ---- record C (slot sA): derivatives of the bin, evaluate, log|det|
         {
             f32x4 accd[DN];
-            gemm_lds<KSH, DN, TGD, HT>(h2, sA, lane, accd);
+            gemm_h<KB, DN>(bh, bl, sA, lane, accd);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 // padded derivative index j+1 holds logit j (utils.py:36-39):
@@ -329,12 +394,12 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                 float raw_k = accd[0][r], raw_k1 = accd[0][r];
 #pragma unroll
                 for (int j = 1; j < K - 1; ++j) {
-                    const bool ge = k >= j;
                     raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
-                    raw_k1 = ge ? accd[j][r] : raw_k1;
+                    raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
                 }
-                raw_k = nfk_softplus_lean(raw_k);  // NSF_CL's D <- softplus(D) (flows.py:235)
-                raw_k1 = nfk_softplus_lean(raw_k1);
+                // NSF_CL's D <- softplus(D) (flows.py:235), only where it is used
+                raw_k = nfk_softplus_lean(raw_k * un3);
+                raw_k1 = nfk_softplus_lean(raw_k1 * un3);
                 raw_k = (k == 0) ? c.dpad : raw_k;
                 raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
                 const float d_k = c.min_d + nfk_softplus_lean(raw_k);
@@ -387,7 +452,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     // ---- identity-copied coordinates, per-sample log|det|
     for (int i = lane; i < 16 * a.n_lo; i += 64) {
         const int row = i / a.n_lo, qq = i - row * a.n_lo;
-        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xt[row * XS + m_lo_in[qq]];
+        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xl[row * XL + qq];
     }
     {
         float v = ldsum;
@@ -407,31 +472,31 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     }
 }
 
-template <int KSH, int K>
+template <int KB, int K>
 int launch_fused(const FusedArgs& a, size_t lds, bool inv, hipStream_t st) {
     const int64_t per_block = (int64_t)kWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
     if (inv)
-        hipLaunchKernelGGL((k_fused_nsf<KSH, K, true>), dim3((unsigned)blocks), dim3(64 * kWaves), lds,
+        hipLaunchKernelGGL((k_fused_nsf<KB, K, true>), dim3((unsigned)blocks), dim3(64 * kWaves), lds,
                            st, a);
     else
-        hipLaunchKernelGGL((k_fused_nsf<KSH, K, false>), dim3((unsigned)blocks), dim3(64 * kWaves),
+        hipLaunchKernelGGL((k_fused_nsf<KB, K, false>), dim3((unsigned)blocks), dim3(64 * kWaves),
                            lds, st, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 
-// explicit instantiation: definitions live in nfk_fused_ksh<KSH>.hip (one TU
-// per hidden k-step count so make -j compiles them in parallel); nfk_fused.hip
+// explicit instantiation: definitions live in nfk_fused_kb<KB>.hip (one TU
+// per hidden k-block count so make -j compiles them in parallel); nfk_fused.hip
 // sees only the extern declarations.
-#define NFK_FUSED_INSTANCE(KSH, K) \
-    template int launch_fused<KSH, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
-#define NFK_FUSED_EXTERN(KSH, K) \
-    extern template int launch_fused<KSH, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
+#define NFK_FUSED_INSTANCE(KB, K) \
+    template int launch_fused<KB, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
+#define NFK_FUSED_EXTERN(KB, K) \
+    extern template int launch_fused<KB, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
 
-// supported hidden sizes: KSH = ceil(H/4) k-steps of 4 (H = 12, 16, 32, 64, 100, 128)
-#define NFK_FUSED_KSH(X) X(3) X(4) X(8) X(16) X(25) X(32)
-#define NFK_FUSED_K(X, KSH) X(KSH, 4) X(KSH, 5) X(KSH, 6) X(KSH, 8) X(KSH, 10)
+// supported hidden widths: KB = ceil(H/32) k-blocks of 32 (H <= 128)
+#define NFK_FUSED_KB(X) X(1) X(2) X(3) X(4)
+#define NFK_FUSED_K(X, KB) X(KB, 4) X(KB, 5) X(KB, 6) X(KB, 8) X(KB, 10)
 
 }  // namespace nfk_fused

@@ -1,4 +1,4 @@
-// nfk_fused_ksh3.hip -- fused NSF layer kernel instances with 3 hidden k-steps (H <= 12).
+// nfk_fused_kb3.hip -- fused NSF layer kernel instances with 3 hidden k-blocks of 32 (H <= 96).
 #include "nfk_fused_impl.h"
 
 namespace nfk_fused {

@@ -1,4 +1,4 @@
-// nfk_fused_ksh4.hip -- fused NSF layer kernel instances with 4 hidden k-steps (H <= 16).
+// nfk_fused_kb4.hip -- fused NSF layer kernel instances with 4 hidden k-blocks of 32 (H <= 128).
 #include "nfk_fused_impl.h"
 
 namespace nfk_fused {

@@ -80,15 +80,6 @@ __device__ __forceinline__ float nfk_softplus_fast(float v) {
 constexpr float kL2E = 1.44269502e+00f;  // log2(e)
 constexpr float kLN2 = 6.93147182e-01f;
 
-// tanh(x) = sign(x) (1 - t) / (1 + t), t = 2^(-2|x| log2e) in (0, 1]: branch
-// free, no overflow; absolute error ~1e-7 (the hidden activations only feed
-// the next linear layer, where absolute error is what propagates).
-__device__ __forceinline__ float nfk_tanh_lean(float x) {
-    const float t = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * (-2.0f * kL2E));
-    const float r = (1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t);
-    return __builtin_copysignf(r, x);
-}
-
 // softplus (threshold 20, like torch) as log2(1 + 2^(v log2e)) ln2.
 __device__ __forceinline__ float nfk_softplus_lean(float v) {
     const float s = __builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(v * kL2E)) * kLN2;
@@ -105,19 +96,20 @@ __device__ __forceinline__ float nfk_softplus_lean(float v) {
 // lies in [0, 2B]) with the 1/sum folded into the exponent's multiplier,
 // m2b = 2B log2e.  The cumsum is still accumulated in double.
 // edge[0] = lo, edge[K] = hi are pinned like utils.py:78-79.
+// l2e = log2(e) times any power-of-two scale the logits still carry.
 template <int K>
-__device__ __forceinline__ void nfk_knots_nsf_lean(const float (&raw)[K], float lo, float hi, float span,
-                                                   float min_b, float fb, float m2b,
+__device__ __forceinline__ void nfk_knots_nsf_lean(const float (&raw)[K], float l2e, float lo, float hi,
+                                                   float span, float min_b, float fb, float m2b,
                                                    float (&edge)[K + 1]) {
     float m = raw[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) m = fmaxf(m, raw[i]);
-    const float mL = m * kL2E;
+    const float mL = m * l2e;
     float e[K];
     float s = 0.0f;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(raw[i], kL2E, -mL));
+        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(raw[i], l2e, -mL));
         s = i == 0 ? e[0] : s + e[i];
     }
     const float q = m2b * __builtin_amdgcn_rcpf(s);
