@@ -268,7 +268,8 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     a.NCH = L.NCH;
     a.mode = logdet_mode;
     a.slot_blocks = L.slot_blocks;
-    a.xlo = xlo_floats(L);
+    a.xtile = x_tile_floats(L);
+    a.xup = x_up_row(L);
     a.blk_h1 = L.blk_h1;
     a.blk_h2 = L.blk_h2;
     a.blk_w = L.blk_w;

@@ -72,14 +72,20 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     return L;
 }
 
-// floats of one wave's lower-x tile: 16 rows x 4*KS1 (16-B aligned)
-inline int xlo_floats(const Layout& L) { return (16 * 4 * L.KS1 + 3) & ~3; }
+// Row lengths of one wave's x tile: 16 rows of the lower coordinates (padded
+// to the layer-1 k-steps), later overwritten by 16 rows of the upper ones
+// (padded to 4).  Both are filled by per-lane LDS-DMA gathers of 64 dwords.
+inline int x_lo_row(const Layout& L) { return 4 * L.KS1; }
+inline int x_up_row(const Layout& L) { return (L.n_up + 3) & ~3; }
+inline int x_tile_floats(const Layout& L) {
+    return 16 * (x_lo_row(L) > x_up_row(L) ? x_lo_row(L) : x_up_row(L));
+}
 
-// dynamic LDS bytes: two record slots, the index maps, one lower-x tile per wave
+// dynamic LDS bytes: two record slots, the index maps, one x tile per wave
 inline size_t lds_bytes(const Layout& L) {
     const int D = L.n_lo + L.n_up;
     const size_t maps = (size_t)((2 * D + 3) / 4) * 16;
-    return 2 * (size_t)L.slot_blocks * 1024 + maps + (size_t)kWaves * xlo_floats(L) * sizeof(float);
+    return 2 * (size_t)L.slot_blocks * 1024 + maps + (size_t)kWaves * x_tile_floats(L) * sizeof(float);
 }
 
 // hidden feature computed by row i (0..15) of hidden tile t
@@ -95,7 +101,7 @@ struct FusedArgs {
     float* logdet;
     int32_t* status;
     int64_t ldx, ldz, batch;
-    int32_t n_lo, n_up, KS1, NCH, mode, slot_blocks, xlo;
+    int32_t n_lo, n_up, KS1, NCH, mode, slot_blocks, xtile, xup;
     int32_t blk_h1, blk_h2, blk_w, blk_d, blk_chunk;
     int32_t o_h1, o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
     NfkSplineConst c;
@@ -122,16 +128,63 @@ __device__ __forceinline__ f32x4 as_f32x4(const float4& v) {
     return r;
 }
 
+// LDS-DMA is issued through inline asm and waited for by hand: the compiler
+// cannot prove that a DMA into one slot does not alias reads of the other, so
+// with the builtin it drains every DMA (vmcnt(0)) before the first ds_read of
+// each phase -- serialising the copy of phase p+1 with the compute of phase p.
+// Invariant instead: a DMA issued right after the barrier that ends phase p
+// is waited for (vmcnt(0)) at the barrier that ends phase p+1, and the kernel
+// issues no other VGPR-destination global loads while DMAs are in flight.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+__device__ __forceinline__ void dma16(const float* gsrc, uint32_t lds) {
+    uint32_t saved;  // m0 is reserved by the compiler: restore it
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "s"(lds), "v"(gsrc)
+                 : "memory");
+}
+
+__device__ __forceinline__ void dma4(const float* gsrc, uint32_t lds) {
+    uint32_t saved;  // m0 is reserved by the compiler: restore it
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "s"(lds), "v"(gsrc)
+                 : "memory");
+}
+
+// every DMA and LDS access of this wave retired, then the workgroup barrier
+__device__ __forceinline__ void dma_barrier() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // Copy one phase record (nblk 1-KiB blocks at src) into an LDS slot: block i
 // goes by wave i % kWaves as one global_load_lds_dwordx4 (LDS destination =
-// wave-uniform base + 16 B x lane).  Completion is waited for by the
-// workgroup barrier that precedes the slot's first read (vmcnt(0) + s_barrier).
+// wave-uniform base + 16 B x lane).
 __device__ __forceinline__ void stage_record(const float* __restrict__ src, int nblk, float4* slot,
                                              int wid, int lane) {
-    for (int i = wid; i < nblk; i += kWaves)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + (int64_t)i * 256 + lane * 4),
-            (__attribute__((address_space(3))) void*)(slot + i * 64), 16, 0, 0);
+    const uint32_t base = lds_addr(slot);
+    for (int i = wid; i < nblk; i += kWaves) dma16(src + (int64_t)i * 256 + lane * 4, base + i * 1024);
+}
+
+// Gather a [16][row] tile of x (rows b0.., columns map[0..n)) into this wave's
+// LDS tile: element e = 64 i + lane of instruction i is (e / row, e % row).
+// Padding columns and rows past the batch re-read a valid element (their
+// weights are zero / their results are dropped).
+__device__ __forceinline__ void gather_x(const float* __restrict__ x, int64_t ldx, int64_t b0, int nrows,
+                                         const int32_t* map, int n, int row, float* tile, int lane) {
+    const uint32_t base = lds_addr(tile);
+    for (int i = 0; i < row / 4; ++i) {
+        const int e = 64 * i + lane, r = e / row, k = e - r * row;
+        const int64_t rr = b0 + (r < nrows ? r : 0);
+        dma4(x + rr * ldx + map[k < n ? k : 0], base + i * 256);
+    }
 }
 
 // tanh of acc * unscale, returned times 2^14 (ready for the fp16 split):
@@ -202,6 +255,18 @@ template <int K, bool SEARCH, bool Y>
 __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
                                            const NfkSplineConst& c, float l2e, int (&kb)[4],
                                            float (&ek)[4], float (&sk)[4]) {
+#ifdef NFK_ABL_NOEPI
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float v = 0.0f;
+#pragma unroll
+        for (int t = 0; t < K; ++t) v += acc[t][r];
+        if (SEARCH) kb[r] = 0;
+        ek[r] = v;
+        sk[r] = xv[r];
+    }
+    return;
+#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         float u[K], edge[K + 1];
@@ -226,6 +291,20 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
     }
 }
 
+// Ablation hooks for diagnostic builds (tools/ablate.sh; never in the product
+// build): NFK_ABL_NOSTAGE drops the chunk-loop record copies, NFK_ABL_NOBAR the
+// chunk-loop barriers, NFK_ABL_NOEPI replaces the spline epilogue by a sum.
+#ifdef NFK_ABL_NOSTAGE
+#define NFK_STAGE(...) ((void)0)
+#else
+#define NFK_STAGE(...) stage_record(__VA_ARGS__)
+#endif
+#ifdef NFK_ABL_NOBAR
+#define NFK_PHASE_BARRIER() ((void)0)
+#else
+#define NFK_PHASE_BARRIER() dma_barrier()
+#endif
+
 // One workgroup = kWaves waves x 16 samples.  Phase records stream through
 // two LDS slots: while phase p computes from slot p&1, the record of phase
 // p+1 is already in the other slot and phase p+2's copy is issued right after
@@ -248,7 +327,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     int32_t* m_lo_in = m_up_out + a.n_up;
     int32_t* m_lo_out = m_lo_in + a.n_lo;
     const int XL = 4 * a.KS1;  // lower-x tile row length (n_lo padded to the k-steps)
-    float* xl = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xlo;
+    const int XU = a.xup;      // upper-x tile row length (n_up padded to 4)
+    float* xt = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xtile;
     const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
@@ -256,8 +336,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     const float* pk = a.pack;
     const bool row_ok = sl < nrows;
 
-    // ---- prologue: first record, index maps, lower-x tile, second record
-    stage_record(pk + a.o_h1, a.blk_h1, slot0, wid, lane);
+    // ---- prologue: index maps (plain loads, before any DMA is in flight),
+    // first record and the lower-x gather, second record
     for (int i = threadIdx.x; i < a.n_up; i += 64 * kWaves) {
         m_up_in[i] = a.up_in[i];
         m_up_out[i] = a.up_out[i];
@@ -266,14 +346,12 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         m_lo_in[i] = a.lo_in[i];
         m_lo_out[i] = a.lo_out[i];
     }
-    __syncthreads();  // maps visible
-    for (int i = lane; i < 16 * XL; i += 64) {
-        const int r = i / XL, k = i - r * XL;
-        xl[i] = (r < nrows && k < a.n_lo) ? a.x[(b0 + r) * a.ldx + m_lo_in[k]] : 0.0f;
-    }
     // factors undoing the fp16 pre-scaling (pack header)
     const float un2 = pk[2], un3 = pk[3];
-    __syncthreads();  // record 1 landed, lower-x tiles visible
+    __syncthreads();  // maps visible (no DMA in flight yet)
+    stage_record(pk + a.o_h1, a.blk_h1, slot0, wid, lane);
+    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xt, lane);
+    dma_barrier();  // layer-1 record and lower-x tiles landed
     stage_record(pk + a.o_h2, a.blk_h2, slot1, wid, lane);
 
     // ---- layer 1 (slot 0, fp32 MFMA): h1^T = tanh(W1 . lower^T + b1)
@@ -284,7 +362,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
         for (int t = 0; t < HT; ++t) h1[t] = as_f32x4(bias[t * 4 + q]);
         for (int ks = 0; ks < a.KS1; ++ks) {
-            const float bf = xl[sl * XL + 4 * ks + q];
+            const float bf = xt[sl * XL + 4 * ks + q];
 #pragma unroll
             for (int g = 0; g < TG1; ++g) {
                 const float4 w = s[(ks * TG1 + g) * 64 + lane];
@@ -296,6 +374,14 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
             }
         }
     }
+    // identity-copied (lower) coordinates straight from the tile, then the
+    // tile is refilled with the upper coordinates
+    for (int i = lane; i < 16 * a.n_lo; i += 64) {
+        const int row = i / a.n_lo, qq = i - row * a.n_lo;
+        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xt[row * XL + qq];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile reads done before the DMA overwrites it
+    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xt, lane);
     h8 bh[KB], bl[KB];
     {
         const float c2 = -2.0f * kL2E;
@@ -306,7 +392,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) split_act<HT>(h1, kb, bh[kb], bl[kb]);
     }
-    __syncthreads();  // slot 0 free, layer-2 record landed
+    dma_barrier();  // slot 0 free; layer-2 record and upper-x tiles landed
     const float* w3 = pk + a.o_w3;
     // execution order of the three records of a chunk: searched knots, other knots, derivatives
     const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
@@ -324,24 +410,17 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) split_act<HT>(h2, kb, bh[kb], bl[kb]);
     }
-    __syncthreads();  // slot 1 free, chunk-0 record A landed
+    dma_barrier();  // slot 1 free, chunk-0 record A landed
     stage_record(w3 + offB * 256, a.blk_w, slot1, wid, lane);
 
     const float l2e3 = kL2E * un3;
     float ldsum = 0.0f;
     bool any_in = false, any_nd = false;
     float* zrow = a.z + (b0 + sl) * a.ldz;
-    const float* xrow = a.x + (b0 + (row_ok ? sl : 0)) * a.ldx;
     // record A and C of a chunk use slot sA, record B slot sB; the next chunk's
     // A is staged into sB once B is consumed, so the roles swap every chunk
     float4* sA = slot0;
     float4* sB = slot1;
-    float xn[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int j = 4 * q + r;
-        xn[r] = (j < a.n_up && row_ok) ? xrow[m_up_in[j]] : 0.0f;
-    }
     for (int ch = 0; ch < a.NCH; ++ch) {
         const int jbase = 16 * ch;
         const float* wc = w3 + (int64_t)ch * a.blk_chunk * 256;
@@ -353,9 +432,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             jj4[r] = jbase + 4 * q + r;
-            xv[r] = xn[r];
-            const int jn = jj4[r] + 16;  // prefetch the next chunk's x
-            xn[r] = (jn < a.n_up && row_ok) ? xrow[m_up_in[jn]] : 0.0f;
+            xv[r] = (jj4[r] < a.n_up) ? xt[sl * XU + jj4[r]] : 0.0f;
         }
 
         // ---- record A (slot sA): searched knots (widths forward / heights inverse)
@@ -367,8 +444,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
             else
                 knot_phase<K, true, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
         }
-        __syncthreads();
-        stage_record(wc + offC * 256, a.blk_d, sA, wid, lane);
+        NFK_PHASE_BARRIER();
+        NFK_STAGE(wc + offC * 256, a.blk_d, sA, wid, lane);
 
         // ---- record B (slot sB): the other knots, selected at the bin
         {
@@ -379,13 +456,26 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
             else
                 knot_phase<K, false, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
         }
-        __syncthreads();
-        if (ch + 1 < a.NCH) stage_record(wn + offA * 256, a.blk_w, sB, wid, lane);
+        NFK_PHASE_BARRIER();
+        if (ch + 1 < a.NCH) NFK_STAGE(wn + offA * 256, a.blk_w, sB, wid, lane);
 
         // ---- record C (slot sA): derivatives of the bin, evaluate, log|det|
         {
             f32x4 accd[DN];
             gemm_h<KB, DN>(bh, bl, sA, lane, accd);
+#ifdef NFK_ABL_NOEPI
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
+#pragma unroll
+                for (int t = 0; t < DN; ++t) v += accd[t][r];
+                const bool live = jj4[r] < a.n_up && row_ok;
+                if (live) zrow[m_up_out[jj4[r]]] = v;
+                ldsum += v;
+                any_in |= live;
+            }
+            if (false)
+#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 // padded derivative index j+1 holds logit j (utils.py:36-39):
@@ -397,15 +487,14 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                     raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
                     raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
                 }
-                // NSF_CL's D <- softplus(D) (flows.py:235), only where it is used
-                raw_k = nfk_softplus_lean(raw_k * un3);
-                raw_k1 = nfk_softplus_lean(raw_k1 * un3);
-                raw_k = (k == 0) ? c.dpad : raw_k;
-                raw_k1 = (k == K - 1) ? c.dpad : raw_k1;
-                const float d_k = c.min_d + nfk_softplus_lean(raw_k);
-                const float d_k1 = c.min_d + nfk_softplus_lean(raw_k1);
+                // d = min_d + softplus(softplus(D)) (flows.py:235, utils.py:82), only
+                // at the two knots the bin uses; the padded ends are the constant d_edge
+                const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k * un3, c.min_d);
+                const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1 * un3, c.min_d);
                 const float x = xv[r];
-                const float delta = nfk_div<true>(h_k[r], w_k[r]);
+                // one reciprocal of the bin width for delta and theta
+                const float rw = nfk_rcp_fast(w_k[r]);
+                const float delta = h_k[r] * rw;
                 const float gap = (d_k + d_k1) - 2.0f * delta;
                 float out, th;
                 bool nd = false;
@@ -420,7 +509,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                     out = root * w_k[r] + cw_k[r];
                     th = root;
                 } else {
-                    th = nfk_div<true>(x - cw_k[r], w_k[r]);
+                    th = (x - cw_k[r]) * rw;
                 }
                 const float t1mt = th * (1.0f - th);
                 const float den = delta + gap * t1mt;
@@ -442,18 +531,14 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                 any_nd |= nd && inside && live;
             }
         }
-        __syncthreads();
-        if (ch + 1 < a.NCH) stage_record(wn + offB * 256, a.blk_w, sA, wid, lane);
+        NFK_PHASE_BARRIER();
+        if (ch + 1 < a.NCH) NFK_STAGE(wn + offB * 256, a.blk_w, sA, wid, lane);
         float4* t = sA;
         sA = sB;
         sB = t;
     }
 
-    // ---- identity-copied coordinates, per-sample log|det|
-    for (int i = lane; i < 16 * a.n_lo; i += 64) {
-        const int row = i / a.n_lo, qq = i - row * a.n_lo;
-        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xl[row * XL + qq];
-    }
+    // ---- per-sample log|det|
     {
         float v = ldsum;
         v += __shfl_xor(v, 16, 64);

@@ -55,6 +55,7 @@ NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, d
     c.dpad = (float)std::log(std::exp(1.0 - min_d) - 1.0);
     c.knot_eps = (float)1e-6;
     c.m2b = (float)((right - left) * 1.4426950408889634);
+    c.d_edge = c.min_d + log1pf(expf(c.dpad));  // fp32 like the reference's tensor ops
     return c;
 }
 

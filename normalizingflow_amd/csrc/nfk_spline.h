@@ -27,6 +27,7 @@ struct NfkSplineConst {
     float dpad;      // (float)log(exp(1 - min_derivative) - 1) (utils.py:37)
     float knot_eps;  // 1e-6f (utils.py:20)
     float m2b;       // (float)((right-left) * log2(e)): lean knots' second-softmax multiplier
+    float d_edge;    // min_d + softplus(dpad) in fp32: the boundary derivative (utils.py:36-39, 82)
 };
 
 __device__ __forceinline__ float nfk_softplus(float v) {
@@ -119,15 +120,29 @@ __device__ __forceinline__ void nfk_knots_nsf_lean(const float (&raw)[K], float 
         e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(e[i], q, -m2b));
         s2 = i == 0 ? e[0] : s2 + e[i];
     }
-    const float f = fb * __builtin_amdgcn_rcpf(s2);
-    double acc = 0.0;
+    // cumsum of the floored fractions in 2^-30 fixed point: every fraction is
+    // >= min_b (~2^-10) so the truncation to 2^-30 loses < 2^-20 of it, the
+    // int32 prefix sums are exact (total < 2^30), and each prefix is rounded
+    // to fp32 once -- the double-accumulated cumsum of ATen without f64 ops.
+    const float f30 = (fb * 1073741824.0f) * __builtin_amdgcn_rcpf(s2);
+    const float mb30 = min_b * 1073741824.0f;
+    const float sp30 = span * (1.0f / 1073741824.0f);
+    int acc = 0;
     edge[0] = lo;
 #pragma unroll
     for (int i = 0; i < K - 1; ++i) {
-        acc += (double)__builtin_fmaf(e[i], f, min_b);
-        edge[i + 1] = __builtin_fmaf(span, (float)acc, lo);
+        acc += (int)__builtin_fmaf(e[i], f30, mb30);
+        edge[i + 1] = __builtin_fmaf(sp30, (float)acc, lo);
     }
     edge[K] = hi;
+}
+
+// min_d + softplus(softplus(v)) of NSF_CL + RQS (flows.py:235, utils.py:82) in
+// one step: e^softplus(v) = 1 + e^v, so softplus(softplus(v)) = log(2 + e^v);
+// torch's threshold 20 passes v through both softplus calls unchanged.
+__device__ __forceinline__ float nfk_deriv_lean(float v, float min_d) {
+    const float s = __builtin_amdgcn_logf(2.0f + __builtin_amdgcn_exp2f(v * kL2E)) * kLN2;
+    return min_d + (v > 20.0f ? v : s);
 }
 
 template <bool FAST>

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build diagnostic variants of libnfk.so (ablation hooks in nfk_fused_impl.h).
+# usage: bash tools/ablate_build.sh   -> normalizingflow_amd/libnfk_abl_*.so
+set -e
+cd "$(dirname "$0")/../normalizingflow_amd/csrc"
+build() {  # name, defines
+  make -s -j8 EXTRA="$2" OUT=../libnfk_abl_$1.so BUILD=../../build/abl_$1 >/dev/null
+  echo "built libnfk_abl_$1.so ($2)"
+}
+build nostage "-DNFK_ABL_NOSTAGE"
+build nostage_nobar "-DNFK_ABL_NOSTAGE -DNFK_ABL_NOBAR"
+build noepi "-DNFK_ABL_NOEPI"
+build mfma_only "-DNFK_ABL_NOEPI -DNFK_ABL_NOSTAGE -DNFK_ABL_NOBAR"
