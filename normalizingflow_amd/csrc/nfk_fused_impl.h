@@ -374,11 +374,22 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
             }
         }
     }
-    // identity-copied (lower) coordinates straight from the tile, then the
-    // tile is refilled with the upper coordinates
-    for (int i = lane; i < 16 * a.n_lo; i += 64) {
-        const int row = i / a.n_lo, qq = i - row * a.n_lo;
-        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xt[row * XL + qq];
+    // identity-copied (lower) coordinates: kept in registers and written after
+    // the chunks, next to the upper stores of the same z lines (written here
+    // when they do not fit: n_lo > 32); then the tile takes the upper coordinates
+    constexpr int kLoRegs = 8;
+    float lo_keep[kLoRegs];
+    const bool lo_late = a.KS1 <= kLoRegs;  // 16 n_lo <= 64 kLoRegs
+#pragma unroll
+    for (int m = 0; m < kLoRegs; ++m) {
+        const int i = lane + 64 * m, row = i / XL, qq = i - row * XL;
+        lo_keep[m] = (lo_late && m < a.KS1) ? xt[row * XL + qq] : 0.0f;
+    }
+    if (!lo_late) {
+        for (int i = lane; i < 16 * a.n_lo; i += 64) {
+            const int row = i / a.n_lo, qq = i - row * a.n_lo;
+            if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xt[row * XL + qq];
+        }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile reads done before the DMA overwrites it
     if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xt, lane);
@@ -538,7 +549,14 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         sB = t;
     }
 
-    // ---- per-sample log|det|
+    // ---- identity-copied coordinates (tile row length XL, see above), per-sample log|det|
+    if (lo_late) {
+#pragma unroll
+        for (int m = 0; m < kLoRegs; ++m) {
+            const int i = lane + 64 * m, row = i / XL, qq = i - row * XL;
+            if (m < a.KS1 && row < nrows && qq < a.n_lo) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = lo_keep[m];
+        }
+    }
     {
         float v = ldsum;
         v += __shfl_xor(v, 16, 64);

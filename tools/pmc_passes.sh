@@ -14,6 +14,7 @@ PASSES=(
  "FETCH_SIZE"
  "WRITE_SIZE"
  "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum"
+ "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU"
 )
 i=0
 for p in "${PASSES[@]}"; do
