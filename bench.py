@@ -107,22 +107,27 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic):
         n_lo = kw["size"]  # mask of one coordinate per particle (dim=2)
         n_up = kw["size"] * (kw["dim"] - 1)
         P = 3 * kw["K"] - 1
-        f1 = 2.0 * n_lo * H                      # layer 1: f32 MFMA (exact fp32 chain)
-        f23 = 2.0 * (H * H + H * n_up * P)       # layers 2-3: fp16 two-way split, 3 products each
-        flops = (f1 + f23) * B                   # 173,600/sample (fp32-equivalent)
-        # MFMA-time floor of this formulation, priced at the dense peak of the
-        # MFMA each part runs on, expressed as an fp32-equivalent TFLOP/s peak
-        t_floor = f1 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * f23 / (PEAK_FP16_TFLOPS * 1e12)
-        peak = (f1 + f23) / t_floor / 1e12
+        # the kernel's formulation (nfk_fused_impl.h): every product runs as a
+        # two-way fp16 split (3 MFMA products) except, when H = 32 KBH + R with
+        # 0 < R <= 4, the R-feature k-tail of layers 2-3 on exact f32 MFMA
+        kbf, R = divmod(H, 32)
+        tail = R if (0 < R <= 4 and kbf >= 1) else 0
+        f32 = 2.0 * tail * (H + n_up * P)
+        f16 = 2.0 * (n_lo * H + H * H + H * n_up * P) - f32
+        flops = (f16 + f32) * B                  # 173,600/sample (fp32-equivalent)
+        # MFMA-time floor of this formulation at the dense peak of the MFMA each
+        # part runs on, expressed as an fp32-equivalent TFLOP/s peak
+        t_floor = f32 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * f16 / (PEAK_FP16_TFLOPS * 1e12)
+        peak = (f16 + f32) / t_floor / 1e12
         achieved = flops / (mean_ms * 1e-3) / 1e12
         return {"kernel": name, "bound": "mfma", "achieved": round(achieved, 2),
                 "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "launches": n, "mean_ms": round(mean_ms, 4),
                 "per_launch": "%d samples x %.0f flop (fp32-equivalent)" % (B, flops / B),
-                "peak_basis": "MFMA floor: layer 1 %.0f flop/sample on f32 MFMA (%.1f TF) + layers "
-                              "2-3 %.0f flop/sample as 3 fp16 products (%.1f TF dense)"
-                              % (f1, PEAK_FP32_TFLOPS, f23, PEAK_FP16_TFLOPS),
+                "peak_basis": "MFMA floor: %.0f flop/sample as 3 fp16 products (%.1f TF dense) + "
+                              "%.0f flop/sample k-tail on f32 MFMA (%.1f TF)"
+                              % (f16, PEAK_FP16_TFLOPS, f32, PEAK_FP32_TFLOPS),
                 "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
     if name == "nfk_rqs_coupling":
         n_up = kw["size"] * (kw["dim"] - 1)
@@ -237,8 +242,9 @@ def main():
             "config": {"workload": args.workload + ": " + desc, "global_batch": world * B,
                        "per_gpu_batch": B, "parallelism": "dp%d (sample sharding)" % world,
                        "fused_layer_kernel": bool(config.USE_FUSED),
-                       "conditioner_arith": ("layer 1 f32 MFMA; layers 2-3 fp16 two-way split "
-                                             "(hi+lo, 3 MFMA products, fp32 accumulate)")
+                       "conditioner_arith": ("fp16 two-way split (hi+lo, 3 MFMA products, fp32 "
+                                             "accumulate, power-of-two pre-scaling); 4-feature "
+                                             "k-tail on f32 MFMA")
                        if (config.USE_FUSED and args.workload == "c3") else "f32 (rocBLAS)"},
             "roofline": rl,
             "cpu_baseline": cpu,

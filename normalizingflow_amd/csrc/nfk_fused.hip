@@ -46,7 +46,7 @@ NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, d
 using namespace nfk_fused;
 
 namespace nfk_fused {
-#define NFK_X(h) NFK_FUSED_K(NFK_FUSED_EXTERN, h)
+#define NFK_X(h, t) NFK_FUSED_K(NFK_FUSED_EXTERN, h, t)
 NFK_FUSED_KB(NFK_X)
 #undef NFK_X
 }  // namespace nfk_fused
@@ -59,27 +59,32 @@ struct PackArgs {
     Layout L;
 };
 
-// max |W| of layer 2 (hdr[0]) and of the output layer (hdr[1]) as uint bits
-// (non-negative floats order like their bit patterns)
+// max |W| of layers 1, 2, 3 into hdr[0..2] as uint bits (non-negative floats
+// order like their bit patterns)
 __global__ __launch_bounds__(256) void k_pack_max(PackArgs a) {
     const Layout& L = a.L;
-    const int64_t n2 = (int64_t)L.H * L.H, n3 = (int64_t)L.n_up * L.P * L.H;
-    float m2 = 0.0f, m3 = 0.0f;
-    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n2 + n3;
+    const int64_t n1 = (int64_t)L.H * L.n_lo, n2 = (int64_t)L.H * L.H, n3 = (int64_t)L.n_up * L.P * L.H;
+    float m1 = 0.0f, m2 = 0.0f, m3 = 0.0f;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n1 + n2 + n3;
          g += (int64_t)gridDim.x * blockDim.x) {
-        if (g < n2)
-            m2 = fmaxf(m2, fabsf(a.w2[g]));
+        if (g < n1)
+            m1 = fmaxf(m1, fabsf(a.w0[g]));
+        else if (g < n1 + n2)
+            m2 = fmaxf(m2, fabsf(a.w2[g - n1]));
         else
-            m3 = fmaxf(m3, fabsf(a.w4[g - n2]));
+            m3 = fmaxf(m3, fabsf(a.w4[g - n1 - n2]));
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
+        m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
         m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
         m3 = fmaxf(m3, __shfl_xor(m3, off, 64));
     }
     if ((threadIdx.x & 63) == 0) {
-        atomicMax(reinterpret_cast<unsigned int*>(a.out), __float_as_uint(m2));
-        atomicMax(reinterpret_cast<unsigned int*>(a.out) + 1, __float_as_uint(m3));
+        unsigned int* h = reinterpret_cast<unsigned int*>(a.out);
+        atomicMax(h, __float_as_uint(m1));
+        atomicMax(h + 1, __float_as_uint(m2));
+        atomicMax(h + 2, __float_as_uint(m3));
     }
 }
 
@@ -98,97 +103,116 @@ __device__ uint32_t f16_part_pair(float v0, float v1, int part) {
     return (uint32_t)__builtin_bit_cast(uint16_t, r0) | ((uint32_t)__builtin_bit_cast(uint16_t, r1) << 16);
 }
 
+// word of an f16-split record (f16 blocks, f32 tail groups, bias block) with
+// nt tiles; row(t, i) and the weight row pointer come from the caller's lambda
+template <class RowF, class BiasF>
+__device__ uint32_t pack_record_word(int blk, int wl, const Layout& L, int nt, float sc, float bsc,
+                                     RowF row_of, BiasF bias_of) {
+    const int nf = L.KBH * nt * 2, ntg = L.T1 ? (nt + 3) / 4 : 0;
+    if (blk < nf) {
+        const int part = blk & 1, idx = blk >> 1, kb = idx / nt, t = idx - kb * nt;
+        const int lane = wl >> 2, j = 2 * (wl & 3);
+        const int k0 = 32 * kb + 8 * (lane >> 4) + j;
+        const float* w = row_of(t, lane & 15);
+        float v0 = 0.0f, v1 = 0.0f;
+        if (w != nullptr) {
+            const int klim = L.T1 ? 32 * L.KBH : L.H;  // the tail step owns k >= 32 KBH
+            if (k0 < klim && k0 < L.H) v0 = w[k0] * sc;
+            if (k0 + 1 < klim && k0 + 1 < L.H) v1 = w[k0 + 1] * sc;
+        }
+        return f16_part_pair(v0, v1, part);
+    }
+    if (blk < nf + ntg) {  // f32 tail: lane l, component e of group g
+        const int g = blk - nf, lane = wl >> 2, e = wl & 3, t = 4 * g + e;
+        const int k = 32 * L.KBH + (lane >> 4);
+        float v = 0.0f;
+        if (t < nt && k < L.H) {
+            const float* w = row_of(t, lane & 15);
+            if (w != nullptr) v = w[k] * sc;
+        }
+        return __float_as_uint(v);
+    }
+    const int t = wl >> 4, i = wl & 15;  // bias block [tile][row]
+    return __float_as_uint(t < nt ? bias_of(t, i) * bsc : 0.0f);
+}
+
 // One thread per packed 32-bit word (layout described in nfk_fused_impl.h).
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     const Layout& L = a.L;
     const unsigned int* hdr = reinterpret_cast<const unsigned int*>(a.out);
-    const int s2 = scale_exp(__uint_as_float(hdr[0])), s3 = scale_exp(__uint_as_float(hdr[1]));
-    const float sc2 = ldexpf(1.0f, s2), sc3 = ldexpf(1.0f, s3);
+    const int s1 = scale_exp(__uint_as_float(hdr[0])), s2 = scale_exp(__uint_as_float(hdr[1])),
+              s3 = scale_exp(__uint_as_float(hdr[2]));
+    const float sc1 = ldexpf(1.0f, s1), sc2 = ldexpf(1.0f, s2), sc3 = ldexpf(1.0f, s3);
     const float bs2 = ldexpf(1.0f, s2 + 14), bs3 = ldexpf(1.0f, s3 + 14);
     uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < L.total;
          g += (int64_t)gridDim.x * blockDim.x) {
-        if (g < L.o_h1) {  // header: the unscale factors (words 0, 1 hold the maxima)
-            if (g == 2) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
-            if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
-            if (g >= 4) out[g] = 0;
+        if (g < L.o_h1) {  // header: the unscale factors (words 0-2 hold the maxima)
+            if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -s1));
+            if (g == 4) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
+            if (g == 5) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
+            if (g >= 6) out[g] = 0;
             continue;
         }
-        if (g < L.o_h2) {  // layer 1, fp32 fragments
+        const int kbh = L.KBH;
+        if (g < L.o_h2) {  // layer 1: KB1 f16 k-blocks over the n_lo inputs + unscaled bias
             const int64_t w = g - L.o_h1;
             const int blk = (int)(w >> 8), wl = (int)(w & 255);
-            float v = 0.0f;
-            if (blk < L.KS1 * L.TG1) {
-                const int lane = wl >> 2, e = wl & 3;
-                const int ks = blk / L.TG1, gg = blk - ks * L.TG1, t = 4 * gg + e;
-                const int f = hid_feature(t, lane & 15), k = 4 * ks + (lane >> 4);
-                if (t < L.HT && f < L.H && k < L.n_lo) v = a.w0[(int64_t)f * L.n_lo + k];
+            if (blk < L.KB1 * L.HT * 2) {
+                const int part = blk & 1, idx = blk >> 1, kb = idx / L.HT, t = idx - kb * L.HT;
+                const int lane = wl >> 2, j = 2 * (wl & 3);
+                const int f = hid_feature(t, lane & 15, kbh), k0 = 32 * kb + 8 * (lane >> 4) + j;
+                float v0 = 0.0f, v1 = 0.0f;
+                if (f < L.H) {
+                    if (k0 < L.n_lo) v0 = a.w0[(int64_t)f * L.n_lo + k0] * sc1;
+                    if (k0 + 1 < L.n_lo) v1 = a.w0[(int64_t)f * L.n_lo + k0 + 1] * sc1;
+                }
+                out[g] = f16_part_pair(v0, v1, part);
             } else {
-                const int t = wl >> 4, f = hid_feature(t, wl & 15);
-                if (t < L.HT && f < L.H) v = a.b0[f];
+                const int t = wl >> 4, f = hid_feature(t, wl & 15, kbh);
+                out[g] = __float_as_uint((t < L.HT && f < L.H) ? a.b0[f] : 0.0f);
             }
-            out[g] = __float_as_uint(v);
             continue;
         }
-        // fp16-split records: layer 2 or one output phase
-        int64_t w;
-        int NT, pbase = 0, chunk = -1;
-        if (g < L.o_w3) {
-            w = g - L.o_h2;
-            NT = L.HT;
-        } else {
-            const int64_t w3 = g - L.o_w3;
-            const int64_t bl = w3 >> 8;
-            chunk = (int)(bl / L.blk_chunk);
-            int b = (int)(bl - (int64_t)chunk * L.blk_chunk);
-            NT = L.K;
+        if (g < L.o_w3) {  // layer 2
+            const int64_t w = g - L.o_h2;
+            out[g] = pack_record_word(
+                (int)(w >> 8), (int)(w & 255), L, L.HT, sc2, bs2,
+                [&](int t, int i) -> const float* {
+                    const int f = hid_feature(t, i, kbh);
+                    return f < L.H ? a.w2 + (int64_t)f * L.H : nullptr;
+                },
+                [&](int t, int i) -> float {
+                    const int f = hid_feature(t, i, kbh);
+                    return f < L.H ? a.b2[f] : 0.0f;
+                });
+            continue;
+        }
+        // output layer: chunk, phase (W, H, D)
+        const int64_t w3 = g - L.o_w3;
+        const int64_t bl = w3 >> 8;
+        const int chunk = (int)(bl / L.blk_chunk);
+        int b = (int)(bl - (int64_t)chunk * L.blk_chunk);
+        int nt = L.K, pbase = 0;
+        if (b >= L.blk_w) {
+            b -= L.blk_w;
+            pbase = L.K;
             if (b >= L.blk_w) {
                 b -= L.blk_w;
-                pbase = L.K;
-                if (b >= L.blk_w) {
-                    b -= L.blk_w;
-                    pbase = 2 * L.K;
-                    NT = L.K - 1;
-                }
+                pbase = 2 * L.K;
+                nt = L.K - 1;
             }
-            w = (int64_t)b * 256 + (w3 & 255);
         }
-        const int blk = (int)(w >> 8), wl = (int)(w & 255);
-        const bool hidden = chunk < 0;
-        if (blk < L.KB * NT * 2) {
-            const int part = blk & 1, idx = blk >> 1, kb = idx / NT, t = idx - kb * NT;
-            const int lane = wl >> 2, j = 2 * (wl & 3);
-            const int k0 = 32 * kb + 8 * (lane >> 4) + j;
-            float v0 = 0.0f, v1 = 0.0f;
-            if (hidden) {
-                const int f = hid_feature(t, lane & 15);
-                if (f < L.H) {
-                    if (k0 < L.H) v0 = a.w2[(int64_t)f * L.H + k0] * sc2;
-                    if (k0 + 1 < L.H) v1 = a.w2[(int64_t)f * L.H + k0 + 1] * sc2;
-                }
-            } else {
-                const int jc = 16 * chunk + (lane & 15);
-                if (jc < L.n_up) {
-                    const float* row = a.w4 + ((int64_t)jc * L.P + pbase + t) * L.H;
-                    if (k0 < L.H) v0 = row[k0] * sc3;
-                    if (k0 + 1 < L.H) v1 = row[k0 + 1] * sc3;
-                }
-            }
-            out[g] = f16_part_pair(v0, v1, part);
-        } else {  // bias block: [tile][row], pre-scaled like the products
-            const int t = wl >> 4, i = wl & 15;
-            float v = 0.0f;
-            if (t < NT) {
-                if (hidden) {
-                    const int f = hid_feature(t, i);
-                    if (f < L.H) v = a.b2[f] * bs2;
-                } else {
-                    const int jc = 16 * chunk + i;
-                    if (jc < L.n_up) v = a.b4[(int64_t)jc * L.P + pbase + t] * bs3;
-                }
-            }
-            out[g] = __float_as_uint(v);
-        }
+        out[g] = pack_record_word(
+            b, (int)(w3 & 255), L, nt, sc3, bs3,
+            [&](int t, int i) -> const float* {
+                const int jc = 16 * chunk + i;
+                return jc < L.n_up ? a.w4 + ((int64_t)jc * L.P + pbase + t) * L.H : nullptr;
+            },
+            [&](int t, int i) -> float {
+                const int jc = 16 * chunk + i;
+                return jc < L.n_up ? a.b4[(int64_t)jc * L.P + pbase + t] : 0.0f;
+            });
     }
 }
 
@@ -198,11 +222,11 @@ bool shape_ok(int n_lo, int n_up, int H, int K) {
     if (lds_bytes(L) > (size_t)kLdsBytes) return false;
     if (L.K > 16 || L.HT > 16) return false;  // one bias block per record
     bool kb = false, kk = false;
-#define CHK_KB(h) kb |= (L.KB == h);
+#define CHK_KB(h, t) kb |= (L.KBH == h && L.T1 == t);
     NFK_FUSED_KB(CHK_KB)
 #undef CHK_KB
-#define CHK_K(h, k) kk |= (K == k);
-    NFK_FUSED_K(CHK_K, 0)
+#define CHK_K(h, t, k) kk |= (K == k);
+    NFK_FUSED_K(CHK_K, 0, 0)
 #undef CHK_K
     return kb && kk;
 }
@@ -226,7 +250,7 @@ extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float*
         return nfk_set_error("nfk_fused_nsf_pack: null pointer");
     PackArgs a{w0, b0, w2, b2, w4, b4, wpack, make_layout(n_lo, n_up, hidden, K)};
     hipStream_t st = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(wpack, 0, 2 * sizeof(float), st);
+    hipError_t e = hipMemsetAsync(wpack, 0, 3 * sizeof(float), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_pack_max, dim3(64), dim3(256), 0, st, a);
     int64_t g = (a.L.total + 255) / 256;
@@ -264,7 +288,7 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     a.batch = batch;
     a.n_lo = n_lo;
     a.n_up = n_up;
-    a.KS1 = L.KS1;
+    a.KB1 = L.KB1;
     a.NCH = L.NCH;
     a.mode = logdet_mode;
     a.slot_blocks = L.slot_blocks;
@@ -282,9 +306,9 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     const size_t lds = lds_bytes(L);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
-#define DISPATCH(h, k) \
-    if (L.KB == h && K == k) return launch_fused<h, k>(a, lds, inv, st);
-#define DISPATCH_KB(h) NFK_FUSED_K(DISPATCH, h)
+#define DISPATCH(h, t, k) \
+    if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, st);
+#define DISPATCH_KB(h, t) NFK_FUSED_K(DISPATCH, h, t)
     NFK_FUSED_KB(DISPATCH_KB)
 #undef DISPATCH_KB
 #undef DISPATCH

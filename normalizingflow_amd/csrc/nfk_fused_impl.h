@@ -21,28 +21,35 @@ constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 
 // Packed weights ("pack"): a header block, then a stream of phase records.
 // A record is a run of 1-KiB blocks (64 lanes x 16 B, one wave-instruction of
 // global_load_lds each) followed by one bias block (float[16 tiles][16 rows]).
-//   header (1 block): hdr[0] = max|W2|, hdr[1] = max|W3| (uint bits, from the
-//            pack's reduction), float hdr[2] = 2^-(s2+14), hdr[3] = 2^-(s3+14):
-//            the factors that undo the fp16 pre-scaling of layer 2 / 3 products
-//   layer 1 (fp32, v_mfma_f32_16x16x4_f32): KS1 k-steps x TG1 groups of 4
-//            tiles: lane l of block (ks, g) holds W1[f(4g+e, l&15)][4ks + l>>4],
-//            e = 0..3 (the float4 components)
-//   layer 2 and the output phases (fp16 split, v_mfma_f32_16x16x32_f16): KB
-//            k-blocks x NT tiles x {hi, lo}: lane l of block (kb, t, p) holds
-//            part p of 2^s W[row(t, l&15)][32kb + 8(l>>4) + j], j = 0..7, where
-//            hi = f16(v), lo = f16(v - hi) and 2^s puts max|W| in [2^14, 2^15)
+//   header (1 block): hdr[0..2] = max|W1|, max|W2|, max|W3| (uint bits, from
+//            the pack's reduction); float hdr[3] = 2^-s1, hdr[4] = 2^-(s2+14),
+//            hdr[5] = 2^-(s3+14): the factors undoing the fp16 pre-scaling
+//   f16 blocks (v_mfma_f32_16x16x32_f16, two-way split): k-blocks x NT tiles
+//            x {hi, lo}: lane l of block (kb, t, p) holds part p of
+//            2^s W[row(t, l&15)][32kb + 8(l>>4) + j], j = 0..7, where hi = f16(v),
+//            lo = f16(v - hi) and 2^s puts max|W| in [2^14, 2^15)
+//   f32 tail (T1 only: H = 32 KBH + R, 0 < R <= 4, v_mfma_f32_16x16x4_f32):
+//            one block per 4 tiles: lane l, component e holds
+//            2^s W[row(4g+e, l&15)][32 KBH + (l>>4)]
+//   layer 1: KB1 = ceil(n_lo/32) f16 k-blocks (x is scaled per wave), bias unscaled
+//   layer 2: KBH f16 k-blocks (+ f32 tail), bias pre-scaled by 2^(s2+14)
 //   per 16-coordinate chunk: W logits (K tiles), H logits (K tiles), D logits
-//            (K-1 tiles); row i of tile t = parameter t of coordinate 16c + i
-// Hidden feature permutation: row i of hidden tile t computes feature
+//            (K-1 tiles), same form; row i of tile t = parameter t of coordinate 16c+i
+// Hidden feature permutation: row i of hidden tile t < 2 KBH computes feature
 //   f(t, i) = 32(t>>1) + 8(i>>2) + 4(t&1) + (i&3),
 // so accumulator register r of tiles 2kb, 2kb+1 of lane l are exactly
 // elements j = r, 4 + r of the next product's B fragment for k-block kb
-// (k = 32kb + 8(l>>4) + j) -- activations never leave registers.
+// (k = 32kb + 8(l>>4) + j) -- activations never leave registers.  With a
+// tail, tile 2 KBH holds feature 32 KBH + q in register 0 of lane group q:
+// exactly the B operand (k = l>>4) of the f32 tail step.
 struct Layout {
-    int n_lo, n_up, H, K, P, KB, HT, KS1, TG1, NCH;
+    int n_lo, n_up, H, K, P, KBH, T1, HT, KB1, NCH;
     int blk_h1, blk_h2, blk_w, blk_d, blk_chunk, slot_blocks;
     int64_t o_h1, o_h2, o_w3, total;  // offsets / size in floats
 };
+
+// blocks of an f16-split record with nt tiles (+ f32 tail groups, + bias)
+inline int rec_blocks(int kbh, int t1, int nt) { return kbh * nt * 2 + (t1 ? (nt + 3) / 4 : 0) + 1; }
 
 inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     Layout L;
@@ -51,15 +58,24 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     L.H = H;
     L.K = K;
     L.P = 3 * K - 1;
-    L.KB = (H + 31) / 32;
-    L.HT = 2 * L.KB;
-    L.KS1 = (n_lo + 3) / 4;
-    L.TG1 = (L.HT + 3) / 4;
+    const int kbf = H / 32, rem = H - 32 * kbf;
+    if (rem == 0) {
+        L.KBH = kbf;
+        L.T1 = 0;
+    } else if (rem <= 4 && kbf >= 1) {
+        L.KBH = kbf;
+        L.T1 = 1;
+    } else {
+        L.KBH = kbf + 1;
+        L.T1 = 0;
+    }
+    L.HT = 2 * L.KBH + L.T1;
+    L.KB1 = (n_lo + 31) / 32;
     L.NCH = (n_up + 15) / 16;
-    L.blk_h1 = L.KS1 * L.TG1 + 1;
-    L.blk_h2 = L.KB * L.HT * 2 + 1;
-    L.blk_w = L.KB * K * 2 + 1;
-    L.blk_d = L.KB * (K - 1) * 2 + 1;
+    L.blk_h1 = L.KB1 * L.HT * 2 + 1;
+    L.blk_h2 = rec_blocks(L.KBH, L.T1, L.HT);
+    L.blk_w = rec_blocks(L.KBH, L.T1, K);
+    L.blk_d = rec_blocks(L.KBH, L.T1, K - 1);
     L.blk_chunk = 2 * L.blk_w + L.blk_d;
     L.slot_blocks = L.blk_h1;
     if (L.blk_h2 > L.slot_blocks) L.slot_blocks = L.blk_h2;
@@ -73,9 +89,9 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
 }
 
 // Row lengths of one wave's x tile: 16 rows of the lower coordinates (padded
-// to the layer-1 k-steps), later overwritten by 16 rows of the upper ones
+// to the layer-1 k-blocks), later overwritten by 16 rows of the upper ones
 // (padded to 4).  Both are filled by per-lane LDS-DMA gathers of 64 dwords.
-inline int x_lo_row(const Layout& L) { return 4 * L.KS1; }
+inline int x_lo_row(const Layout& L) { return 32 * L.KB1; }
 inline int x_up_row(const Layout& L) { return (L.n_up + 3) & ~3; }
 inline int x_tile_floats(const Layout& L) {
     return 16 * (x_lo_row(L) > x_up_row(L) ? x_lo_row(L) : x_up_row(L));
@@ -88,9 +104,10 @@ inline size_t lds_bytes(const Layout& L) {
     return 2 * (size_t)L.slot_blocks * 1024 + maps + (size_t)kWaves * x_tile_floats(L) * sizeof(float);
 }
 
-// hidden feature computed by row i (0..15) of hidden tile t
-__host__ __device__ inline int hid_feature(int t, int i) {
-    return 32 * (t >> 1) + 8 * (i >> 2) + 4 * (t & 1) + (i & 3);
+// hidden feature computed by row i (0..15) of hidden tile t (>= H: padding)
+__host__ __device__ inline int hid_feature(int t, int i, int kbh) {
+    if (t < 2 * kbh) return 32 * (t >> 1) + 8 * (i >> 2) + 4 * (t & 1) + (i & 3);
+    return (i & 3) == 0 ? 32 * kbh + (i >> 2) : (1 << 20);
 }
 
 struct FusedArgs {
@@ -101,7 +118,7 @@ struct FusedArgs {
     float* logdet;
     int32_t* status;
     int64_t ldx, ldz, batch;
-    int32_t n_lo, n_up, KS1, NCH, mode, slot_blocks, xtile, xup;
+    int32_t n_lo, n_up, KB1, NCH, mode, slot_blocks, xtile, xup;
     int32_t blk_h1, blk_h2, blk_w, blk_d, blk_chunk;
     int32_t o_h1, o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
     NfkSplineConst c;
@@ -210,18 +227,29 @@ __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, 
     }
 }
 
-// acc[t] = bias + 2^s W[tile t] . act^T over KB k-blocks of 32 in the fp16
-// split: three MFMAs per (tile, k-block), small terms first.  A fragments
-// come from the LDS slot PF tiles ahead of their MFMAs.
-template <int KB, int NT>
-__device__ __forceinline__ void gemm_h(const h8 (&bh)[KB], const h8 (&bl)[KB], const float4* slot,
-                                       int lane, f32x4 (&acc)[NT]) {
-    constexpr int N = KB * NT;
+// acc[t] = bias + 2^s W[tile t] . act^T: KBH k-blocks of 32 in the fp16
+// split (three MFMAs per (tile, k-block), small terms first; A fragments read
+// from the LDS slot PF tiles ahead of their MFMAs), then the f32 tail step.
+template <int KBH, bool T1, int NT>
+__device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH], float btail,
+                                       const float4* slot, int lane, f32x4 (&acc)[NT]) {
+    constexpr int N = KBH * NT;
+    constexpr int NTG = T1 ? (NT + 3) / 4 : 0;
     constexpr int PF = 2;
     const int q = lane >> 4;
-    const float4* bias = slot + N * 2 * 64;
+    const float4* tail = slot + N * 2 * 64;
+    const float4* bias = tail + NTG * 64;
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = as_f32x4(bias[t * 4 + q]);
+    if constexpr (T1) {
+#pragma unroll
+        for (int g = 0; g < NTG; ++g) {
+            const float4 w = tail[g * 64 + lane];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (4 * g + e < NT) acc[4 * g + e] = mfma32(pick4(w, e), btail, acc[4 * g + e]);
+        }
+    }
     float4 ring[PF + 1][2];
 #pragma unroll
     for (int i = 0; i < PF && i < N; ++i) {
@@ -242,6 +270,19 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KB], const h8 (&bl)[KB], c
         acc[t] = mfma16(ahi, bl[kb], acc[t]);
         acc[t] = mfma16(ahi, bh[kb], acc[t]);
     }
+}
+
+// activations of a hidden layer -> B operands of the next product
+template <int KBH, bool T1, int HT>
+__device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[KBH], h8 (&bl)[KBH],
+                                             float& btail) {
+#pragma unroll
+    for (int t = 0; t < 2 * KBH; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[t][r] = tanh_scaled(h[t][r], c2);
+#pragma unroll
+    for (int kb = 0; kb < KBH; ++kb) split_act<HT>(h, kb, bh[kb], bl[kb]);
+    btail = T1 ? tanh_scaled(h[HT - 1][0], c2) : 0.0f;  // registers 1-3 of the tail tile are padding
 }
 
 // Knot phase epilogue: for the 4 coordinates of this lane, turn the K logits
@@ -310,10 +351,9 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
 // p+1 is already in the other slot and phase p+2's copy is issued right after
 // the barrier that ends phase p.  One barrier per phase; everything else is
 // wave-local.
-template <int KB, int K, bool INV>
+template <int KBH, bool T1, int K, bool INV>
 __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
-    constexpr int HT = 2 * KB;
-    constexpr int TG1 = (HT + 3) / 4;
+    constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -326,8 +366,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     int32_t* m_up_out = m_up_in + a.n_up;
     int32_t* m_lo_in = m_up_out + a.n_up;
     int32_t* m_lo_out = m_lo_in + a.n_lo;
-    const int XL = 4 * a.KS1;  // lower-x tile row length (n_lo padded to the k-steps)
-    const int XU = a.xup;      // upper-x tile row length (n_up padded to 4)
+    const int XL = 32 * a.KB1;  // lower-x tile row length (n_lo padded to the k-blocks)
+    const int XU = a.xup;       // upper-x tile row length (n_up padded to 4)
     float* xt = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xtile;
     const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
@@ -347,31 +387,62 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         m_lo_out[i] = a.lo_out[i];
     }
     // factors undoing the fp16 pre-scaling (pack header)
-    const float un2 = pk[2], un3 = pk[3];
+    const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
     __syncthreads();  // maps visible (no DMA in flight yet)
     stage_record(pk + a.o_h1, a.blk_h1, slot0, wid, lane);
     if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xt, lane);
     dma_barrier();  // layer-1 record and lower-x tiles landed
     stage_record(pk + a.o_h2, a.blk_h2, slot1, wid, lane);
 
-    // ---- layer 1 (slot 0, fp32 MFMA): h1^T = tanh(W1 . lower^T + b1)
+    // ---- layer 1 (slot 0, fp16 split): h1^T = tanh(W1 . lower^T + b1).  x has
+    // any magnitude, so each wave scales its tile by a power of two 2^sx that
+    // puts max|x| just under 2^14 before the split; acc = 2^(s1+sx) W1 x.
     f32x4 h1[HT];
     {
+        float mx = 0.0f;
+        for (int kb = 0; kb < a.KB1; ++kb) {
+            const float4* xr = reinterpret_cast<const float4*>(xt + sl * XL + 32 * kb + 8 * q);
+            const float4 u = xr[0], v = xr[1];
+            mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))),
+                                 fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        int ex = 0;
+        if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
+        const float sx = ldexpf(1.0f, 14 - ex), unx = ldexpf(un1, ex - 14);
+#pragma unroll
+        for (int t = 0; t < HT; ++t) h1[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         const float4* s = slot0;
-        const float4* bias = s + a.KS1 * TG1 * 64;
+        for (int kb = 0; kb < a.KB1; ++kb) {
+            const float4* xr = reinterpret_cast<const float4*>(xt + sl * XL + 32 * kb + 8 * q);
+            const float4 u = xr[0], v = xr[1];
+            const float xv8[8] = {u.x * sx, u.y * sx, u.z * sx, u.w * sx, v.x * sx, v.y * sx, v.z * sx, v.w * sx};
+            h8 xh, xlo;
 #pragma unroll
-        for (int t = 0; t < HT; ++t) h1[t] = as_f32x4(bias[t * 4 + q]);
-        for (int ks = 0; ks < a.KS1; ++ks) {
-            const float bf = xt[sl * XL + 4 * ks + q];
-#pragma unroll
-            for (int g = 0; g < TG1; ++g) {
-                const float4 w = s[(ks * TG1 + g) * 64 + lane];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int t = 4 * g + e;
-                    if (t < HT) h1[t] = mfma32(pick4(w, e), bf, h1[t]);
-                }
+            for (int j = 0; j < 8; ++j) {
+                const _Float16 hh = (_Float16)xv8[j];
+                xh[j] = hh;
+                xlo[j] = (_Float16)(xv8[j] - (float)hh);
             }
+#pragma unroll
+            for (int t = 0; t < HT; ++t) {
+                const h8 ahi = __builtin_bit_cast(h8, s[((kb * HT + t) * 2) * 64 + lane]);
+                const h8 alo = __builtin_bit_cast(h8, s[((kb * HT + t) * 2 + 1) * 64 + lane]);
+                h1[t] = mfma16(alo, xh, h1[t]);
+                h1[t] = mfma16(ahi, xlo, h1[t]);
+                h1[t] = mfma16(ahi, xh, h1[t]);
+            }
+        }
+        // unscale and add the (unscaled) bias before the activation
+        const float4* bias = s + a.KB1 * HT * 2 * 64;
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+            const float4 bv = bias[t * 4 + q];
+            h1[t][0] = __builtin_fmaf(h1[t][0], unx, bv.x);
+            h1[t][1] = __builtin_fmaf(h1[t][1], unx, bv.y);
+            h1[t][2] = __builtin_fmaf(h1[t][2], unx, bv.z);
+            h1[t][3] = __builtin_fmaf(h1[t][3], unx, bv.w);
         }
     }
     // identity-copied (lower) coordinates: kept in registers and written after
@@ -379,11 +450,11 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     // when they do not fit: n_lo > 32); then the tile takes the upper coordinates
     constexpr int kLoRegs = 8;
     float lo_keep[kLoRegs];
-    const bool lo_late = a.KS1 <= kLoRegs;  // 16 n_lo <= 64 kLoRegs
+    const bool lo_late = a.KB1 == 1;  // 16 x 32 = 64 lanes x kLoRegs
 #pragma unroll
     for (int m = 0; m < kLoRegs; ++m) {
         const int i = lane + 64 * m, row = i / XL, qq = i - row * XL;
-        lo_keep[m] = (lo_late && m < a.KS1) ? xt[row * XL + qq] : 0.0f;
+        lo_keep[m] = lo_late ? xt[row * XL + qq] : 0.0f;
     }
     if (!lo_late) {
         for (int i = lane; i < 16 * a.n_lo; i += 64) {
@@ -393,16 +464,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile reads done before the DMA overwrites it
     if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xt, lane);
-    h8 bh[KB], bl[KB];
-    {
-        const float c2 = -2.0f * kL2E;
-#pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) h1[t][r] = tanh_scaled(h1[t][r], c2);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) split_act<HT>(h1, kb, bh[kb], bl[kb]);
-    }
+    h8 bh[KBH], bl[KBH];
+    float btail;
+    act_operands<KBH, T1, HT>(h1, -2.0f * kL2E, bh, bl, btail);
     dma_barrier();  // slot 0 free; layer-2 record and upper-x tiles landed
     const float* w3 = pk + a.o_w3;
     // execution order of the three records of a chunk: searched knots, other knots, derivatives
@@ -412,14 +476,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     // ---- layer 2 (slot 1, fp16 split): h2^T = tanh(W2 . h1^T + b2)
     {
         f32x4 h2[HT];
-        gemm_h<KB, HT>(bh, bl, slot1, lane, h2);
-        const float c2 = -2.0f * kL2E * un2;
-#pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) h2[t][r] = tanh_scaled(h2[t][r], c2);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) split_act<HT>(h2, kb, bh[kb], bl[kb]);
+        gemm_h<KBH, T1, HT>(bh, bl, btail, slot1, lane, h2);
+        act_operands<KBH, T1, HT>(h2, -2.0f * kL2E * un2, bh, bl, btail);
     }
     dma_barrier();  // slot 1 free, chunk-0 record A landed
     stage_record(w3 + offB * 256, a.blk_w, slot1, wid, lane);
@@ -449,7 +507,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         // ---- record A (slot sA): searched knots (widths forward / heights inverse)
         {
             f32x4 acc[K];
-            gemm_h<KB, K>(bh, bl, sA, lane, acc);
+            gemm_h<KBH, T1, K>(bh, bl, btail, sA, lane, acc);
             if (INV)
                 knot_phase<K, true, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
             else
@@ -461,7 +519,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         // ---- record B (slot sB): the other knots, selected at the bin
         {
             f32x4 acc[K];
-            gemm_h<KB, K>(bh, bl, sB, lane, acc);
+            gemm_h<KBH, T1, K>(bh, bl, btail, sB, lane, acc);
             if (INV)
                 knot_phase<K, false, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
             else
@@ -473,7 +531,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         // ---- record C (slot sA): derivatives of the bin, evaluate, log|det|
         {
             f32x4 accd[DN];
-            gemm_h<KB, DN>(bh, bl, sA, lane, accd);
+            gemm_h<KBH, T1, DN>(bh, bl, btail, sA, lane, accd);
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -554,7 +612,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 #pragma unroll
         for (int m = 0; m < kLoRegs; ++m) {
             const int i = lane + 64 * m, row = i / XL, qq = i - row * XL;
-            if (m < a.KS1 && row < nrows && qq < a.n_lo) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = lo_keep[m];
+            if (row < nrows && qq < a.n_lo) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = lo_keep[m];
         }
     }
     {
@@ -575,31 +633,32 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     }
 }
 
-template <int KB, int K>
+template <int KBH, int T1, int K>
 int launch_fused(const FusedArgs& a, size_t lds, bool inv, hipStream_t st) {
     const int64_t per_block = (int64_t)kWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
     if (inv)
-        hipLaunchKernelGGL((k_fused_nsf<KB, K, true>), dim3((unsigned)blocks), dim3(64 * kWaves), lds,
-                           st, a);
+        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true>), dim3((unsigned)blocks), dim3(64 * kWaves),
+                           lds, st, a);
     else
-        hipLaunchKernelGGL((k_fused_nsf<KB, K, false>), dim3((unsigned)blocks), dim3(64 * kWaves),
+        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, false>), dim3((unsigned)blocks), dim3(64 * kWaves),
                            lds, st, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 
-// explicit instantiation: definitions live in nfk_fused_kb<KB>.hip (one TU
+// explicit instantiation: definitions live in nfk_fused_kb<KBH>.hip (one TU
 // per hidden k-block count so make -j compiles them in parallel); nfk_fused.hip
 // sees only the extern declarations.
-#define NFK_FUSED_INSTANCE(KB, K) \
-    template int launch_fused<KB, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
-#define NFK_FUSED_EXTERN(KB, K) \
-    extern template int launch_fused<KB, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
+#define NFK_FUSED_INSTANCE(KBH, T1, K) \
+    template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
+#define NFK_FUSED_EXTERN(KBH, T1, K) \
+    extern template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
 
-// supported hidden widths: KB = ceil(H/32) k-blocks of 32 (H <= 128)
-#define NFK_FUSED_KB(X) X(1) X(2) X(3) X(4)
-#define NFK_FUSED_K(X, KB) X(KB, 4) X(KB, 5) X(KB, 6) X(KB, 8) X(KB, 10)
+// hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f32 tail step of <= 4
+// features (H = 32 KBH + 1..4); H <= 132
+#define NFK_FUSED_KB(X) X(1, 0) X(1, 1) X(2, 0) X(2, 1) X(3, 0) X(3, 1) X(4, 0) X(4, 1)
+#define NFK_FUSED_K(X, KBH, T1) X(KBH, T1, 4) X(KBH, T1, 5) X(KBH, T1, 6) X(KBH, T1, 8) X(KBH, T1, 10)
 
 }  // namespace nfk_fused
