@@ -302,7 +302,22 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     a.o_h1 = (int32_t)L.o_h1;
     a.o_h2 = (int32_t)L.o_h2;
     a.o_w3 = (int32_t)L.o_w3;
-    a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+    {
+        // NSF_CL's spline constants (flows.py:236-237 defaults), evaluated like the
+        // reference's Python scalars (nfk_make_const), folded for the fixed-point knots
+        const NfkSplineConst sc =
+            nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+        const float two30 = 1073741824.0f;
+        a.c.lo = sc.lo;
+        a.c.hi = sc.hi;
+        a.c.sp30 = sc.span / two30;
+        a.c.inv30 = two30 / sc.span;
+        a.c.fb30 = sc.fw * two30;
+        a.c.mb30 = sc.min_w * two30;
+        a.c.m2b = sc.m2b;
+        a.c.min_d = sc.min_d;
+        a.c.d_edge = sc.d_edge;
+    }
     const size_t lds = lds_bytes(L);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;

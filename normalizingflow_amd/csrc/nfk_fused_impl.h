@@ -10,9 +10,13 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
+#ifndef NFK_WAVES
+#define NFK_WAVES 8
+#endif
+
 namespace nfk_fused {
 
-constexpr int kWaves = 8;  // waves per workgroup (two per SIMD), 16 samples each
+constexpr int kWaves = NFK_WAVES;  // waves per workgroup (two per SIMD by default), 16 samples each
 constexpr int kMaxD = 128;
 constexpr int kLdsBytes = 160 * 1024;
 constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 2^14 <= 2^14)
@@ -110,6 +114,18 @@ __host__ __device__ inline int hid_feature(int t, int i, int kbh) {
     return (i & 3) == 0 ? 32 * kbh + (i >> 2) : (1 << 20);
 }
 
+// Spline constants of NSF_CL (flows.py:236: left = bottom = -B, right = top = B,
+// default min bin width = height = derivative = 1e-3), one set for x and y.
+struct FusedConst {
+    float lo, hi;     // -B, B (knot range and the tails' inside test)
+    float sp30;       // 2B * 2^-30: fixed-point prefix -> edge offset
+    float inv30;      // 2^30 / 2B: x -> fixed-point domain
+    float fb30, mb30; // (1 - min_bin K) 2^30, min_bin 2^30: floored fractions in fixed point
+    float m2b;        // 2B log2(e): second softmax (nfk_knots_nsf_lean)
+    float min_d;      // min_derivative
+    float d_edge;     // min_d + softplus(pad constant): boundary derivative
+};
+
 struct FusedArgs {
     const float* x;
     const float* pack;
@@ -121,7 +137,7 @@ struct FusedArgs {
     int32_t n_lo, n_up, KB1, NCH, mode, slot_blocks, xtile, xup;
     int32_t blk_h1, blk_h2, blk_w, blk_d, blk_chunk;
     int32_t o_h1, o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
-    NfkSplineConst c;
+    FusedConst c;
 };
 
 __device__ __forceinline__ f32x4 mfma32(float a, float b, f32x4 c) {
@@ -286,15 +302,17 @@ __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[
 }
 
 // Knot phase epilogue: for the 4 coordinates of this lane, turn the K logits
-// of register r into knots (NSF_CL's 2B softmax, then RQS's softmax, floor and
-// cumsum: nfk_knots_nsf_lean; the logits still carry the 2^(s3+14) product
-// scale, which l2e absorbs) and keep (edge_k, size_k) of the bin.  The
-// searched phase finds the bin by a running select over the interior edges
-// (edges are strictly increasing, so the last edge <= x is the bin of
-// utils.py:20-25 for every x inside the tails); the other phase selects by k.
-template <int K, bool SEARCH, bool Y>
+// of register r into fixed-point knot prefixes (NSF_CL's 2B softmax, then
+// RQS's softmax, floor and cumsum: nfk_prefix_nsf_lean; the logits still carry
+// the 2^(s3+14) product scale, which l2e absorbs) and keep (edge_k, size_k) of
+// the bin.  The searched phase finds the bin in the integer domain:
+// floor((x - lo) 2^30 / 2B) >= pre[j] counts the interior edges <= x, which is
+// the bin of utils.py:20-25 for every x inside the tails (edges are strictly
+// increasing; elements within an ulp of an edge may take the neighbouring
+// bin, where the C1 spline agrees); the other phase selects by k.
+template <int K, bool SEARCH>
 __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
-                                           const NfkSplineConst& c, float l2e, int (&kb)[4],
+                                           const FusedConst& c, float l2e, int (&kb)[4],
                                            float (&ek)[4], float (&sk)[4]) {
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
@@ -310,23 +328,24 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
 #endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        float u[K], edge[K + 1];
+        float u[K];
+        int pre[K];
 #pragma unroll
         for (int t = 0; t < K; ++t) u[t] = acc[t][r];
-        if (Y)
-            nfk_knots_nsf_lean<K>(u, l2e, c.ylo, c.yhi, c.yspan, c.min_h, c.fh, c.m2b, edge);
-        else
-            nfk_knots_nsf_lean<K>(u, l2e, c.lo, c.hi, c.span, c.min_w, c.fw, c.m2b, edge);
-        float e = edge[0], e1 = edge[1];
-        int k = 0;
+        nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
+        int p0 = 0, p1 = pre[1 < K ? 1 : 0], k = 0;
+        const int xi = __float2int_rd(__builtin_fmaf(xv[r], c.inv30, -c.lo * c.inv30));
 #pragma unroll
         for (int j = 1; j < K; ++j) {
-            const bool ge = SEARCH ? (xv[r] >= edge[j]) : (kb[r] >= j);
-            e = ge ? edge[j] : e;
-            e1 = ge ? edge[j + 1] : e1;
+            const bool ge = SEARCH ? (xi >= pre[j]) : (kb[r] >= j);
+            p0 = ge ? pre[j] : p0;
+            if (j + 1 < K) p1 = ge ? pre[j + 1] : p1;
             if (SEARCH) k += ge ? 1 : 0;
         }
         if (SEARCH) kb[r] = k;
+        const int kk = kb[r];
+        const float e = __builtin_fmaf(c.sp30, (float)p0, c.lo);
+        const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, c.lo);
         ek[r] = e;
         sk[r] = e1 - e;
     }
@@ -372,7 +391,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
-    const NfkSplineConst& c = a.c;
+    const FusedConst& c = a.c;
     const float* pk = a.pack;
     const bool row_ok = sl < nrows;
 
@@ -509,9 +528,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
             f32x4 acc[K];
             gemm_h<KBH, T1, K>(bh, bl, btail, sA, lane, acc);
             if (INV)
-                knot_phase<K, true, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
+                knot_phase<K, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
             else
-                knot_phase<K, true, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
+                knot_phase<K, true>(acc, xv, c, l2e3, kb, cw_k, w_k);
         }
         NFK_PHASE_BARRIER();
         NFK_STAGE(wc + offC * 256, a.blk_d, sA, wid, lane);
@@ -521,9 +540,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
             f32x4 acc[K];
             gemm_h<KBH, T1, K>(bh, bl, btail, sB, lane, acc);
             if (INV)
-                knot_phase<K, false, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
+                knot_phase<K, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
             else
-                knot_phase<K, false, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
+                knot_phase<K, false>(acc, xv, c, l2e3, kb, ch_k, h_k);
         }
         NFK_PHASE_BARRIER();
         if (ch + 1 < a.NCH) NFK_STAGE(wn + offA * 256, a.blk_w, sB, wid, lane);

@@ -137,6 +137,37 @@ __device__ __forceinline__ void nfk_knots_nsf_lean(const float (&raw)[K], float 
     edge[K] = hi;
 }
 
+// Same knots kept as 2^-30 fixed-point prefix sums: pre[j] = sum_{i<j} of
+// the floored fractions (pre[0] = 0); edge j = fma(span 2^-30, (float)pre[j], lo)
+// for j < K and the pinned right end for j = K.  The fused kernel searches
+// the bin in this integer domain and converts only the two edges it uses.
+template <int K>
+__device__ __forceinline__ void nfk_prefix_nsf_lean(const float (&raw)[K], float l2e, float m2b,
+                                                    float fb30, float mb30, int (&pre)[K]) {
+    float m = raw[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) m = fmaxf(m, raw[i]);
+    const float mL = m * l2e;
+    float e[K];
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(raw[i], l2e, -mL));
+        s = i == 0 ? e[0] : s + e[i];
+    }
+    const float q = m2b * __builtin_amdgcn_rcpf(s);
+    float s2 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(e[i], q, -m2b));
+        s2 = i == 0 ? e[0] : s2 + e[i];
+    }
+    const float f30 = fb30 * __builtin_amdgcn_rcpf(s2);
+    pre[0] = 0;
+#pragma unroll
+    for (int i = 0; i < K - 1; ++i) pre[i + 1] = pre[i] + (int)__builtin_fmaf(e[i], f30, mb30);
+}
+
 // min_d + softplus(softplus(v)) of NSF_CL + RQS (flows.py:235, utils.py:82) in
 // one step: e^softplus(v) = 1 + e^v, so softplus(softplus(v)) = log(2 + e^v);
 // torch's threshold 20 passes v through both softplus calls unchanged.
