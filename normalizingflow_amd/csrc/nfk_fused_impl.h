@@ -13,6 +13,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef NFK_WAVES
 #define NFK_WAVES 8
 #endif
+#ifndef NFK_PINGPONG
+#define NFK_PINGPONG 0  // 1: waves 4-7 trail waves 0-3 by half a phase (see k_fused_nsf)
+#endif
 
 namespace nfk_fused {
 
@@ -92,16 +95,15 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     return L;
 }
 
-// Row lengths of one wave's x tile: 16 rows of the lower coordinates (padded
-// to the layer-1 k-blocks), later overwritten by 16 rows of the upper ones
-// (padded to 4).  Both are filled by per-lane LDS-DMA gathers of 64 dwords.
+// Each wave owns two x tiles, filled in the prologue by per-lane LDS-DMA
+// gathers of 64 dwords: 16 rows of the lower coordinates (padded to the
+// layer-1 k-blocks) and 16 rows of the upper ones (padded to 4).  The upper
+// tile also collects the transformed values, so z is written once at the end.
 inline int x_lo_row(const Layout& L) { return 32 * L.KB1; }
 inline int x_up_row(const Layout& L) { return (L.n_up + 3) & ~3; }
-inline int x_tile_floats(const Layout& L) {
-    return 16 * (x_lo_row(L) > x_up_row(L) ? x_lo_row(L) : x_up_row(L));
-}
+inline int x_tile_floats(const Layout& L) { return 16 * (x_lo_row(L) + x_up_row(L)); }
 
-// dynamic LDS bytes: two record slots, the index maps, one x tile per wave
+// dynamic LDS bytes: two record slots, the index maps, the x tiles of every wave
 inline size_t lds_bytes(const Layout& L) {
     const int D = L.n_lo + L.n_up;
     const size_t maps = (size_t)((2 * D + 3) / 4) * 16;
@@ -177,7 +179,7 @@ __device__ __forceinline__ void dma16(const float* gsrc, uint32_t lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
                  "global_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(saved)
-                 : "s"(lds), "v"(gsrc)
+                 : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(gsrc)
                  : "memory");
 }
 
@@ -186,7 +188,7 @@ __device__ __forceinline__ void dma4(const float* gsrc, uint32_t lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
                  "global_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(saved)
-                 : "s"(lds), "v"(gsrc)
+                 : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(gsrc)
                  : "memory");
 }
 
@@ -243,17 +245,20 @@ __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, 
     }
 }
 
-// acc[t] = bias + 2^s W[tile t] . act^T: KBH k-blocks of 32 in the fp16
-// split (three MFMAs per (tile, k-block), small terms first; A fragments read
-// from the LDS slot PF tiles ahead of their MFMAs), then the f32 tail step.
+// acc[t] = bias + 2^s W[tile t] . act^T: the f32 tail step, then KBH k-blocks
+// of 32 in the fp16 split, three MFMAs per (tile, k-block), small terms first.
+// Tiles go in pairs whose MFMAs alternate accumulators: a dependent MFMA
+// chain blocks the SIMD partner wave's VALU, two interleaved chains let it
+// overlap (tools/ubench_coexec2.hip, modes 5-6).  A fragments of the next
+// pair are read from the LDS slot while the current pair's MFMAs run.
 template <int KBH, bool T1, int NT>
 __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH], float btail,
                                        const float4* slot, int lane, f32x4 (&acc)[NT]) {
-    constexpr int N = KBH * NT;
+    constexpr int NPR = (NT + 1) / 2;  // tile pairs (the last may be a single tile)
+    constexpr int N = KBH * NPR;
     constexpr int NTG = T1 ? (NT + 3) / 4 : 0;
-    constexpr int PF = 2;
     const int q = lane >> 4;
-    const float4* tail = slot + N * 2 * 64;
+    const float4* tail = slot + KBH * NT * 2 * 64;
     const float4* bias = tail + NTG * 64;
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = as_f32x4(bias[t * 4 + q]);
@@ -266,25 +271,41 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
                 if (4 * g + e < NT) acc[4 * g + e] = mfma32(pick4(w, e), btail, acc[4 * g + e]);
         }
     }
-    float4 ring[PF + 1][2];
+    // blocks of pair i = (kb, pr): tile t0 = 2 pr {hi, lo}, tile t0 + 1 {hi, lo}
+    auto blk = [](int i, int j) {  // j = 0..3
+        const int kb = i / NPR, pr = i - kb * NPR;
+        return (kb * NT + 2 * pr) * 2 + j;
+    };
+    float4 ring[2][4];
 #pragma unroll
-    for (int i = 0; i < PF && i < N; ++i) {
-        ring[i][0] = slot[(2 * i) * 64 + lane];
-        ring[i][1] = slot[(2 * i + 1) * 64 + lane];
-    }
+    for (int j = 0; j < 4; ++j)
+        if (2 * (0 % NPR) + (j >> 1) < NT) ring[0][j] = slot[blk(0, j) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        if (i + PF < N) {
-            ring[(i + PF) % (PF + 1)][0] = slot[(2 * (i + PF)) * 64 + lane];
-            ring[(i + PF) % (PF + 1)][1] = slot[(2 * (i + PF) + 1) * 64 + lane];
+        const int kb = i / NPR, pr = i - kb * NPR, t0 = 2 * pr;
+        const bool two = t0 + 1 < NT;
+        if (i + 1 < N) {
+            const int pn = (i + 1) % NPR;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (2 * pn + (j >> 1) < NT) ring[(i + 1) & 1][j] = slot[blk(i + 1, j) * 64 + lane];
         }
         __builtin_amdgcn_sched_barrier(0);
-        const int kb = i / NT, t = i - kb * NT;
-        const h8 ahi = __builtin_bit_cast(h8, ring[i % (PF + 1)][0]);
-        const h8 alo = __builtin_bit_cast(h8, ring[i % (PF + 1)][1]);
-        acc[t] = mfma16(alo, bh[kb], acc[t]);
-        acc[t] = mfma16(ahi, bl[kb], acc[t]);
-        acc[t] = mfma16(ahi, bh[kb], acc[t]);
+        const float4* r = ring[i & 1];
+        const h8 ahi0 = __builtin_bit_cast(h8, r[0]), alo0 = __builtin_bit_cast(h8, r[1]);
+        if (two) {
+            const h8 ahi1 = __builtin_bit_cast(h8, r[2]), alo1 = __builtin_bit_cast(h8, r[3]);
+            acc[t0] = mfma16(alo0, bh[kb], acc[t0]);
+            acc[t0 + 1] = mfma16(alo1, bh[kb], acc[t0 + 1]);
+            acc[t0] = mfma16(ahi0, bl[kb], acc[t0]);
+            acc[t0 + 1] = mfma16(ahi1, bl[kb], acc[t0 + 1]);
+            acc[t0] = mfma16(ahi0, bh[kb], acc[t0]);
+            acc[t0 + 1] = mfma16(ahi1, bh[kb], acc[t0 + 1]);
+        } else {
+            acc[t0] = mfma16(alo0, bh[kb], acc[t0]);
+            acc[t0] = mfma16(ahi0, bl[kb], acc[t0]);
+            acc[t0] = mfma16(ahi0, bh[kb], acc[t0]);
+        }
     }
 }
 
@@ -351,31 +372,80 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
     }
 }
 
-// Ablation hooks for diagnostic builds (tools/ablate.sh; never in the product
-// build): NFK_ABL_NOSTAGE drops the chunk-loop record copies, NFK_ABL_NOBAR the
-// chunk-loop barriers, NFK_ABL_NOEPI replaces the spline epilogue by a sum.
+// Ablation hooks for diagnostic builds (tools/ablate_build.sh; never in the
+// product build): NFK_ABL_NOSTAGE drops the chunk-loop record copies,
+// NFK_ABL_NOBAR the half-step barriers, NFK_ABL_NOEPI replaces the spline
+// epilogue by a sum.
 #ifdef NFK_ABL_NOSTAGE
 #define NFK_STAGE(...) ((void)0)
 #else
 #define NFK_STAGE(...) stage_record(__VA_ARGS__)
 #endif
-#ifdef NFK_ABL_NOBAR
-#define NFK_PHASE_BARRIER() ((void)0)
-#else
-#define NFK_PHASE_BARRIER() dma_barrier()
-#endif
 
-// One workgroup = kWaves waves x 16 samples.  Phase records stream through
-// two LDS slots: while phase p computes from slot p&1, the record of phase
-// p+1 is already in the other slot and phase p+2's copy is issued right after
-// the barrier that ends phase p.  One barrier per phase; everything else is
-// wave-local.
+// One workgroup = kWaves waves x 16 samples.  A layer is a sequence of NP =
+// 2 + 3 NCH phases (layer 1, layer 2, then per 16-coordinate chunk: searched
+// knots, other knots, derivatives); each phase is a GEMM half (MFMA from an
+// LDS record slot) and an epilogue half (VALU on the accumulators).
+//
+// Half-steps: the GEMM half of phase p is half-step 2p, its epilogue 2p+1.
+// Phase p's record sits in slot p&1; phase p+2's record is copied into that
+// slot at the start of half-step 2p+2 and waited for (vmcnt(0)) at the
+// barrier ending half-step 2p+3.  The loop issues no other global memory
+// operation: x is staged in the prologue and z is collected in LDS.
+// Default (lockstep): all 8 waves run the same half-step; only the end of an
+// epilogue half is a barrier.
+// NFK_PINGPONG=1: waves w and w+4 share a SIMD (tools/simd_map.hip), and a
+// partner's VALU can overlap fp16 MFMAs that alternate accumulators
+// (tools/ubench_coexec2.hip), so waves 4..7 trail waves 0..3 by one half-step
+// (one in its GEMM half while its partner is in its epilogue half) with a
+// barrier after every half-step.  Measured: 13 % slower than lockstep on c3
+// (co-execution stays < 10 % of MFMA cycles and barrier waits double), so it
+// is off.
+// Copy the record of phase p into its slot (p & 1).  Phases: 0 = layer 1,
+// 1 = layer 2, 2 + 3c + {0, 1, 2} = chunk c's searched knots, other knots,
+// derivatives (offA/offB/offC: block offsets of those records in the chunk).
+__device__ __forceinline__ void stage_phase(const FusedArgs& a, int p, int offA, int offB, int offC,
+                                            float4* slot0, float4* slot1, int wid, int lane) {
+    float4* slot = (p & 1) ? slot1 : slot0;
+    if (p == 0) {
+        stage_record(a.pack + a.o_h1, a.blk_h1, slot, wid, lane);
+    } else if (p == 1) {
+        stage_record(a.pack + a.o_h2, a.blk_h2, slot, wid, lane);
+    } else {
+        const int ch = (p - 2) / 3, part = (p - 2) - 3 * ch;
+        const float* wc = a.pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
+        const int off = part == 0 ? offA : (part == 1 ? offB : offC);
+        NFK_STAGE(wc + off * 256, part == 2 ? a.blk_d : a.blk_w, slot, wid, lane);
+    }
+}
+
+// End of half-step hs: retire this wave's LDS work (and, at odd half-steps,
+// its record copies), workgroup barrier, then issue the copy that the next
+// half-step owns (phase hs/2 + 1 at even hs >= 2).
+__device__ __forceinline__ void half_step(int& hs, int np, const FusedArgs& a, int offA, int offB, int offC,
+                                          float4* slot0, float4* slot1, int wid, int lane) {
+    // in lockstep mode only the end of an epilogue half (odd hs) is a barrier
+    if (NFK_PINGPONG || (hs & 1)) {
+        if (hs & 1)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef NFK_ABL_NOBAR
+        __builtin_amdgcn_s_barrier();
+#endif
+        asm volatile("" ::: "memory");
+    }
+    ++hs;
+    if (!(hs & 1) && hs >= 2 && hs / 2 + 1 < np) stage_phase(a, hs / 2 + 1, offA, offB, offC, slot0, slot1, wid, lane);
+}
+
 template <int KBH, bool T1, int K, bool INV>
 __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = (NFK_PINGPONG && wid >= kWaves / 2) ? 1 : 0;
     const int q = lane >> 4, sl = lane & 15;
     const int D = a.n_lo + a.n_up;
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
@@ -387,16 +457,24 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     int32_t* m_lo_out = m_lo_in + a.n_lo;
     const int XL = 32 * a.KB1;  // lower-x tile row length (n_lo padded to the k-blocks)
     const int XU = a.xup;       // upper-x tile row length (n_up padded to 4)
-    float* xt = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xtile;
+    float* xlo = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xtile;
+    float* xup = xlo + 16 * XL;
     const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const FusedConst& c = a.c;
     const float* pk = a.pack;
     const bool row_ok = sl < nrows;
+    const int NP = 2 + 3 * a.NCH;
+    const float* w3 = pk + a.o_w3;
+    // execution order of the three records of a chunk: searched knots, other knots, derivatives
+    const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
+
+    int hs = 0;  // global index of the half-step this wave is in
+#define NFK_HALF_STEP() half_step(hs, NP, a, offA, offB, offC, slot0, slot1, wid, lane)
 
     // ---- prologue: index maps (plain loads, before any DMA is in flight),
-    // first record and the lower-x gather, second record
+    // first two records and both x tiles
     for (int i = threadIdx.x; i < a.n_up; i += 64 * kWaves) {
         m_up_in[i] = a.up_in[i];
         m_up_out[i] = a.up_out[i];
@@ -408,19 +486,22 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     // factors undoing the fp16 pre-scaling (pack header)
     const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
     __syncthreads();  // maps visible (no DMA in flight yet)
-    stage_record(pk + a.o_h1, a.blk_h1, slot0, wid, lane);
-    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xt, lane);
-    dma_barrier();  // layer-1 record and lower-x tiles landed
-    stage_record(pk + a.o_h2, a.blk_h2, slot1, wid, lane);
+    stage_phase(a, 0, offA, offB, offC, slot0, slot1, wid, lane);
+    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xlo, lane);
+    stage_phase(a, 1, offA, offB, offC, slot0, slot1, wid, lane);
+    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xup, lane);
+    dma_barrier();  // layer-1 record and the x tiles landed (layer-2 record: by half-step 1's end)
+    if (grp == 1) NFK_HALF_STEP();  // group 1 trails by one half-step
 
-    // ---- layer 1 (slot 0, fp16 split): h1^T = tanh(W1 . lower^T + b1).  x has
-    // any magnitude, so each wave scales its tile by a power of two 2^sx that
-    // puts max|x| just under 2^14 before the split; acc = 2^(s1+sx) W1 x.
+    // ---- phase 0 (slot 0): layer 1, fp16 split.  x has any magnitude, so each
+    // wave scales its tile by a power of two 2^sx that puts max|x| just under
+    // 2^14 before the split; acc = 2^(s1+sx) W1 x.
     f32x4 h1[HT];
+    float unx;
     {
         float mx = 0.0f;
         for (int kb = 0; kb < a.KB1; ++kb) {
-            const float4* xr = reinterpret_cast<const float4*>(xt + sl * XL + 32 * kb + 8 * q);
+            const float4* xr = reinterpret_cast<const float4*>(xlo + sl * XL + 32 * kb + 8 * q);
             const float4 u = xr[0], v = xr[1];
             mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))),
                                  fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
@@ -429,138 +510,106 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
         int ex = 0;
         if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
-        const float sx = ldexpf(1.0f, 14 - ex), unx = ldexpf(un1, ex - 14);
-#pragma unroll
-        for (int t = 0; t < HT; ++t) h1[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const float sx = ldexpf(1.0f, 14 - ex);
+        unx = ldexpf(un1, ex - 14);
+        // accumulators start at b1 2^(s1+sx) (exact power-of-two scaling), so the
+        // epilogue only multiplies by 2^-(s1+sx): the bias is read in this GEMM
+        // half, before the slot is recycled
         const float4* s = slot0;
+        const float4* bias = s + a.KB1 * HT * 2 * 64;
+        const float bsc = ldexpf(1.0f, 14 - ex) / un1;
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+            const float4 bv = bias[t * 4 + q];
+            h1[t] = f32x4{bv.x * bsc, bv.y * bsc, bv.z * bsc, bv.w * bsc};
+        }
         for (int kb = 0; kb < a.KB1; ++kb) {
-            const float4* xr = reinterpret_cast<const float4*>(xt + sl * XL + 32 * kb + 8 * q);
+            const float4* xr = reinterpret_cast<const float4*>(xlo + sl * XL + 32 * kb + 8 * q);
             const float4 u = xr[0], v = xr[1];
             const float xv8[8] = {u.x * sx, u.y * sx, u.z * sx, u.w * sx, v.x * sx, v.y * sx, v.z * sx, v.w * sx};
-            h8 xh, xlo;
+            h8 xh, xl8;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const _Float16 hh = (_Float16)xv8[j];
                 xh[j] = hh;
-                xlo[j] = (_Float16)(xv8[j] - (float)hh);
+                xl8[j] = (_Float16)(xv8[j] - (float)hh);
             }
 #pragma unroll
             for (int t = 0; t < HT; ++t) {
                 const h8 ahi = __builtin_bit_cast(h8, s[((kb * HT + t) * 2) * 64 + lane]);
                 const h8 alo = __builtin_bit_cast(h8, s[((kb * HT + t) * 2 + 1) * 64 + lane]);
                 h1[t] = mfma16(alo, xh, h1[t]);
-                h1[t] = mfma16(ahi, xlo, h1[t]);
+                h1[t] = mfma16(ahi, xl8, h1[t]);
                 h1[t] = mfma16(ahi, xh, h1[t]);
             }
         }
-        // unscale and add the (unscaled) bias before the activation
-        const float4* bias = s + a.KB1 * HT * 2 * 64;
-#pragma unroll
-        for (int t = 0; t < HT; ++t) {
-            const float4 bv = bias[t * 4 + q];
-            h1[t][0] = __builtin_fmaf(h1[t][0], unx, bv.x);
-            h1[t][1] = __builtin_fmaf(h1[t][1], unx, bv.y);
-            h1[t][2] = __builtin_fmaf(h1[t][2], unx, bv.z);
-            h1[t][3] = __builtin_fmaf(h1[t][3], unx, bv.w);
-        }
     }
-    // identity-copied (lower) coordinates: kept in registers and written after
-    // the chunks, next to the upper stores of the same z lines (written here
-    // when they do not fit: n_lo > 32); then the tile takes the upper coordinates
-    constexpr int kLoRegs = 8;
-    float lo_keep[kLoRegs];
-    const bool lo_late = a.KB1 == 1;  // 16 x 32 = 64 lanes x kLoRegs
-#pragma unroll
-    for (int m = 0; m < kLoRegs; ++m) {
-        const int i = lane + 64 * m, row = i / XL, qq = i - row * XL;
-        lo_keep[m] = lo_late ? xt[row * XL + qq] : 0.0f;
-    }
-    if (!lo_late) {
-        for (int i = lane; i < 16 * a.n_lo; i += 64) {
-            const int row = i / a.n_lo, qq = i - row * a.n_lo;
-            if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = xt[row * XL + qq];
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile reads done before the DMA overwrites it
-    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xt, lane);
+    NFK_HALF_STEP();
+    // epilogue 0: tanh of acc 2^-(s1+sx), split -> layer-2 operands
     h8 bh[KBH], bl[KBH];
     float btail;
-    act_operands<KBH, T1, HT>(h1, -2.0f * kL2E, bh, bl, btail);
-    dma_barrier();  // slot 0 free; layer-2 record and upper-x tiles landed
-    const float* w3 = pk + a.o_w3;
-    // execution order of the three records of a chunk: searched knots, other knots, derivatives
-    const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
-    stage_record(w3 + offA * 256, a.blk_w, slot0, wid, lane);
+    act_operands<KBH, T1, HT>(h1, -2.0f * kL2E * unx, bh, bl, btail);
+    NFK_HALF_STEP();
 
-    // ---- layer 2 (slot 1, fp16 split): h2^T = tanh(W2 . h1^T + b2)
+    // ---- phase 1 (slot 1): layer 2, fp16 split: h2^T = tanh(W2 . h1^T + b2)
     {
         f32x4 h2[HT];
         gemm_h<KBH, T1, HT>(bh, bl, btail, slot1, lane, h2);
+        NFK_HALF_STEP();
         act_operands<KBH, T1, HT>(h2, -2.0f * kL2E * un2, bh, bl, btail);
     }
-    dma_barrier();  // slot 1 free, chunk-0 record A landed
-    stage_record(w3 + offB * 256, a.blk_w, slot1, wid, lane);
+    NFK_HALF_STEP();
 
     const float l2e3 = kL2E * un3;
     float ldsum = 0.0f;
     bool any_in = false, any_nd = false;
-    float* zrow = a.z + (b0 + sl) * a.ldz;
-    // record A and C of a chunk use slot sA, record B slot sB; the next chunk's
-    // A is staged into sB once B is consumed, so the roles swap every chunk
-    float4* sA = slot0;
-    float4* sB = slot1;
     for (int ch = 0; ch < a.NCH; ++ch) {
         const int jbase = 16 * ch;
-        const float* wc = w3 + (int64_t)ch * a.blk_chunk * 256;
-        const float* wn = wc + (int64_t)a.blk_chunk * 256;  // next chunk
+        // phase 2 + 3 ch + {0, 1, 2}: slots alternate with the phase parity
+        float4* sA = (ch & 1) ? slot1 : slot0;  // phase 2 + 3ch is even for even ch
+        float4* sB = (ch & 1) ? slot0 : slot1;
         int jj4[4];
         float xv[4];
         int kb[4];
         float cw_k[4], w_k[4], ch_k[4], h_k[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            jj4[r] = jbase + 4 * q + r;
-            xv[r] = (jj4[r] < a.n_up) ? xt[sl * XU + jj4[r]] : 0.0f;
-        }
 
-        // ---- record A (slot sA): searched knots (widths forward / heights inverse)
+        // ---- phase A: searched knots (widths forward / heights inverse)
         {
             f32x4 acc[K];
             gemm_h<KBH, T1, K>(bh, bl, btail, sA, lane, acc);
-            if (INV)
-                knot_phase<K, true>(acc, xv, c, l2e3, kb, ch_k, h_k);
-            else
-                knot_phase<K, true>(acc, xv, c, l2e3, kb, cw_k, w_k);
+            NFK_HALF_STEP();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                jj4[r] = jbase + 4 * q + r;
+                xv[r] = (jj4[r] < a.n_up) ? xup[sl * XU + jj4[r]] : 0.0f;
+            }
+            knot_phase<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k);
         }
-        NFK_PHASE_BARRIER();
-        NFK_STAGE(wc + offC * 256, a.blk_d, sA, wid, lane);
+        NFK_HALF_STEP();
 
-        // ---- record B (slot sB): the other knots, selected at the bin
+        // ---- phase B: the other knots, selected at the bin
         {
             f32x4 acc[K];
             gemm_h<KBH, T1, K>(bh, bl, btail, sB, lane, acc);
-            if (INV)
-                knot_phase<K, false>(acc, xv, c, l2e3, kb, cw_k, w_k);
-            else
-                knot_phase<K, false>(acc, xv, c, l2e3, kb, ch_k, h_k);
+            NFK_HALF_STEP();
+            knot_phase<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k);
         }
-        NFK_PHASE_BARRIER();
-        if (ch + 1 < a.NCH) NFK_STAGE(wn + offA * 256, a.blk_w, sB, wid, lane);
+        NFK_HALF_STEP();
 
-        // ---- record C (slot sA): derivatives of the bin, evaluate, log|det|
+        // ---- phase C: derivatives of the bin, evaluate, log|det|
         {
             f32x4 accd[DN];
             gemm_h<KBH, T1, DN>(bh, bl, btail, sA, lane, accd);
+            NFK_HALF_STEP();
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
 #pragma unroll
                 for (int t = 0; t < DN; ++t) v += accd[t][r];
-                const bool live = jj4[r] < a.n_up && row_ok;
-                if (live) zrow[m_up_out[jj4[r]]] = v;
+                if (jj4[r] < a.n_up) xup[sl * XU + jj4[r]] = v;
                 ldsum += v;
-                any_in |= live;
+                any_in = true;
             }
             if (false)
 #endif
@@ -613,26 +662,24 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                 const bool inside = (x >= c.lo) && (x <= c.hi);
                 const bool live = jj4[r] < a.n_up && row_ok;
                 out = inside ? out : x;
-                if (live) zrow[m_up_out[jj4[r]]] = out;
+                if (jj4[r] < a.n_up) xup[sl * XU + jj4[r]] = out;  // z collected in the tile
                 ldsum += (inside && live) ? lad : 0.0f;
                 any_in |= inside && live;
                 any_nd |= nd && inside && live;
             }
         }
-        NFK_PHASE_BARRIER();
-        if (ch + 1 < a.NCH) NFK_STAGE(wn + offB * 256, a.blk_w, sA, wid, lane);
-        float4* t = sA;
-        sA = sB;
-        sB = t;
+        if (grp == 0 || ch + 1 < a.NCH) NFK_HALF_STEP();  // group 1 ends one barrier early
     }
 
-    // ---- identity-copied coordinates (tile row length XL, see above), per-sample log|det|
-    if (lo_late) {
-#pragma unroll
-        for (int m = 0; m < kLoRegs; ++m) {
-            const int i = lane + 64 * m, row = i / XL, qq = i - row * XL;
-            if (row < nrows && qq < a.n_lo) a.z[(b0 + row) * a.ldz + m_lo_out[qq]] = lo_keep[m];
-        }
+    // ---- z rows of this wave (upper from the tile, lower = identity copy), log|det|
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = lane; i < 16 * a.n_up; i += 64) {
+        const int row = i / a.n_up, j = i - row * a.n_up;
+        if (row < nrows) a.z[(b0 + row) * a.ldz + m_up_out[j]] = xup[row * XU + j];
+    }
+    for (int i = lane; i < 16 * a.n_lo; i += 64) {
+        const int row = i / a.n_lo, j = i - row * a.n_lo;
+        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[j]] = xlo[row * XL + j];
     }
     {
         float v = ldsum;
@@ -650,6 +697,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                 atomicOr(a.status, bits);
         }
     }
+#undef NFK_HALF_STEP
 }
 
 template <int KBH, int T1, int K>

@@ -12,6 +12,10 @@
 // Python scalars of the reference are, then rounded to fp32 once.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#ifndef NFK_TREESUM
+#define NFK_TREESUM 0
+#endif
 #include <stdint.h>
 
 struct NfkSplineConst {
@@ -141,6 +145,26 @@ __device__ __forceinline__ void nfk_knots_nsf_lean(const float (&raw)[K], float 
 // the floored fractions (pre[0] = 0); edge j = fma(span 2^-30, (float)pre[j], lo)
 // for j < K and the pinned right end for j = K.  The fused kernel searches
 // the bin in this integer domain and converts only the two edges it uses.
+// sum of K values: pairwise tree (short dependency chains) or sequential
+template <int K>
+__device__ __forceinline__ float nfk_sum(const float (&v)[K]) {
+#if NFK_TREESUM
+    float t[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) t[i] = v[i];
+#pragma unroll
+    for (int w = 1; w < K; w *= 2)
+#pragma unroll
+        for (int i = 0; i + w < K; i += 2 * w) t[i] = t[i] + t[i + w];
+    return t[0];
+#else
+    float s = v[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) s = s + v[i];
+    return s;
+#endif
+}
+
 template <int K>
 __device__ __forceinline__ void nfk_prefix_nsf_lean(const float (&raw)[K], float l2e, float m2b,
                                                     float fb30, float mb30, int (&pre)[K]) {
@@ -149,19 +173,12 @@ __device__ __forceinline__ void nfk_prefix_nsf_lean(const float (&raw)[K], float
     for (int i = 1; i < K; ++i) m = fmaxf(m, raw[i]);
     const float mL = m * l2e;
     float e[K];
-    float s = 0.0f;
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(raw[i], l2e, -mL));
-        s = i == 0 ? e[0] : s + e[i];
-    }
-    const float q = m2b * __builtin_amdgcn_rcpf(s);
-    float s2 = 0.0f;
+    for (int i = 0; i < K; ++i) e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(raw[i], l2e, -mL));
+    const float q = m2b * __builtin_amdgcn_rcpf(nfk_sum<K>(e));
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(e[i], q, -m2b));
-        s2 = i == 0 ? e[0] : s2 + e[i];
-    }
+    for (int i = 0; i < K; ++i) e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(e[i], q, -m2b));
+    const float s2 = nfk_sum<K>(e);
     const float f30 = fb30 * __builtin_amdgcn_rcpf(s2);
     pre[0] = 0;
 #pragma unroll

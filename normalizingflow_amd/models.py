@@ -78,7 +78,10 @@ class NormalizingFlowModel(nn.Module):
         n = sum(f._n_status for f in self.flows if isinstance(f, _HipFlow))
         return torch.zeros(max(n, 1), dtype=torch.int32, device=device), n
 
-    def _chain(self, x, inverse):
+    def _chain(self, x, inverse, deferred=None):
+        """Run the layer chain.  With ``deferred`` (a list) the status check is
+        left to the caller, who appends its prior kernel first so the GPU queue
+        runs layers + prior back to back before the one host sync."""
         x = _check_input(x)
         _grad_warning(self)
         m = x.shape[0]
@@ -96,27 +99,43 @@ class NormalizingFlowModel(nn.Module):
                 else:  # a user-defined layer: reference protocol
                     x, ld = flow.inverse(x) if inverse else flow.forward(x)
                     logdet += ld
-        if n_st and config.STRICT_CHECKS:
+        if deferred is not None:
+            deferred.append((status, n_st))
+        elif n_st and config.STRICT_CHECKS:
             raise_on_status(status, n_st)
         return x, logdet
 
+    @staticmethod
+    def _check(deferred):
+        for status, n_st in deferred:
+            if n_st and config.STRICT_CHECKS:
+                raise_on_status(status, n_st)
+
     # ------------------------------------------------------------------ API
     def forward(self, x):
-        z, log_det = self._chain(x, False)
-        return z, self._prior_log_prob(z), log_det
+        d = []
+        z, log_det = self._chain(x, False, d)
+        lp = self._prior_log_prob(z)
+        self._check(d)
+        return z, lp, log_det
 
     def inverse(self, z):
         return self._chain(z, True)
 
     def sample(self, n_samples):
         z = self.prior.sample((n_samples,))
-        x, log_det = self.inverse(z)
+        d = []
+        x, log_det = self._chain(z, True, d)
         log_px = self._prior_log_prob(z, logdet=log_det, sign=-1)
+        self._check(d)
         return x.data, log_px.data, z.data
 
     def evaluate(self, x):
-        z, log_det = self._chain(x, False)
-        return self._prior_log_prob(z, logdet=log_det, sign=1).data
+        d = []
+        z, log_det = self._chain(x, False, d)
+        out = self._prior_log_prob(z, logdet=log_det, sign=1)
+        self._check(d)
+        return out.data
 
     def log_prob(self, x):
         return self.evaluate(x)
