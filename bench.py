@@ -40,6 +40,16 @@ WORKLOADS = {
            dict(size=32, dim=2, K=8, B=3, hidden_dim=100), 64, 8),
     "c2": ("64-dim synthetic Gaussian, 8-layer RealNVP affine coupling (H=100), log_prob",
            "RealNVP", dict(dim=64, hidden_dim=100), 64, 8),
+    "c5": ("256-dim synthetic Gaussian, 16-layer NSF_CL RQS spline coupling (K=16 bins, H=256, "
+           "mask [i%2], B=3), log_prob", "NSF_CL",
+           dict(size=128, dim=2, K=16, B=3, hidden_dim=256), 256, 16),
+}
+
+
+METRICS = {
+    "c3": "samples/sec log_prob (1M×64, 8 RQS coupling layers) at 1/2/4/8 GPU",  # BASELINE.json
+    "c2": "samples/sec log_prob (1M×64, 8 RealNVP affine coupling layers)",
+    "c5": "samples/sec log_prob (1M×256, 16 RQS coupling layers, H=256, K=16)",
 }
 
 
@@ -225,9 +235,7 @@ def main():
             cpu = cpu_baseline(args.workload, {k: v.cpu() for k, v in sd.items()})
         desc = WORKLOADS[args.workload][0]
         out = {
-            "metric": "samples/sec log_prob (1M×64, 8 RQS coupling layers) at 1/2/4/8 GPU"
-                      if args.workload == "c3" else "samples/sec log_prob (1M×64, 8 RealNVP "
-                                                    "affine coupling layers)",
+            "metric": METRICS[args.workload],
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
