@@ -109,7 +109,8 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic):
     """Roofline of the dominant kernel from live HIP-event timings."""
     if not timer_summary:
         return None
-    name, (n, mean_ms, tot) = max(timer_summary.items(), key=lambda kv: kv[1][2])
+    name, (n_launch, mean_ms, tot) = max(timer_summary.items(), key=lambda kv: kv[1][2])
+    n = n_launch
     desc, kind, kw, D, L = WORKLOADS[workload]
     B = per_gpu_batch
     if name == "nfk_fused_nsf":
@@ -139,6 +140,22 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic):
                               "%.0f flop/sample k-tail on f32 MFMA (%.1f TF)"
                               % (f16, PEAK_FP16_TFLOPS, f32, PEAK_FP32_TFLOPS),
                 "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
+    if name == "nfk_fused_realnvp":
+        H, n = kw["hidden_dim"], kw["dim"] // 2
+        kbf, R = divmod(H, 32)
+        tail = R if (0 < R <= 4 and kbf >= 1) else 0
+        f32 = 4 * 2.0 * tail * (H + n)                       # k-tails of layers 2-3, 4 nets
+        f16 = 4 * 2.0 * (n * H + H * H + H * n) - f32         # 131,200/sample
+        flops = (f16 + f32) * B
+        t_floor = f32 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * f16 / (PEAK_FP16_TFLOPS * 1e12)
+        peak = (f16 + f32) / t_floor / 1e12
+        achieved = flops / (mean_ms * 1e-3) / 1e12
+        return {"kernel": name, "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                "launches": n_launch, "mean_ms": round(mean_ms, 4),
+                "per_launch": "%d samples x %.0f flop (fp32-equivalent)" % (B, flops / B),
+                "peak_basis": "MFMA floor: %.0f flop/sample as 3 fp16 products + %.0f on f32 MFMA"
+                              % (f16, f32)}
     if name == "nfk_rqs_coupling":
         n_up = kw["size"] * (kw["dim"] - 1)
         P = 3 * kw["K"] - 1

@@ -144,9 +144,10 @@ int nfk_trig_features(const float* x, int64_t ldx, float* feat, int64_t ldf, int
                       int32_t n, double B, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
- * Fused NSF coupling layer: conditioner MLP (FCNN, flows.py:20-35) on fp32
- * MFMA (v_mfma_f32_16x16x4_f32) + spline epilogue, one launch per layer; the
- * [batch, n_up, 3K-1] conditioner output never touches HBM.
+ * Fused NSF coupling layer: conditioner MLP (FCNN, flows.py:20-35) on MFMA
+ * (fp16 two-way split with power-of-two pre-scaling, fp32 accumulation) +
+ * spline epilogue, one launch per layer; the [batch, n_up, 3K-1] conditioner
+ * output never touches HBM.  Replaces NSF_CL.forward/inverse (flows.py:227-253).
  *   wpack: weights re-packed by nfk_fused_nsf_pack() into MFMA fragment order
  *   (a device buffer of nfk_fused_nsf_pack_elems() floats).
  * Supported shapes: nfk_fused_nsf_supported() != 0.
@@ -161,6 +162,24 @@ int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t
                   const int32_t* lo_out, int32_t n_lo, int32_t hidden, float* z, int64_t ldz,
                   float* logdet, int32_t logdet_mode, int64_t batch, int32_t K,
                   double tail_bound, int32_t inverse, int32_t* status, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused RealNVP layer: both affine half-couplings with their four FCNN
+ * conditioners (s1, t1, s2, t2) in one launch; replaces RealNVP.forward /
+ * inverse (flows.py:44-76).  x, z: [batch, 2*half_dim] row-major.
+ *   nets: HOST array of 24 device pointers, nets s1, t1, s2, t2 in that order,
+ *         each W0 [H, half_dim], b0, W2 [H, H], b2, W4 [half_dim, H], b4
+ *         (nn.Linear weight/bias of network.0/.2/.4).
+ * Supported shapes: nfk_fused_realnvp_supported() != 0 (half_dim = 16, 32,
+ * 48 or 64; hidden <= 132).
+ * ------------------------------------------------------------------------- */
+int nfk_fused_realnvp_supported(int32_t half_dim, int32_t hidden);
+int64_t nfk_fused_realnvp_pack_elems(int32_t half_dim, int32_t hidden);
+int nfk_fused_realnvp_pack(const float* const* nets, int32_t half_dim, int32_t hidden, float* wpack,
+                           nfk_stream_t stream);
+int nfk_fused_realnvp(const float* x, int64_t ldx, const float* wpack, int32_t half_dim, int32_t hidden,
+                      float* z, int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
+                      int32_t inverse, nfk_stream_t stream);
 
 #ifdef __cplusplus
 }

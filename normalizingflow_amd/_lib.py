@@ -53,6 +53,13 @@ SIGNATURES = {
         P, P, I32, I32,                 # lo_in, lo_out, n_lo, hidden
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
         I64, I32, F64, I32, P, P]),     # batch, K, tail_bound, inverse, status, stream
+    "nfk_fused_realnvp_supported": (ctypes.c_int, [I32, I32]),
+    "nfk_fused_realnvp_pack_elems": (ctypes.c_int64, [I32, I32]),
+    "nfk_fused_realnvp_pack": (ctypes.c_int, [P, I32, I32, P, P]),
+    "nfk_fused_realnvp": (ctypes.c_int, [
+        P, I64, P, I32, I32,            # x, ldx, wpack, half_dim, hidden
+        P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
+        I64, I32, P]),                  # batch, inverse, stream
 }
 
 _lock = threading.Lock()

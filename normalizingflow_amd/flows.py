@@ -143,6 +143,27 @@ class RealNVP(_HipFlow):
         self.s1 = base_network(dim // 2, dim // 2, hidden_dim)
         self.t2 = base_network(dim // 2, dim // 2, hidden_dim)
         self.s2 = base_network(dim // 2, dim // 2, hidden_dim)
+        self._pack_cache = None
+
+    def _fused_pack(self, device):
+        """Weights of the four conditioners re-packed for nfk_fused_realnvp;
+        rebuilt when any weight changes (None when the fused kernel does not apply)."""
+        nets = (self.s1, self.t1, self.s2, self.t2)
+        if not config.USE_FUSED or not all(_is_stock_fcnn(n) for n in nets):
+            return None
+        h = self.dim // 2
+        hidden = self.s1.network[0].out_features
+        if any(n.network[0].out_features != hidden for n in nets) or not K_.fused_realnvp_supported(h, hidden):
+            return None
+        params = [t for n in nets for i in (0, 2, 4) for t in (n.network[i].weight, n.network[i].bias)]
+        if any(p.device != device or p.dtype != torch.float32 for p in params):
+            return None
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._pack_cache is not None and self._pack_cache[0] == key:
+            return self._pack_cache[1]
+        pack = K_.fused_realnvp_pack(params, h, hidden)
+        self._pack_cache = (key, pack, hidden)
+        return pack
 
     def _run(self, x, inverse, logdet, mode, status):
         h = self.dim // 2
@@ -151,6 +172,11 @@ class RealNVP(_HipFlow):
             raise RuntimeError("RealNVP needs an even feature dimension equal to dim=%d (got %d)"
                                % (self.dim, x.shape[1]))
         z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        pack = self._fused_pack(x.device)
+        if pack is not None:
+            K_.fused_realnvp(x, pack, h, self._pack_cache[2], z, logdet=logdet, logdet_mode=mode,
+                             inverse=inverse)
+            return z
         lo, up = x[:, :h], x[:, h:]
         zlo, zup = z[:, :h], z[:, h:]
         m2 = K_.MODE_ACC if mode != K_.MODE_NONE else K_.MODE_NONE

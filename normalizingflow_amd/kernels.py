@@ -6,6 +6,8 @@ only place the package touches raw pointers.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -252,3 +254,28 @@ def fused_nsf(x, wpack, up_in, up_out, lo_in, lo_out, hidden, z, *, logdet, logd
               up_in.numel(), lo_in.data_ptr(), lo_out.data_ptr(), lo_in.numel(), hidden, zp, ldz,
               _vec(logdet, B, "logdet"), logdet_mode, B, K, float(tail_bound),
               1 if inverse else 0, _vec(status, 1, "status", torch.int32), _stream(dev))
+
+
+def fused_realnvp_supported(half_dim, hidden):
+    return bool(_lib.load().nfk_fused_realnvp_supported(half_dim, hidden))
+
+
+def fused_realnvp_pack(nets, half_dim, hidden):
+    """nets: 24 tensors, s1, t1, s2, t2 each (W0, b0, W2, b2, W4, b4)."""
+    dev = _require_hip(*nets)
+    n = int(_lib.load().nfk_fused_realnvp_pack_elems(half_dim, hidden))
+    pack = torch.empty(n, dtype=F32, device=dev)
+    ws = [t.detach().contiguous() for t in nets]
+    ptrs = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in ws])
+    _lib.call("nfk_fused_realnvp_pack", ctypes.cast(ptrs, ctypes.c_void_p), half_dim, hidden, pack.data_ptr(),
+              _stream(dev))
+    return pack
+
+
+def fused_realnvp(x, wpack, half_dim, hidden, z, *, logdet, logdet_mode, inverse=False):
+    dev = _require_hip(x, wpack, z, logdet)
+    B = x.shape[0]
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    _timed("nfk_fused_realnvp", dev, "nfk_fused_realnvp", xp, ldx, wpack.data_ptr(), half_dim, hidden, zp, ldz,
+           _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, _stream(dev))

@@ -238,6 +238,35 @@ def test_realnvp_c2_vs_oracle(hip_device):
     close(xr, x, 1e-4, 1e-4)
 
 
+@pytest.mark.parametrize("half,hidden", [(16, 16), (32, 100), (48, 64), (64, 64), (32, 36)])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_realnvp_fused_layer_vs_oracle(half, hidden, inverse, hip_device):
+    """nfk_fused_realnvp (one launch per layer, both half-couplings) against the
+    oracle's RealNVP (flows.py:44-76) on one layer, ragged batch, and against
+    the unfused HIP path (rocBLAS conditioners + nfk_affine_coupling)."""
+    from normalizingflow_amd import config, kernels as K_
+    assert K_.fused_realnvp_supported(half, hidden)
+    torch.manual_seed(40 + half + hidden)
+    layer = nff.RealNVP(2 * half, hidden_dim=hidden)
+    x = torch.randn(1000, 2 * half, generator=torch.Generator().manual_seed(3)) * 1.5
+    sd = cpu_sd(layer)
+    z_ref, ld_ref = orc.realnvp(x, sd, "", 2 * half, inverse=inverse)
+    dev = layer.to(hip_device)
+    xd = x.to(hip_device)
+    with torch.no_grad():
+        z, ld = (dev.inverse(xd) if inverse else dev(xd))
+        assert dev._pack_cache is not None  # the fused kernel ran
+        close(z, z_ref, Z_RTOL, 5e-5)
+        close(ld, ld_ref, LD_RTOL, 1e-4)
+        config.USE_FUSED = False
+        try:
+            z2, ld2 = (dev.inverse(xd) if inverse else dev(xd))
+        finally:
+            config.USE_FUSED = True
+        close(z, z2, Z_RTOL, 5e-5)
+        close(ld, ld2, LD_RTOL, 1e-4)
+
+
 @pytest.mark.parametrize("K", [2, 4, 5, 8, 10, 16, 32])
 @pytest.mark.parametrize("inverse", [False, True])
 def test_unconstrained_rqs_random_vs_oracle(K, inverse, hip_device):
