@@ -15,8 +15,12 @@ What runs where (ROCm device only -- CPU tensors raise, there is no fallback):
   Planar         nfk_planar -- flows_1.py:21-63
   Radial         nfk_radial_sumsq (+ optional all-reduce) + nfk_radial_apply
                  -- flows_1.py:66-97
-Gradients do not flow through the kernels yet (backward kernels are the next
-row of the plan); calls under autograd warn once.
+Gradients: when autograd needs them (grad mode on and x or a parameter
+requires grad) a layer runs as ``_LayerFn``: the forward is the same HIP
+kernel chain; backward recomputes the layer from the saved input with the
+differentiable torch restatement (``torch_math``) on the same device and
+back-propagates through it (activation memory = one input per layer, like
+gradient checkpointing).  Hand-written backward kernels are the next step.
 """
 from __future__ import annotations
 
@@ -31,6 +35,7 @@ import torch.nn.init as init
 
 from . import config
 from . import kernels as K_
+from . import torch_math
 from ._lib import ST_INSIDE_SEEN, ST_NEG_DISC
 
 __all__ = ["FCNN", "RealNVP", "NSF_AR", "NSF_CL", "Planar", "Radial", "functional_derivatives"]
@@ -42,18 +47,46 @@ functional_derivatives = {
     F.elu: lambda x: (x > 0).type(x.dtype) + (x < 0).type(x.dtype) * torch.exp(x),
 }
 
-_warned_grad = False
+def _needs_grad(module, x):
+    return torch.is_grad_enabled() and (
+        x.requires_grad or any(p.requires_grad for p in module.parameters()))
 
 
-def _grad_warning(module):
-    global _warned_grad
-    if _warned_grad or not torch.is_grad_enabled():
-        return
-    if any(p.requires_grad for p in module.parameters()):
-        _warned_grad = True
-        warnings.warn("normalizingflow_amd: outputs of the HIP flow kernels carry no autograd "
-                      "graph yet (backward kernels pending); use torch.no_grad() for inference",
-                      RuntimeWarning, stacklevel=3)
+class _LayerFn(torch.autograd.Function):
+    """One layer as an autograd node: HIP forward, recompute-backward.
+
+    forward(layer, inverse, status, names, x, *params) -> (z, logdet)
+    backward recomputes (z, logdet) = torch_math.layer_forward(...) from the
+    saved x and parameters under enable_grad and returns their vector-Jacobian
+    products.  The kernels' outputs are the values the graph continues from;
+    the recomputation only supplies derivatives.
+    """
+
+    @staticmethod
+    def forward(ctx, layer, inverse, status, names, x, *params):
+        ctx.layer, ctx.inverse, ctx.names = layer, inverse, names
+        ctx.save_for_backward(x, *params)
+        return layer._eval(x, inverse, status)
+
+    @staticmethod
+    def backward(ctx, gz, gld):
+        x, *params = ctx.saved_tensors
+        need = ctx.needs_input_grad[4:]
+        with torch.enable_grad():
+            xd = x.detach().requires_grad_(need[0])
+            pd = [p.detach().requires_grad_(n) for p, n in zip(params, need[1:])]
+            z, ld = torch_math.layer_forward(ctx.layer, xd, dict(zip(ctx.names, pd)), ctx.inverse)
+            outs, grads_out = [], []
+            for o, g in ((z, gz), (ld, gld)):
+                if g is not None and o.requires_grad:
+                    outs.append(o)
+                    grads_out.append(g.expand_as(o) if g.shape != o.shape else g)
+            inputs = [t for t in [xd] + pd if t.requires_grad]
+            got = (torch.autograd.grad(outs, inputs, grads_out, allow_unused=True)
+                   if outs and inputs else [None] * len(inputs))
+        it = iter(got)
+        res = [next(it) if t.requires_grad else None for t in [xd] + pd]
+        return (None, None, None, None, *res)
 
 
 def _check_input(x, what="x"):
@@ -94,15 +127,26 @@ class _HipFlow(nn.Module):
     def _run(self, x, inverse, logdet, mode, status):
         raise NotImplementedError
 
-    def _call(self, x, inverse):
-        x = _check_input(x)
-        _grad_warning(self)
-        st = (torch.zeros(self._n_status, dtype=torch.int32, device=x.device)
-              if self._n_status else None)
+    def _eval(self, x, inverse, status):
+        """(z, logdet) with logdet written by the kernels (no autograd)."""
         logdet = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
         with torch.no_grad():
-            z = self._run(x, inverse, logdet, K_.MODE_WRITE, st)
-        if st is not None and config.STRICT_CHECKS:
+            z = self._run(x, inverse, logdet, K_.MODE_WRITE, status)
+        return z, logdet
+
+    def _call(self, x, inverse, status=None):
+        """Run the layer; with ``status`` given the caller checks it later."""
+        x = _check_input(x)
+        st = status
+        if st is None and self._n_status:
+            st = torch.zeros(self._n_status, dtype=torch.int32, device=x.device)
+        if _needs_grad(self, x):
+            named = list(self.named_parameters())
+            z, logdet = _LayerFn.apply(self, inverse, st, tuple(n for n, _ in named), x,
+                                       *(t for _, t in named))
+        else:
+            z, logdet = self._eval(x, inverse, st)
+        if status is None and st is not None and config.STRICT_CHECKS:
             raise_on_status(st)
         return z, logdet
 
@@ -448,10 +492,11 @@ class Radial(_HipFlow):
                         z, ld_scalar, logdet=logdet, logdet_mode=mode)
         return z
 
-    def forward(self, x):
-        x = _check_input(x)
-        _grad_warning(self)
+    def _eval(self, x, inverse, status):
         ld = torch.empty(1, dtype=torch.float32, device=x.device)
         with torch.no_grad():
-            z = self._run(x, False, None, K_.MODE_NONE, None, ld_scalar=ld)
+            z = self._run(x, inverse, None, K_.MODE_NONE, None, ld_scalar=ld)
         return z, ld
+
+    def forward(self, x):
+        return self._call(x, False)

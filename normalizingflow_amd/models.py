@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from . import config
 from . import kernels as K_
-from .flows import _HipFlow, _check_input, _grad_warning, raise_on_status
+from .flows import _HipFlow, _check_input, _needs_grad, raise_on_status
 
 __all__ = ["NormalizingFlowModel", "NormalizingFlow"]
 
@@ -40,6 +40,24 @@ def _iso_normal(prior):
         return None
     hld = float(d.log().sum())  # MultivariateNormal's half_log_det, as torch evaluates it
     return float(d[0]), hld
+
+
+class _NormalLogProbFn(torch.autograd.Function):
+    """log N(z; 0, s^2 I) by the nfk_normal_logprob kernel, differentiable in
+    z: d/dz = -z / s^2 (the values are those of the inference path)."""
+
+    @staticmethod
+    def forward(ctx, z, scale, hld):
+        out = torch.empty(z.shape[0], dtype=torch.float32, device=z.device)
+        K_.normal_logprob(z, out, scale=scale, hld=hld)
+        ctx.save_for_backward(z)
+        ctx.inv_var = 1.0 / (scale * scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        z, = ctx.saved_tensors
+        return g[:, None] * z * (-ctx.inv_var), None, None
 
 
 class NormalizingFlowModel(nn.Module):
@@ -65,9 +83,13 @@ class NormalizingFlowModel(nn.Module):
     def _prior_log_prob(self, z, logdet=None, sign=1):
         iso = self._prior_consts()
         if iso is not None and z.shape[1] == self.prior.loc.shape[0]:
-            out = torch.empty(z.shape[0], dtype=torch.float32, device=z.device)
-            K_.normal_logprob(z, out, scale=iso[0], hld=iso[1], logdet=logdet, sign=sign)
-            return out
+            if not (torch.is_grad_enabled() and z.requires_grad):
+                out = torch.empty(z.shape[0], dtype=torch.float32, device=z.device)
+                K_.normal_logprob(z, out, scale=iso[0], hld=iso[1], logdet=logdet, sign=sign)
+                return out
+            if not (self.prior.loc.requires_grad or self.prior.scale_tril.requires_grad):
+                lp = _NormalLogProbFn.apply(z, iso[0], iso[1])
+                return lp if logdet is None else (lp + logdet if sign >= 0 else lp - logdet)
         lp = self.prior.log_prob(z)
         if logdet is None:
             return lp
@@ -81,24 +103,32 @@ class NormalizingFlowModel(nn.Module):
     def _chain(self, x, inverse, deferred=None):
         """Run the layer chain.  With ``deferred`` (a list) the status check is
         left to the caller, who appends its prior kernel first so the GPU queue
-        runs layers + prior back to back before the one host sync."""
+        runs layers + prior back to back before the one host sync.
+
+        Inference accumulates log|det| in place; when autograd needs gradients
+        every kernel-backed layer runs as an autograd node (flows._LayerFn) and
+        the per-layer log|det| are summed out of place."""
         x = _check_input(x)
-        _grad_warning(self)
         m = x.shape[0]
+        grad = _needs_grad(self, x)
         logdet = torch.zeros(m, dtype=torch.float32, device=x.device)
         status, n_st = self._status(x.device)
         off = 0
         flows = self.flows[::-1] if inverse else self.flows
-        with torch.no_grad():
+        with torch.set_grad_enabled(grad):
             for flow in flows:
                 if isinstance(flow, _HipFlow):
                     k = flow._n_status
                     st = status[off:off + k] if k else None
                     off += k
-                    x = flow._run(x, inverse, logdet, K_.MODE_ACC, st)
+                    if grad:
+                        x, ld = flow._call(x, inverse, status=st)
+                        logdet = logdet + ld
+                    else:
+                        x = flow._run(x, inverse, logdet, K_.MODE_ACC, st)
                 else:  # a user-defined layer: reference protocol
                     x, ld = flow.inverse(x) if inverse else flow.forward(x)
-                    logdet += ld
+                    logdet = logdet + ld if grad else logdet.add_(ld)
         if deferred is not None:
             deferred.append((status, n_st))
         elif n_st and config.STRICT_CHECKS:
@@ -122,6 +152,9 @@ class NormalizingFlowModel(nn.Module):
     def inverse(self, z):
         return self._chain(z, True)
 
+    # sample / evaluate return detached ``.data`` (models.py:35, 40), so they
+    # never build a graph: the in-place kernel chain serves them even in grad mode
+    @torch.no_grad()
     def sample(self, n_samples):
         z = self.prior.sample((n_samples,))
         d = []
@@ -130,6 +163,7 @@ class NormalizingFlowModel(nn.Module):
         self._check(d)
         return x.data, log_px.data, z.data
 
+    @torch.no_grad()
     def evaluate(self, x):
         d = []
         z, log_det = self._chain(x, False, d)

@@ -36,7 +36,8 @@ def _worker(rank, world, port, x, sd_radial, q):
         layer.load_state_dict(sd_radial)
         layer = layer.to(dev)
         nfd.attach_process_group(torch.nn.ModuleList([layer]))
-        z, ld = layer(x[lo:hi].to(dev))
+        with torch.no_grad():
+            z, ld = layer(x[lo:hi].to(dev))
         # c3-shaped 2-layer NSF_CL model, same weights on every rank
         torch.manual_seed(1234)
         flows = [nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=100, mask=[i % 2]) for i in range(2)]
@@ -48,7 +49,7 @@ def _worker(rank, world, port, x, sd_radial, q):
         a, b = nfd.shard_range(xb.shape[0], rank, world)
         nll = nfd.nll_allreduce(model.log_prob(xb[a:b].to(dev)))
         full = float(-model.log_prob(xb.to(dev)).double().mean())
-        q.put((rank, lo, z.cpu(), ld.cpu(), float(nll), full))
+        q.put((rank, lo, z.cpu().numpy(), ld.cpu().numpy(), float(nll), full))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:
@@ -76,8 +77,8 @@ def test_sharded_radial_and_nll_world2():
     for o in out:
         assert len(o) == 6, o
     out.sort(key=lambda o: o[1])
-    z = torch.cat([o[2] for o in out])
+    z = torch.cat([torch.from_numpy(o[2]) for o in out])
     torch.testing.assert_close(z, z_ref, rtol=1e-5, atol=2e-5)
     for o in out:
-        torch.testing.assert_close(o[3], ld_ref, rtol=1e-5, atol=5e-5)
+        torch.testing.assert_close(torch.from_numpy(o[3]), ld_ref, rtol=1e-5, atol=5e-5)
         assert abs(o[4] - o[5]) < 1e-5 * abs(o[5]) + 1e-6

@@ -1,0 +1,271 @@
+"""Training path on the GPU: gradients through the kernel-backed layers
+(HIP forward + recompute-backward, flows._LayerFn) against the oracle's
+autograd on the CPU, for every layer type and both directions; the
+reference's training step (applications/src/train.py:22-28: loss =
+-mean(prior_lp + log_det), Adam) run side by side for a few steps, which also
+checks that the fused kernels re-pack their weights after every optimizer
+step; the reverse-KL path (setup.py:90-94) through model.inverse; and
+DistributedDataParallel over two ranks (gloo on the box's one device) whose
+averaged gradients must equal the full-batch oracle gradient.
+
+Tolerance: gradients agree to max|ours - oracle| <= 1e-4 * max|oracle| per
+tensor (both are fp32; the GPU's summation order differs from the CPU's).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+import nf.flows as nff
+import nf.models as nfm
+from oracle import nf_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+GRAD_TOL = 1e-4
+
+
+def rel_close(a, b, tol=GRAD_TOL, what=""):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    scale = max(float(b.abs().max()), 1e-12)
+    err = float((a - b).abs().max()) / scale
+    assert err <= tol, "%s: rel err %.3g" % (what, err)
+
+
+def spec_of(layer, prefix):
+    if isinstance(layer, nff.NSF_CL):
+        return dict(type="NSF_CL", prefix=prefix, size=layer.size, dim=layer.dim, K=layer.K,
+                    B=layer.B, mask=[int(m) for m in layer.mask])
+    if isinstance(layer, nff.RealNVP):
+        return dict(type="RealNVP", prefix=prefix, dim=layer.dim)
+    if isinstance(layer, nff.NSF_AR):
+        return dict(type="NSF_AR", prefix=prefix, dim=layer.dim, K=layer.K, B=layer.B)
+    if isinstance(layer, nff.Planar):
+        return dict(type="Planar", prefix=prefix, nonlinearity=layer.h.__name__)
+    if isinstance(layer, nff.Radial):
+        return dict(type="Radial", prefix=prefix)
+    raise TypeError(type(layer))
+
+
+def _radial(d):
+    r = nff.Radial(d)
+    r.reset_parameters(d)
+    return r
+
+
+LAYERS = {
+    # c3's layer: the fused MFMA NSF kernel
+    "nsfcl_fused": (lambda: nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=100, mask=[0]), 64, True),
+    # 3 coordinates, non-prefix mask: FCNN + nfk_rqs_coupling
+    "nsfcl_unfused": (lambda: nff.NSF_CL(size=6, dim=3, K=5, B=3, hidden_dim=24, mask=[1]), 18, True),
+    "realnvp_fused": (lambda: nff.RealNVP(64, hidden_dim=100), 64, True),
+    "realnvp_unfused": (lambda: nff.RealNVP(10, hidden_dim=20), 10, True),
+    "nsfar": (lambda: nff.NSF_AR(dim=4, K=5, B=3, hidden_dim=16), 4, True),
+    "planar_tanh": (lambda: nff.Planar(6), 6, False),
+    "planar_elu": (lambda: nff.Planar(6, nonlinearity=F.elu), 6, False),
+    "radial": (lambda: _radial(6), 6, False),
+}
+
+
+def _layer_case(name, inverse):
+    make, d, has_inv = LAYERS[name]
+    if inverse and not has_inv:
+        pytest.skip("no inverse")
+    torch.manual_seed(11)
+    layer = make()
+    x = torch.randn(1024, d, generator=torch.Generator().manual_seed(3)) * 1.5
+    g = torch.Generator().manual_seed(4)
+    gz = torch.randn(1024, d, generator=g)
+    gld = torch.randn(1 if name == "radial" else 1024, generator=g)
+    return layer, x, gz, gld
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("name", list(LAYERS))
+def test_layer_grads_vs_oracle(name, inverse, hip_device):
+    layer, x, gz, gld = _layer_case(name, inverse)
+    # oracle: autograd of the CPU restatement
+    sd = {"l." + k: v.detach().clone().requires_grad_(True) for k, v in layer.named_parameters()}
+    xr = x.clone().requires_grad_(True)
+    zr, ldr = orc.apply_layer(spec_of(layer, "l."), xr, sd, inverse=inverse)
+    ((zr * gz).sum() + (ldr * gld).sum()).backward()
+    # ours
+    layer = layer.to(hip_device)
+    xg = x.to(hip_device).requires_grad_(True)
+    z, ld = layer.inverse(xg) if inverse else layer(xg)
+    assert z.requires_grad and ld.requires_grad
+    ((z * gz.to(hip_device)).sum() + (ld * gld.to(hip_device)).sum()).backward()
+    rel_close(z, zr, 1e-5, "z")
+    rel_close(ld.expand_as(ldr), ldr, 1e-5, "logdet")
+    rel_close(xg.grad, xr.grad, what="x.grad")
+    for k, p in layer.named_parameters():
+        ref = sd["l." + k].grad
+        if ref is None:
+            assert p.grad is None or not bool(p.grad.any()), k
+        else:
+            rel_close(p.grad, ref, what=k)
+
+
+def _c3(n_layers, seed=1234, hidden=100):
+    torch.manual_seed(seed)
+    flows = [nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=hidden, mask=[i % 2])
+             for i in range(n_layers)]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(64), torch.eye(64))
+    return nfm.NormalizingFlowModel(prior, flows)
+
+
+def _to_dev(model, dev):
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(64, device=dev),
+                                                        torch.eye(64, device=dev))
+    return model.to(dev)
+
+
+def _specs(model):
+    return [spec_of(f, "flows.%d." % i) for i, f in enumerate(model.flows)]
+
+
+def test_train_steps_match_oracle(hip_device):
+    """train.py:22-28 for 3 optimizer steps on the GPU model and on the oracle
+    with the same initial weights and batches: per-step loss and gradients,
+    and the final weights.  SGD with momentum (its update is proportional to
+    the gradient, so the final weights inherit the gradient tolerance; Adam's
+    sign-like update of ~0 gradients would amplify fp32 summation noise)."""
+    model = _c3(2)
+    specs = _specs(model)
+    ref = {k: v.detach().clone().requires_grad_(True) for k, v in model.named_parameters()}
+    opt_ref = torch.optim.SGD(list(ref.values()), lr=0.05, momentum=0.9)
+    model = _to_dev(model, hip_device)
+    opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9)
+    g = torch.Generator().manual_seed(9)
+    for step in range(3):
+        x = torch.randn(2048, 64, generator=g)
+        opt_ref.zero_grad()
+        _, plp, ld = orc.model_forward(specs, ref, x)
+        loss_ref = -torch.mean(plp + ld)
+        loss_ref.backward()
+        opt.zero_grad()
+        z, plp_g, ld_g = model(x.to(hip_device))
+        loss = -torch.mean(plp_g + ld_g)
+        loss.backward()
+        assert abs(float(loss.detach()) - float(loss_ref.detach())) <= 1e-5 * abs(float(loss_ref.detach())), step
+        for k, p in model.named_parameters():
+            rel_close(p.grad, ref[k].grad, what="step%d %s" % (step, k))
+        opt_ref.step()
+        opt.step()
+    for k, p in model.named_parameters():
+        rel_close(p, ref[k], 1e-5, "final " + k)
+    # inference after training uses the re-packed weights
+    with torch.no_grad():
+        x = torch.randn(512, 64, generator=g)
+        lp_ref = orc.model_log_prob(specs, {k: v.detach() for k, v in ref.items()}, x)
+        rel_close(model.log_prob(x.to(hip_device)), lp_ref, 1e-5, "log_prob after training")
+
+
+def test_reverse_kl_grads(hip_device):
+    """setup.py:90-94 reverseKL through model.inverse (gradient w.r.t. the
+    prior draws and the weights)."""
+    model = _c3(2, seed=7)
+    specs = _specs(model)
+    ref = {k: v.detach().clone().requires_grad_(True) for k, v in model.named_parameters()}
+    z = torch.randn(1024, 64, generator=torch.Generator().manual_seed(2))
+    zr = z.clone().requires_grad_(True)
+    xr, ldr = orc.model_inverse(specs, ref, zr)
+    loss_ref = torch.mean(xr.pow(2).sum(1)) + torch.mean(orc.normal_log_prob(zr) - ldr)
+    loss_ref.backward()
+    model = _to_dev(model, hip_device)
+    zg = z.to(hip_device).requires_grad_(True)
+    x, ld = model.inverse(zg)
+    loss = torch.mean(x.pow(2).sum(1)) + torch.mean(model.prior.log_prob(zg) - ld)
+    loss.backward()
+    rel_close(loss, loss_ref, 1e-5, "loss")
+    rel_close(zg.grad, zr.grad, what="z.grad")
+    for k, p in model.named_parameters():
+        rel_close(p.grad, ref[k].grad, what=k)
+
+
+def test_no_grad_path_unchanged(hip_device):
+    """With grad enabled but nothing requiring grad, the in-place chain runs
+    (no autograd nodes) and evaluate() never builds a graph."""
+    model = _to_dev(_c3(2), hip_device)
+    x = torch.randn(256, 64, device=hip_device)
+    for p in model.parameters():
+        p.requires_grad_(False)
+    z, plp, ld = model(x)
+    assert not z.requires_grad
+    for p in model.parameters():
+        p.requires_grad_(True)
+    lp = model.evaluate(x)
+    assert not lp.requires_grad
+    z2, plp2, ld2 = model(x)
+    assert z2.requires_grad
+    rel_close(z2, z, 1e-6, "z")
+    rel_close(plp2 + ld2, lp, 1e-5, "log_prob")
+
+
+# --------------------------------------------------------------------------- DDP
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _build_mixed(seed):
+    torch.manual_seed(seed)
+    flows = [_radial(64)] + [nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=100, mask=[i % 2])
+                             for i in range(2)]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(64), torch.eye(64))
+    return nfm.NormalizingFlowModel(prior, flows)
+
+
+def _ddp_worker(rank, world, port, x, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    try:
+        import torch.distributed as dist
+        from normalizingflow_amd import dist as nfd
+        nfd.init_from_env(backend="gloo")
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        model = _to_dev(_build_mixed(21), dev)
+        ddp = nfd.data_parallel(model, device=dev)
+        xs = nfd.shard(x).to(dev)
+        z, plp, ld = ddp(xs)
+        loss = -torch.mean(plp + ld)
+        loss.backward()
+        # numpy: pickled by value (a torch CPU tensor would be shared through a
+        # file descriptor that vanishes when this process exits)
+        q.put((rank, {k: p.grad.cpu().numpy() for k, p in model.named_parameters()}))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+def test_ddp_world2_grads_equal_full_batch():
+    model = _build_mixed(21)
+    specs = [spec_of(f, "flows.%d." % i) for i, f in enumerate(model.flows)]
+    ref = {k: v.detach().clone().requires_grad_(True) for k, v in model.named_parameters()}
+    x = torch.randn(4096, 64, generator=torch.Generator().manual_seed(8)) * 0.8
+    _, plp, ld = orc.model_forward(specs, ref, x)
+    (-torch.mean(plp + ld)).backward()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, x, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, grads in out:
+        assert isinstance(grads, dict), grads
+        for k, g in grads.items():
+            rel_close(torch.from_numpy(g), ref[k].grad, what="rank%d %s" % (rank, k))
