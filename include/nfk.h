@@ -78,6 +78,24 @@ int nfk_rqs_coupling(const float* x, int64_t ldx, const float* params,
                      int32_t param_mode, int32_t inverse, int32_t* status,
                      nfk_stream_t stream);
 
+/* Backward (vector-Jacobian product) of nfk_rqs_coupling: same x / params /
+ * maps / spline arguments as the forward call, plus the upstream gradients
+ *   gz [batch, ldgz]   dL/dz (may be NULL: 0),  glogdet [batch] dL/dlog|det|
+ *   (may be NULL: 0).
+ * Writes gparams (dense, the layout of params) = dL/dparams, and
+ *   gx[:, up_in[j]] = dL/dx_up,  gx[:, lo_in[q]] = gz[:, lo_out[q]]
+ * (the conditioner's contribution to the lower coordinates is added by the
+ * caller after its own backward).  No status words: the forward reported them.
+ * Replaces the autograd graph of nf/flows.py:227-253 + nf/utils.py:27-152. */
+int nfk_rqs_coupling_bwd(const float* x, int64_t ldx, const float* params,
+                         const int32_t* up_in, const int32_t* up_out, int32_t n_up,
+                         const int32_t* lo_in, const int32_t* lo_out, int32_t n_lo,
+                         const float* gz, int64_t ldgz, const float* glogdet,
+                         float* gparams, float* gx, int64_t ldgx, int64_t batch, int32_t K,
+                         double left, double right, double bottom, double top, int32_t tails,
+                         double min_bin_width, double min_bin_height, double min_derivative,
+                         int32_t param_mode, int32_t inverse, nfk_stream_t stream);
+
 /* searchsorted (nf/utils.py:20-25), including its side effect:
  *   bin_locations[r, n_loc-1] += eps  (in place, fp32), then
  *   idx[r] = #{j : inputs[r] >= bin_locations[r, j]} - 1

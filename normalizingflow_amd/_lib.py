@@ -27,6 +27,15 @@ F32 = ctypes.c_float
 SIGNATURES = {
     "nfk_abi_version": (ctypes.c_int, []),
     "nfk_last_error": (ctypes.c_char_p, []),
+    "nfk_rqs_coupling_bwd": (ctypes.c_int, [
+        P, I64, P,                      # x, ldx, params
+        P, P, I32,                      # up_in, up_out, n_up
+        P, P, I32,                      # lo_in, lo_out, n_lo
+        P, I64, P,                      # gz, ldgz, glogdet
+        P, P, I64, I64, I32,            # gparams, gx, ldgx, batch, K
+        F64, F64, F64, F64, I32,        # left, right, bottom, top, tails
+        F64, F64, F64,                  # min_bin_width, min_bin_height, min_derivative
+        I32, I32, P]),                  # param_mode, inverse, stream
     "nfk_rqs_coupling": (ctypes.c_int, [
         P, I64, P,                      # x, ldx, params
         P, P, I32,                      # up_in, up_out, n_up

@@ -72,6 +72,9 @@ class _LayerFn(torch.autograd.Function):
     def backward(ctx, gz, gld):
         x, *params = ctx.saved_tensors
         need = ctx.needs_input_grad[4:]
+        vjp = getattr(ctx.layer, "_vjp", None)
+        if vjp is not None:
+            return (None, None, None, None, *vjp(x, ctx.names, params, gz, gld, ctx.inverse, need))
         with torch.enable_grad():
             xd = x.detach().requires_grad_(need[0])
             pd = [p.detach().requires_grad_(n) for p, n in zip(params, need[1:])]
@@ -333,6 +336,33 @@ class NSF_CL(_HipFlow):
                         left=-b, right=b, bottom=-b, top=b, tails=True, param_mode=0,
                         inverse=inverse, status=status)
         return z
+
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward: the conditioner is recomputed and differentiated by torch
+        (hipBLASLt GEMMs), the spline by nfk_rqs_coupling_bwd."""
+        maps = self._maps(x.device)
+        with torch.enable_grad():
+            lower = x.detach().index_select(1, maps.lo_in_long).requires_grad_(need[0])
+            pd = {n: t.detach().requires_grad_(r) for n, t, r in zip(names, params, need[1:])}
+            raw = torch_math.conditioner(self, pd, "psi", lower)
+        rawc = raw.detach().contiguous()
+        gp = torch.empty_like(rawc)
+        gx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        b = float(self.B)
+        K_.rqs_coupling_bwd(x, rawc, maps.up_in, maps.up_out,
+                            None if gz is None else gz.contiguous(),
+                            None if gld is None else gld.contiguous(), gp, gx, lo_in=maps.lo_in,
+                            lo_out=maps.lo_out, K=self.K, left=-b, right=b, bottom=-b, top=b,
+                            tails=True, param_mode=0, inverse=inverse)
+        inputs = [t for t in [lower] + list(pd.values()) if t.requires_grad]
+        got = list(torch.autograd.grad(raw, inputs, gp, allow_unused=True)) if inputs else []
+        g_lower = got.pop(0) if need[0] else None
+        if g_lower is not None:
+            gx.index_add_(1, maps.lo_in_long, g_lower)
+        out = [gx if need[0] else None]
+        for t in pd.values():
+            out.append(got.pop(0) if t.requires_grad else None)
+        return out
 
     def forward(self, x):
         return self._call(x, False)

@@ -129,6 +129,35 @@ def rqs_coupling(x, params, up_in, up_out, z, *, lo_in=None, lo_out=None, logdet
               _vec(status, 1, "status", torch.int32), _stream(dev))
 
 
+def rqs_coupling_bwd(x, params, up_in, up_out, gz, glogdet, gparams, gx, *, lo_in=None,
+                     lo_out=None, K, left, right, bottom, top, tails=True, min_bin_width=1e-3,
+                     min_bin_height=1e-3, min_derivative=1e-3, param_mode=0, inverse=False):
+    """Backward of rqs_coupling (nfk_rqs_coupling_bwd): writes gparams (layout of
+    params) and gx (upper columns = dL/dx, lower columns = gz pass-through)."""
+    dev = _require_hip(x, params, up_in, gz, glogdet, gparams, gx)
+    B = x.shape[0]
+    n_up = up_in.numel()
+    n_lo = 0 if lo_in is None else lo_in.numel()
+    per = 3 * K + 1 if param_mode == 2 else 3 * K - 1
+    for name, t in (("params", params), ("gparams", gparams)):
+        if t.dtype != F32 or not t.is_contiguous() or t.numel() != B * n_up * per:
+            raise ValueError("%s must be a dense float32 [B, n_up, %d] tensor" % (name, per))
+    xp, ldx = _mat(x, "x")
+    gxp, ldgx = _mat(gx, "gx")
+    gzp, ldgz = (None, 0) if gz is None else _mat(gz, "gz")
+    if gx.shape[0] != B or (gz is not None and gz.shape[0] != B):
+        raise ValueError("gradient batch mismatch")
+    for m in (up_in, up_out, lo_in, lo_out):
+        if m is not None and (m.dtype != torch.int32 or not m.is_contiguous()):
+            raise ValueError("index maps must be contiguous int32")
+    _timed("nfk_rqs_coupling_bwd", dev, "nfk_rqs_coupling_bwd", xp, ldx, params.data_ptr(),
+           up_in.data_ptr(), up_out.data_ptr(), n_up, _ptr(lo_in), _ptr(lo_out), n_lo, gzp, ldgz,
+           _vec(glogdet, B, "glogdet"), gparams.data_ptr(), gxp, ldgx, B, K, float(left),
+           float(right), float(bottom), float(top), 1 if tails else 0, float(min_bin_width),
+           float(min_bin_height), float(min_derivative), param_mode, 1 if inverse else 0,
+           _stream(dev))
+
+
 def searchsorted(bin_locations, inputs, eps=1e-6):
     dev = _require_hip(bin_locations, inputs)
     if bin_locations.dtype != F32 or not bin_locations.is_contiguous():

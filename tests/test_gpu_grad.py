@@ -269,3 +269,60 @@ def test_ddp_world2_grads_equal_full_batch():
         assert isinstance(grads, dict), grads
         for k, g in grads.items():
             rel_close(torch.from_numpy(g), ref[k].grad, what="rank%d %s" % (rank, k))
+
+
+# --------------------------------------------------------------------------- kernel
+def _spline_ref(mode, x, u, K, B, inverse):
+    """Reference function of the raw per-element parameters for each param_mode."""
+    uw, uh, ud = u[..., :K], u[..., K:2 * K], u[..., 2 * K:]
+    if mode == 0:   # NSF_CL raw conditioner output (flows.py:233-236)
+        return orc.unconstrained_rq_spline(x, 2 * B * torch.softmax(uw, -1),
+                                           2 * B * torch.softmax(uh, -1), F.softplus(ud),
+                                           inverse=inverse, tail_bound=B, strict=False)
+    if mode == 1:   # unconstrained_RQS arguments (utils.py:27)
+        return orc.unconstrained_rq_spline(x, uw, uh, ud, inverse=inverse, tail_bound=B,
+                                           strict=False)
+    y, lad, _ = orc.rq_spline(x, uw, uh, ud, inverse=inverse, left=-B, right=B, bottom=-B, top=B)
+    return y, lad
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("K", [3, 8, 16])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_rqs_coupling_bwd_kernel_vs_fp64_autograd(mode, K, inverse, hip_device):
+    """nfk_rqs_coupling_bwd against the fp64 autograd of the oracle spline, with
+    inputs inside and outside [-B, B] (identity tails) and gz, gld both live."""
+    from normalizingflow_amd import kernels as K_
+    n, n_up, B = 2048, 4, 3.0
+    P = 3 * K + 1 if mode == 2 else 3 * K - 1
+    g = torch.Generator().manual_seed(K * 7 + mode)
+    scale = 3.5 if mode != 2 else 2.9   # mode 2 has no tails: stay inside
+    x = (torch.rand(n, n_up, generator=g) * 2 - 1) * scale
+    u = torch.randn(n, n_up, P, generator=g)
+    gz = torch.randn(n, n_up, generator=g)
+    gld = torch.randn(n, generator=g)
+    x64, u64 = x.double().requires_grad_(True), u.double().requires_grad_(True)
+    y, lad = _spline_ref(mode, x64, u64, K, B, inverse)
+    ((y * gz.double()).sum() + (lad.sum(1) * gld.double()).sum()).backward()
+    dev = hip_device
+    idx = torch.arange(n_up, dtype=torch.int32, device=dev)
+    gp = torch.empty(n, n_up * P, device=dev)
+    gx = torch.empty(n, n_up, device=dev)
+    K_.rqs_coupling_bwd(x.to(dev), u.reshape(n, -1).contiguous().to(dev), idx, idx, gz.to(dev),
+                        gld.to(dev), gp, gx, K=K, left=-B, right=B, bottom=-B, top=B,
+                        tails=(mode != 2), param_mode=mode, inverse=inverse)
+    torch.cuda.synchronize()
+    # the fp32 autograd of the same function (what the reference computes)
+    # sets the bar: ours must be within 2e-4 of fp64 or on par with it
+    x32, u32 = x.clone().requires_grad_(True), u.clone().requires_grad_(True)
+    y32, lad32 = _spline_ref(mode, x32, u32, K, B, inverse)
+    ((y32 * gz).sum() + (lad32.sum(1) * gld).sum()).backward()
+    for name, ours, r32, r64 in (("gx", gx, x32.grad, x64.grad),
+                                 ("gparams", gp.reshape(n, n_up, P), u32.grad, u64.grad)):
+        scale = float(r64.abs().max())
+        e32 = float((r32.double() - r64).abs().max()) / scale
+        rel_close(ours, r64, max(2e-4, 4 * e32), name)
+    out = ~((x >= -B) & (x <= B))
+    if mode != 2 and bool(out.any()):
+        assert torch.equal(gx.cpu()[out], gz[out])
+        assert bool((gp.cpu().reshape(n, n_up, P)[out] == 0).all())
