@@ -96,6 +96,26 @@ int nfk_rqs_coupling_bwd(const float* x, int64_t ldx, const float* params,
                          double min_bin_width, double min_bin_height, double min_derivative,
                          int32_t param_mode, int32_t inverse, nfk_stream_t stream);
 
+/* MAF (nf/flows_1.py:159-195): per-coordinate affine map of the columns
+ * [c0, c1) with (mu_i, alpha_i) = init_param[0..1] for i = 0 and
+ * params[b*ldp + 2*(i - max(c0,1)) + {0,1}] (the conditioner outputs) otherwise.
+ *   forward: out[b, dim-1-i] = (x[b,i] - mu_i) / exp(alpha_i),  log|det| -= alpha_i
+ *   inverse: out[b, i] = mu_i + exp(alpha_i) * x[b, dim-1-i],   log|det| += alpha_i
+ * (the output flip of flows_1.py:183 and the input flip of :187 are folded in).
+ * The inverse is sequential in i: call it once per column after the
+ * conditioner of that column has read out[:, :i]. */
+int nfk_maf(const float* x, int64_t ldx, const float* init_param, const float* params,
+            int64_t ldp, int32_t c0, int32_t c1, int32_t dim, float* out, int64_t ldo,
+            float* logdet, int32_t logdet_mode, int64_t batch, int32_t inverse,
+            nfk_stream_t stream);
+
+/* ActNorm (nf/flows_1.py:198-215): z = x*exp(log_sigma) + mu (inverse
+ * (z - mu)/exp(log_sigma)); log|det| = +-sum(log_sigma), a scalar, written to
+ * ld_scalar (may be NULL) and/or written/accumulated into logdet[batch]. */
+int nfk_actnorm(const float* x, int64_t ldx, const float* mu, const float* log_sigma,
+                int32_t dim, float* z, int64_t ldz, float* logdet, int32_t logdet_mode,
+                float* ld_scalar, int64_t batch, int32_t inverse, nfk_stream_t stream);
+
 /* searchsorted (nf/utils.py:20-25), including its side effect:
  *   bin_locations[r, n_loc-1] += eps  (in place, fp32), then
  *   idx[r] = #{j : inputs[r] >= bin_locations[r, j]} - 1

@@ -27,6 +27,13 @@ F32 = ctypes.c_float
 SIGNATURES = {
     "nfk_abi_version": (ctypes.c_int, []),
     "nfk_last_error": (ctypes.c_char_p, []),
+    "nfk_maf": (ctypes.c_int, [
+        P, I64, P, P, I64,              # x, ldx, init_param, params, ldp
+        I32, I32, I32, P, I64,          # c0, c1, dim, out, ldo
+        P, I32, I64, I32, P]),          # logdet, logdet_mode, batch, inverse, stream
+    "nfk_actnorm": (ctypes.c_int, [
+        P, I64, P, P, I32, P, I64,      # x, ldx, mu, log_sigma, dim, z, ldz
+        P, I32, P, I64, I32, P]),       # logdet, logdet_mode, ld_scalar, batch, inverse, stream
     "nfk_rqs_coupling_bwd": (ctypes.c_int, [
         P, I64, P,                      # x, ldx, params
         P, P, I32,                      # up_in, up_out, n_up

@@ -466,7 +466,6 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     const float* pk = a.pack;
     const bool row_ok = sl < nrows;
     const int NP = 2 + 3 * a.NCH;
-    const float* w3 = pk + a.o_w3;
     // execution order of the three records of a chunk: searched knots, other knots, derivatives
     const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
 

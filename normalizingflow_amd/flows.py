@@ -15,6 +15,9 @@ What runs where (ROCm device only -- CPU tensors raise, there is no fallback):
   Planar         nfk_planar -- flows_1.py:21-63
   Radial         nfk_radial_sumsq (+ optional all-reduce) + nfk_radial_apply
                  -- flows_1.py:66-97
+  MAF            per-coordinate FCNN conditioners + nfk_maf -- flows_1.py:159-195
+  ActNorm        nfk_actnorm -- flows_1.py:198-215
+  OneByOneConv   x @ P @ L @ (U + diag S) as library GEMMs -- flows_1.py:218-252
 Gradients: when autograd needs them (grad mode on and x or a parameter
 requires grad) a layer runs as ``_LayerFn``: the forward is the same HIP
 kernel chain; backward recomputes the layer from the saved input with the
@@ -38,7 +41,8 @@ from . import kernels as K_
 from . import torch_math
 from ._lib import ST_INSIDE_SEEN, ST_NEG_DISC
 
-__all__ = ["FCNN", "RealNVP", "NSF_AR", "NSF_CL", "Planar", "Radial", "functional_derivatives"]
+__all__ = ["FCNN", "RealNVP", "NSF_AR", "NSF_CL", "Planar", "Radial", "MAF", "ActNorm",
+           "OneByOneConv", "functional_derivatives"]
 
 # flows.py:12-18 -- kept for API parity (used by Planar's CPU reference semantics)
 functional_derivatives = {
@@ -530,3 +534,154 @@ class Radial(_HipFlow):
 
     def forward(self, x):
         return self._call(x, False)
+
+
+class MAF(_HipFlow):
+    """Masked autoregressive flow (flows_1.py:159-195).
+
+    Coordinate i is mapped by z_i = (x_i - mu_i) / exp(alpha_i) with
+    (mu_i, alpha_i) = layers[i-1](x[:, :i]) (``initial_param`` for i = 0); the
+    output is flipped along the features.  The forward conditioners all read
+    x, so they run first and one nfk_maf launch maps every column; the inverse
+    is sequential (column i conditions on the already-inverted columns).
+    The reference allocates its log|det| on the CPU (flows_1.py:176), so it only
+    runs on CPU tensors; here it runs on the device.
+    """
+
+    def __init__(self, dim, hidden_dim=8, base_network=FCNN):
+        super().__init__()
+        self.dim = dim
+        self.layers = nn.ModuleList()
+        self.initial_param = nn.Parameter(torch.Tensor(2))
+        for i in range(1, dim):
+            self.layers += [base_network(i, 2, hidden_dim)]
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        init.uniform_(self.initial_param, -math.sqrt(0.5), math.sqrt(0.5))
+
+    def _run(self, x, inverse, logdet, mode, status):
+        if x.shape[1] != self.dim:
+            raise RuntimeError("MAF(dim=%d) got %d features" % (self.dim, x.shape[1]))
+        out = torch.empty_like(x, memory_format=torch.contiguous_format)
+        ip = self.initial_param.detach().to(torch.float32).contiguous()
+        if not inverse:
+            prm = (torch.cat([self.layers[i - 1](x[:, :i]) for i in range(1, self.dim)], dim=1)
+                   if self.dim > 1 else None)
+            K_.maf(x, ip, prm, out, 0, self.dim, logdet=logdet, logdet_mode=mode)
+            return out
+        K_.maf(x, ip, None, out, 0, 1, logdet=logdet, logdet_mode=mode, inverse=True)
+        m2 = K_.MODE_ACC if mode != K_.MODE_NONE else K_.MODE_NONE
+        for i in range(1, self.dim):
+            prm = self.layers[i - 1](out[:, :i])
+            K_.maf(x, ip, prm, out, i, i + 1, logdet=logdet, logdet_mode=m2, inverse=True)
+        return out
+
+    def forward(self, x):
+        return self._call(x, False)
+
+    def inverse(self, z):
+        return self._call(z, True)
+
+
+class ActNorm(_HipFlow):
+    """ActNorm (flows_1.py:198-215): z = x * exp(log_sigma) + mu; log|det| is
+    the scalar sum(log_sigma) (shape [], broadcast by the model)."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.mu = nn.Parameter(torch.zeros(dim, dtype=torch.float))
+        self.log_sigma = nn.Parameter(torch.zeros(dim, dtype=torch.float))
+
+    def _launch(self, x, inverse, logdet, mode, ld_scalar):
+        if x.shape[1] != self.dim:
+            raise RuntimeError("ActNorm(dim=%d) got %d features" % (self.dim, x.shape[1]))
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        K_.actnorm(x, self.mu.detach(), self.log_sigma.detach(), z, logdet=logdet,
+                   logdet_mode=mode, ld_scalar=ld_scalar, inverse=inverse)
+        return z
+
+    def _run(self, x, inverse, logdet, mode, status):
+        return self._launch(x, inverse, logdet, mode, None)
+
+    def _eval(self, x, inverse, status):
+        ld = torch.empty((), dtype=torch.float32, device=x.device)
+        with torch.no_grad():
+            z = self._launch(x, inverse, None, K_.MODE_NONE, ld)
+        return z, ld
+
+    def forward(self, x):
+        return self._call(x, False)
+
+    def inverse(self, z):
+        return self._call(z, True)
+
+
+class OneByOneConv(_HipFlow):
+    """Invertible 1x1 convolution (flows_1.py:218-252): z = x @ P @ L @ (U + diag S).
+
+    Same construction as the reference (QR of a numpy normal matrix, scipy LU),
+    so a given ``np.random`` state yields the same P, L, S, U.  P is a
+    non-persistent buffer (the reference keeps it as a plain attribute, so it
+    is not in the state_dict either, but here it follows ``.to(device)``).  The
+    products are plain GEMMs (hipBLASLt through torch.matmul) in the
+    reference's association.  The inverse matrix is cached per weight version;
+    the reference caches it once (``if not self.W_inv``, flows_1.py:244), which
+    raises on its second call for dim > 1.
+    """
+
+    def __init__(self, dim):
+        super().__init__()
+        import scipy.linalg as sla
+        self.dim = dim
+        W, _ = sla.qr(np.random.randn(dim, dim))
+        P, L, U = sla.lu(W)
+        self.register_buffer("P", torch.tensor(P, dtype=torch.float), persistent=False)
+        self.L = nn.Parameter(torch.tensor(L, dtype=torch.float))
+        self.S = nn.Parameter(torch.tensor(np.diag(U), dtype=torch.float))
+        self.U = nn.Parameter(torch.triu(torch.tensor(U, dtype=torch.float), diagonal=1))
+        self.W_inv = None
+        self._winv_key = None
+
+    def _factors(self):
+        eye = torch.diag(torch.ones(self.dim, device=self.L.device))
+        L = torch.tril(self.L, diagonal=-1) + eye
+        U = torch.triu(self.U, diagonal=1)
+        return L, U + torch.diag(self.S)
+
+    def _logdet_scalar(self, inverse):
+        v = torch.sum(torch.log(torch.abs(self.S)))
+        return -v if inverse else v
+
+    def _z(self, x, inverse):
+        if x.shape[1] != self.dim:
+            raise RuntimeError("OneByOneConv(dim=%d) got %d features" % (self.dim, x.shape[1]))
+        L, US = self._factors()
+        if not inverse:
+            return x @ self.P @ L @ US
+        key = tuple((p.data_ptr(), p._version) for p in (self.P, self.L, self.S, self.U))
+        if self.W_inv is None or self._winv_key != key:
+            self.W_inv = torch.inverse(self.P @ L @ US)
+            self._winv_key = key
+        return x @ self.W_inv
+
+    def _run(self, x, inverse, logdet, mode, status):
+        z = self._z(x, inverse).contiguous()
+        if mode != K_.MODE_NONE:
+            ld = self._logdet_scalar(inverse)
+            if mode == K_.MODE_ACC:
+                logdet.add_(ld)
+            else:
+                logdet.copy_(ld.expand_as(logdet))
+        return z
+
+    def _eval(self, x, inverse, status):
+        with torch.no_grad():
+            return self._z(x, inverse).contiguous(), self._logdet_scalar(inverse)
+
+    def forward(self, x):
+        return self._call(x, False)
+
+    def inverse(self, z):
+        return self._call(z, True)

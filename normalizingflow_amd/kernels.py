@@ -158,6 +158,43 @@ def rqs_coupling_bwd(x, params, up_in, up_out, gz, glogdet, gparams, gx, *, lo_i
            _stream(dev))
 
 
+def maf(x, init_param, params, out, c0, c1, *, logdet=None, logdet_mode=MODE_NONE,
+        inverse=False):
+    """MAF per-coordinate affine map of columns [c0, c1) (nfk_maf)."""
+    dev = _require_hip(x, init_param, params, out, logdet)
+    B, dim = x.shape
+    if out.shape != x.shape:
+        raise ValueError("out must match x")
+    if init_param.dtype != F32 or init_param.numel() != 2 or not init_param.is_contiguous():
+        raise ValueError("init_param must be a contiguous float32 [2] tensor")
+    pp, ldp = (None, 0)
+    if params is not None:
+        pp, ldp = _mat(params, "params")
+        if params.shape[0] != B or params.shape[1] < 2 * (c1 - max(c0, 1)):
+            raise ValueError("params must be [B, >= 2 x columns]")
+    elif c1 > 1:
+        raise ValueError("params are required for columns >= 1")
+    xp, ldx = _mat(x, "x")
+    op, ldo = _mat(out, "out")
+    _lib.call("nfk_maf", xp, ldx, init_param.data_ptr(), pp, ldp, int(c0), int(c1), dim, op, ldo,
+              _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, _stream(dev))
+
+
+def actnorm(x, mu, log_sigma, z, *, logdet=None, logdet_mode=MODE_NONE, ld_scalar=None,
+            inverse=False):
+    """ActNorm (nfk_actnorm)."""
+    dev = _require_hip(x, mu, log_sigma, z, logdet, ld_scalar)
+    B, dim = x.shape
+    for name, t in (("mu", mu), ("log_sigma", log_sigma)):
+        if t.dtype != F32 or t.numel() != dim or not t.is_contiguous():
+            raise ValueError("%s must be a contiguous float32 [%d] tensor" % (name, dim))
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    _lib.call("nfk_actnorm", xp, ldx, mu.data_ptr(), log_sigma.data_ptr(), dim, zp, ldz,
+              _vec(logdet, B, "logdet"), logdet_mode, _vec(ld_scalar, 1, "ld_scalar"), B,
+              1 if inverse else 0, _stream(dev))
+
+
 def searchsorted(bin_locations, inputs, eps=1e-6):
     dev = _require_hip(bin_locations, inputs)
     if bin_locations.dtype != F32 or not bin_locations.is_contiguous():

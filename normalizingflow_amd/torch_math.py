@@ -190,8 +190,51 @@ def radial(layer, x, p, inverse):
     return z, ld
 
 
+def maf(layer, x, p, inverse):
+    """MAF.forward / inverse (flows_1.py:171-195)."""
+    dim = layer.dim
+    ip = p["initial_param"]
+    cols, ld = [], torch.zeros(x.shape[0], dtype=x.dtype, device=x.device)
+    src = x.flip(dims=(1,)) if inverse else x
+    for i in range(dim):
+        if i == 0:
+            mu, alpha = ip[0], ip[1]
+        else:
+            out = conditioner(layer, p, "layers.%d" % (i - 1),
+                              torch.stack(cols, dim=1) if inverse else x[:, :i])
+            mu, alpha = out[:, 0], out[:, 1]
+        if inverse:
+            cols.append(mu + torch.exp(alpha) * src[:, i])
+            ld = ld + alpha
+        else:
+            cols.append((src[:, i] - mu) / torch.exp(alpha))
+            ld = ld - alpha
+    z = torch.stack(cols, dim=1)
+    return (z, ld) if inverse else (z.flip(dims=(1,)), ld)
+
+
+def actnorm(layer, x, p, inverse):
+    """ActNorm.forward / inverse (flows_1.py:207-215); log|det| is a scalar."""
+    mu, ls = p["mu"], p["log_sigma"]
+    if inverse:
+        return (x - mu) / torch.exp(ls), -torch.sum(ls)
+    return x * torch.exp(ls) + mu, torch.sum(ls)
+
+
+def onebyone(layer, x, p, inverse):
+    """OneByOneConv.forward / inverse (flows_1.py:235-252)."""
+    dim = layer.dim
+    L = torch.tril(p["L"], diagonal=-1) + torch.diag(torch.ones(dim, dtype=x.dtype, device=x.device))
+    US = torch.triu(p["U"], diagonal=1) + torch.diag(p["S"])
+    P = layer.P.to(x.dtype)
+    ld = torch.sum(torch.log(torch.abs(p["S"])))
+    if inverse:
+        return x @ torch.inverse(P @ L @ US), -ld
+    return x @ P @ L @ US, ld
+
+
 _BY_CLASS = {"NSF_CL": nsf_cl, "RealNVP": realnvp, "NSF_AR": nsf_ar, "Planar": planar,
-             "Radial": radial}
+             "Radial": radial, "MAF": maf, "ActNorm": actnorm, "OneByOneConv": onebyone}
 
 
 def layer_forward(layer, x, p, inverse):

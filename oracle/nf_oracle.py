@@ -13,6 +13,7 @@ algorithm of the reference ``sherryli59/NormalizingFlow`` for the hot path:
 * affine coupling (``RealNVP``)                  -> nf/flows.py:38-76
 * autoregressive spline (``NSF_AR``)             -> nf/flows.py:152-209
 * planar / radial flows                          -> nf/flows_1.py:21-97
+* MAF / ActNorm / OneByOneConv                    -> nf/flows_1.py:159-252
 * MLP conditioner (``FCNN``)                     -> nf/flows.py:20-35
 * flow container (``NormalizingFlowModel``)      -> nf/models.py:5-40
 
@@ -282,6 +283,54 @@ def radial(x, sd, prefix):
     return z, ld
 
 
+def maf(x, sd, prefix, dim, inverse=False):
+    """MAF.forward / inverse (flows_1.py:171-195).  Columns are collected and
+    stacked instead of written in place (value-identical; keeps autograd valid
+    when a conditioner reads the columns already produced)."""
+    n = x.shape[0]
+    ip = sd[prefix + "initial_param"]
+    logdet = torch.zeros(n, dtype=x.dtype)
+    src = x.flip(dims=(1,)) if inverse else x
+    cols = []
+    for i in range(dim):
+        if i == 0:
+            mu, alpha = ip[0], ip[1]
+        else:
+            inp = torch.stack(cols, dim=1) if inverse else x[:, :i]
+            out = fcnn(inp, sd, prefix + "layers.%d." % (i - 1))
+            mu, alpha = out[:, 0], out[:, 1]
+        if inverse:
+            cols.append(mu + torch.exp(alpha) * src[:, i])
+            logdet = logdet + alpha
+        else:
+            cols.append((src[:, i] - mu) / torch.exp(alpha))
+            logdet = logdet - alpha
+    z = torch.stack(cols, dim=1)
+    return (z, logdet) if inverse else (z.flip(dims=(1,)), logdet)
+
+
+def actnorm(x, sd, prefix, inverse=False):
+    """ActNorm.forward / inverse (flows_1.py:207-215): scalar log|det|."""
+    mu, ls = sd[prefix + "mu"], sd[prefix + "log_sigma"]
+    if inverse:
+        return (x - mu) / torch.exp(ls), -torch.sum(ls)
+    return x * torch.exp(ls) + mu, torch.sum(ls)
+
+
+def onebyone(x, sd, prefix, inverse=False):
+    """OneByOneConv.forward / inverse (flows_1.py:235-252).  ``sd[prefix+"P"]``
+    must hold the permutation (the reference keeps it outside its state_dict)."""
+    Lp, S, Up, P = sd[prefix + "L"], sd[prefix + "S"], sd[prefix + "U"], sd[prefix + "P"]
+    dim = S.shape[0]
+    L = torch.tril(Lp, diagonal=-1) + torch.diag(torch.ones(dim, dtype=x.dtype))
+    U = torch.triu(Up, diagonal=1)
+    ld = torch.sum(torch.log(torch.abs(S)))
+    if inverse:
+        W = P @ L @ (U + torch.diag(S))
+        return x @ torch.inverse(W), -ld
+    return x @ P @ L @ (U + torch.diag(S)), ld
+
+
 # --------------------------------------------------------------------------
 # model container (nf/models.py:5-40)
 # --------------------------------------------------------------------------
@@ -303,6 +352,12 @@ def apply_layer(spec, x, sd, inverse=False, strict=True):
         if inverse:
             raise NotImplementedError("Radial flow has no inverse.")
         return radial(x, sd, p)
+    if t == "MAF":
+        return maf(x, sd, p, spec["dim"], inverse=inverse)
+    if t == "ActNorm":
+        return actnorm(x, sd, p, inverse=inverse)
+    if t == "OneByOneConv":
+        return onebyone(x, sd, p, inverse=inverse)
     raise KeyError(t)
 
 

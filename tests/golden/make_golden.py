@@ -113,6 +113,34 @@ def case_layer(name, ctor, kwargs, x, inverse=True, f64=True, init=None, seed=12
     _save(name, meta, arrays, layer)
 
 
+def case_onebyone(name, dim, x, seed=1234):
+    """OneByOneConv: P, L, S, U from np.random (flows_1.py:227-233); a fresh
+    instance per inverse call (the reference caches W^-1 once)."""
+    def make():
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        return rflows1.OneByOneConv(dim)
+    layer = make()
+    arrays = dict(x=x)
+    with torch.no_grad():
+        z, ld = layer.forward(x.clone())
+        arrays.update(z=z, ld=ld)
+        xi, ldi = layer.inverse(z.clone())
+        arrays.update(rt_x=xi, rt_ld=ldi)
+        xa, lda = make().inverse(x.clone())
+        arrays.update(inv_x=xa, inv_ld=lda)
+    _extra_p(layer, arrays)
+    _save(name, dict(kind="layer", type="OneByOneConv", kwargs=dict(dim=dim), seed=seed,
+                     np_seed=seed), arrays, layer)
+
+
+def actnorm_init(layer):
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(9)
+        layer.mu.copy_(torch.randn(layer.dim, generator=g) * 0.5)
+        layer.log_sigma.copy_(torch.randn(layer.dim, generator=g) * 0.3)
+
+
 def radial_init(layer):
     with torch.no_grad():
         g = torch.Generator().manual_seed(7)
@@ -122,14 +150,30 @@ def radial_init(layer):
 
 
 # ---------------------------------------------------------------- models
-def case_model(name, flow_specs, dim, var, n, seed=1234):
+def _extra_p(module, arrays):
+    """OneByOneConv keeps its permutation P outside the state_dict
+    (flows_1.py:229): save it as sd.<prefix>P so the fixture is complete."""
+    for name, m in module.named_modules():
+        if type(m).__name__ == "OneByOneConv":
+            arrays["sd." + (name + "." if name else "") + "P"] = m.P
+
+
+def case_model(name, flow_specs, dim, var, n, seed=1234, init=None):
+    import copy
     torch.manual_seed(seed)
+    np.random.seed(seed)
     flows = [ctor(**kw) for ctor, kw in flow_specs]
+    if init is not None:
+        init(flows)
     prior = torch.distributions.MultivariateNormal(torch.zeros(dim), var * torch.eye(dim))
     model = rmodels.NormalizingFlowModel(prior, flows)
+    # OneByOneConv caches W^-1 once and raises on a second inverse (flows_1.py:244):
+    # sample() runs on a fresh copy
+    model_s = copy.deepcopy(model)
     g = torch.Generator().manual_seed(seed + 1)
     x = torch.randn(n, dim, generator=g) * 1.3
     arrays = dict(x=x)
+    _extra_p(model, arrays)
     with torch.no_grad():
         z, plp, ld = model(x.clone())
         arrays.update(z=z, prior_lp=plp, ld=ld, log_prob=model.evaluate(x.clone()))
@@ -137,13 +181,34 @@ def case_model(name, flow_specs, dim, var, n, seed=1234):
             xi, ldi = model.inverse(z.clone())
             arrays.update(rt_x=xi, rt_ld=ldi)
             torch.manual_seed(seed + 2)
-            xs, lps, zs = model.sample(n)
+            xs, lps, zs = model_s.sample(n)
             arrays.update(sample_x=xs, sample_log_px=lps, sample_z=zs)
         except NotImplementedError:  # Planar / Radial have no inverse
             pass
     _save(name, dict(kind="model", dim=dim, var=var, seed=seed,
                      layers=[dict(type=c.__name__, kwargs=kw) for c, kw in flow_specs]),
           arrays, model)
+
+
+def extra_cases():
+    """flows_1.py MAF / ActNorm / OneByOneConv."""
+    g = torch.Generator().manual_seed(4242)
+    x8 = torch.randn(256, 8, generator=g) * 1.3
+    case_layer("maf_d8_h8", rflows1.MAF, dict(dim=8, hidden_dim=8), x8)
+    x5 = torch.randn(128, 5, generator=g)
+    case_layer("maf_d5_h16", rflows1.MAF, dict(dim=5, hidden_dim=16), x5)
+    case_layer("actnorm_d8", rflows1.ActNorm, dict(dim=8), x8, init=actnorm_init)
+    case_onebyone("onebyone_d8", 8, x8)
+    case_onebyone("onebyone_d16", 16, torch.randn(128, 16, generator=g))
+
+    def init_glow(flows):
+        actnorm_init(flows[0])
+    case_model("model_glow", [
+        (rflows1.ActNorm, dict(dim=8)),
+        (rflows1.OneByOneConv, dict(dim=8)),
+        (rflows.NSF_CL, dict(size=4, dim=2, K=6, B=3, hidden_dim=16, mask=[0])),
+        (rflows1.MAF, dict(dim=8, hidden_dim=8)),
+        (rflows.RealNVP, dict(dim=8, hidden_dim=16))], dim=8, var=1.0, n=128, init=init_glow)
 
 
 def main():
@@ -193,4 +258,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["extra"]:
+        extra_cases()
+    else:
+        main()
+        extra_cases()

@@ -34,3 +34,15 @@ def layer_spec(meta, prefix=""):
         spec.setdefault("dim", 3)
         spec.setdefault("mask", [1])
     return spec
+
+
+def load_into(module, sd, strict=True):
+    """load_state_dict plus OneByOneConv's permutation P, which the reference
+    keeps outside the state_dict (flows_1.py:229); fixtures carry it as
+    ``[<prefix>.]P``."""
+    extra = {k: v for k, v in sd.items() if k == "P" or k.endswith(".P")}
+    module.load_state_dict({k: v for k, v in sd.items() if k not in extra}, strict=strict)
+    for k, v in extra.items():
+        owner = module if k == "P" else module.get_submodule(k[:-2])
+        owner.P = v.clone().to(owner.P.device)
+    return module

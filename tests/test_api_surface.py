@@ -2,6 +2,7 @@
 state_dict keys and parameter-initialisation order match the reference (the
 golden fixtures hold the reference's own state_dicts built under the same
 seed), and the product path refuses CPU tensors instead of falling back."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -22,41 +23,63 @@ def build_layer(meta):
     return cls(**kw)
 
 
-LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar")]
+LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar",
+                                                       "maf", "actnorm", "onebyone")]
+# fixtures whose values were set after construction (ActNorm starts at zero, flows_1.py:204-205)
+_REINIT = ("mu", "log_sigma")
+
+
+def _check_values(ours, sd, module):
+    """Same keys; same values except re-initialised ActNorm parameters; OneByOneConv's
+    P (outside the state_dict, flows_1.py:229) equals the fixture's under the same
+    numpy seed."""
+    keys = [k for k in sd if not (k == "P" or k.endswith(".P"))]
+    assert list(ours.keys()) == keys
+    for k in keys:
+        if k.split(".")[-1] in _REINIT:
+            continue
+        torch.testing.assert_close(ours[k], sd[k], rtol=0, atol=0)
+    for k in sd:
+        if k == "P" or k.endswith(".P"):
+            owner = module if k == "P" else module.get_submodule(k[:-2])
+            torch.testing.assert_close(owner.P, sd[k], rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("name", LAYERS)
 def test_same_seed_same_weights_and_keys(name):
     meta, _, sd = gio.load(name)
     torch.manual_seed(meta["seed"])
+    np.random.seed(meta.get("np_seed", 0))
     layer = build_layer(meta)
     ours = layer.state_dict()
-    assert list(ours.keys()) == list(sd.keys())
     if meta["type"] == "Radial":
-        return  # the reference leaves Radial's parameters uninitialised (flows_1.py:72-83)
-    for k in sd:
-        torch.testing.assert_close(ours[k], sd[k], rtol=0, atol=0)
+        # the reference leaves Radial's parameters uninitialised (flows_1.py:72-83)
+        assert list(ours.keys()) == list(sd.keys())
+        return
+    _check_values(ours, sd, layer)
 
 
 @pytest.mark.parametrize("name", gio.names("model_"))
 def test_model_state_dict_round_trip(name):
     meta, _, sd = gio.load(name)
     torch.manual_seed(meta["seed"])
+    np.random.seed(meta["seed"])
     flows = []
     for l in meta["layers"]:
         flows.append(build_layer(dict(type=l["type"], kwargs=l["kwargs"])))
     d = meta["dim"]
     prior = torch.distributions.MultivariateNormal(torch.zeros(d), meta["var"] * torch.eye(d))
     model = nfm.NormalizingFlowModel(prior, flows)
-    assert list(model.state_dict().keys()) == list(sd.keys())
-    for k in sd:
-        torch.testing.assert_close(model.state_dict()[k], sd[k], rtol=0, atol=0)
-    model.load_state_dict(sd, strict=False)
+    _check_values(model.state_dict(), sd, model)
+    gio.load_into(model, sd)
 
 
 def test_exports():
     for n in ("FCNN", "RealNVP", "NSF_AR", "NSF_CL", "Planar", "Radial"):
         assert hasattr(nff, n)
+    import nf.flows_1 as nff1
+    for n in ("FCNN", "RealNVP", "NSF_AR", "Planar", "Radial", "MAF", "ActNorm", "OneByOneConv"):
+        assert hasattr(nff1, n)
     assert nfm.NormalizingFlow is nfm.NormalizingFlowModel
     assert hasattr(nfm.NormalizingFlowModel, "log_prob")
     for n in ("unconstrained_RQS", "RQS", "searchsorted", "DEFAULT_MIN_BIN_WIDTH"):

@@ -73,6 +73,12 @@ def spec_of(layer, prefix):
         return dict(type="Planar", prefix=prefix, nonlinearity=layer.h.__name__)
     if isinstance(layer, nff.Radial):
         return dict(type="Radial", prefix=prefix)
+    if isinstance(layer, nff.MAF):
+        return dict(type="MAF", prefix=prefix, dim=layer.dim)
+    if isinstance(layer, nff.ActNorm):
+        return dict(type="ActNorm", prefix=prefix)
+    if isinstance(layer, nff.OneByOneConv):
+        return dict(type="OneByOneConv", prefix=prefix)
     raise TypeError(type(layer))
 
 
@@ -81,14 +87,15 @@ def cpu_sd(module):
 
 
 # --------------------------------------------------------------------------- golden
-LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar")]
+LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar",
+                                                               "maf", "actnorm", "onebyone")]
 
 
 @pytest.mark.parametrize("name", LAYERS)
 def test_layer_vs_reference_golden(name, hip_device):
     meta, d, sd = gio.load(name)
     layer = build_layer(meta)
-    layer.load_state_dict(sd)
+    gio.load_into(layer, sd)
     layer = layer.to(hip_device)
     with torch.no_grad():
         z, ld = layer(d["x"].to(hip_device))
@@ -109,7 +116,7 @@ def _golden_model(meta, sd, device):
     prior = torch.distributions.MultivariateNormal(torch.zeros(d, device=device),
                                                    meta["var"] * torch.eye(d, device=device))
     model = nfm.NormalizingFlowModel(prior, flows)
-    model.load_state_dict(sd, strict=False)
+    gio.load_into(model, sd, strict=False)
     return model.to(device)
 
 

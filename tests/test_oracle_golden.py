@@ -31,7 +31,8 @@ def test_rqs_fixture(name):
     _close(y64, d["y_f64"], rtol=1e-12, atol=1e-12); _close(lad64, d["lad_f64"], rtol=1e-12, atol=1e-12)
 
 
-LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar")]
+LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar",
+                                                               "maf", "actnorm", "onebyone")]
 
 
 @pytest.mark.parametrize("name", LAYERS)

@@ -181,3 +181,22 @@ def test_layer_fn_plumbing_cpu():
     _, ld3 = nff._LayerFn.apply(L, False, None, tuple(n for n, _ in named), xc, *(t for _, t in named))
     ld3.sum().backward()
     assert xc.grad is not None and torch.isfinite(xc.grad).all()
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_maf_actnorm_onebyone_grads(inverse):
+    torch.manual_seed(10)
+    x = torch.randn(24, 6)
+    L = nff.MAF(6, hidden_dim=8)
+    _compare(L, lambda xx, sd, inv: orc.maf(xx, sd, "l.", 6, inverse=inv), x, inverse)
+    A = nff.ActNorm(6)
+    with torch.no_grad():
+        A.mu.normal_(0, 0.5)
+        A.log_sigma.normal_(0, 0.3)
+    _compare(A, lambda xx, sd, inv: orc.actnorm(xx, sd, "l.", inverse=inv), x, inverse)
+    np_state = __import__("numpy").random.seed(3)
+    C = nff.OneByOneConv(6)
+    P = C.P.clone()
+    _compare(C, lambda xx, sd, inv: orc.onebyone(xx, dict(sd, **{"l.P": P}), "l.", inverse=inv),
+             x, inverse)
+    del np_state
