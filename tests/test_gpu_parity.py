@@ -430,7 +430,8 @@ def test_c3_full_batch_properties(hip_device):
     pre = nfm.NormalizingFlowModel(model.prior, [nff.NSF_CL(size=32, dim=2, K=8, B=3,
                                                             hidden_dim=100, mask=[0])
                                                  for _ in range(4)]).to(hip_device)
-    z, _, ld_f = pre(xd)
-    xr, ld_i = pre.inverse(z)
+    with torch.no_grad():
+        z, _, ld_f = pre(xd)
+        xr, ld_i = pre.inverse(z)
     assert float((xr - xd).abs().max()) < 1e-3
     assert float((ld_f + ld_i).abs().max()) < 1e-3
