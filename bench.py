@@ -53,6 +53,15 @@ METRICS = {
 }
 
 
+# conditioner arithmetic of the fused layer kernels per workload
+_SPLIT = "fp16 two-way split (hi+lo, 3 MFMA products, fp32 accumulate, power-of-two pre-scaling)"
+ARITH = {
+    "c3": _SPLIT + "; 4-feature k-tail on f32 MFMA (nfk_fused_impl.h)",
+    "c2": _SPLIT + "; 4-feature k-tail on f32 MFMA (nfk_fused_rnvp.hip)",
+    "c5": _SPLIT + " (nfk_fused_wide.h)",
+}
+
+
 def build_model(workload, device):
     import nf.flows as nff
     import nf.models as nfm
@@ -174,15 +183,19 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic):
             "per_launch": "%d samples x %.0f B" % (B, byts / B)}
 
 
-def load_traffic(kernel):
+def load_traffic(kernel, workload):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
+    (profiles/pmc_traffic.json: entries keyed "<workload>:<kernel>", or by the
+    kernel alone for the c3 default)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            rec = json.load(f).get(kernel)
+            tab = json.load(f)
     except (OSError, ValueError):
         return None
+    rec = tab.get("%s:%s" % (workload, kernel))
+    if rec is None and workload == "c3":
+        rec = tab.get(kernel)
     return None if rec is None else rec.get("bytes_per_launch")
 
 
@@ -246,7 +259,7 @@ def main():
     if rank == 0:
         value = world * B * args.steps / dt
         dom = max(summary.items(), key=lambda kv: kv[1][2])[0] if summary else None
-        rl = roofline(args.workload, summary, B, load_traffic(dom) if dom else None)
+        rl = roofline(args.workload, summary, B, load_traffic(dom, args.workload) if dom else None)
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.workload, {k: v.cpu() for k, v in sd.items()})
@@ -267,10 +280,8 @@ def main():
             "config": {"workload": args.workload + ": " + desc, "global_batch": world * B,
                        "per_gpu_batch": B, "parallelism": "dp%d (sample sharding)" % world,
                        "fused_layer_kernel": bool(config.USE_FUSED),
-                       "conditioner_arith": ("fp16 two-way split (hi+lo, 3 MFMA products, fp32 "
-                                             "accumulate, power-of-two pre-scaling); 4-feature "
-                                             "k-tail on f32 MFMA")
-                       if (config.USE_FUSED and args.workload == "c3") else "f32 (rocBLAS)"},
+                       "conditioner_arith": ARITH.get(args.workload) if config.USE_FUSED
+                       else "f32 (rocBLAS)"},
             "roofline": rl,
             "cpu_baseline": cpu,
             "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4)} for k, v in summary.items()},

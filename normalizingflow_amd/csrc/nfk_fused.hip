@@ -42,12 +42,16 @@ NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, d
                               int tails, double min_w, double min_h, double min_d);
 
 #include "nfk_fused_impl.h"
+#include "nfk_fused_wide.h"
 
 using namespace nfk_fused;
 
 namespace nfk_fused {
 #define NFK_X(h, t) NFK_FUSED_K(NFK_FUSED_EXTERN, h, t)
 NFK_FUSED_KB(NFK_X)
+#undef NFK_X
+#define NFK_X(h) NFK_WIDE_K(NFK_WIDE_EXTERN, h)
+NFK_WIDE_KB(NFK_X)
 #undef NFK_X
 }  // namespace nfk_fused
 
@@ -136,83 +140,137 @@ __device__ uint32_t pack_record_word(int blk, int wl, const Layout& L, int nt, f
     return __float_as_uint(t < nt ? bias_of(t, i) * bsc : 0.0f);
 }
 
-// One thread per packed 32-bit word (layout described in nfk_fused_impl.h).
-__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+struct PackScales {
+    float sc1, sc2, sc3, bs2, bs3;
+};
+
+// Word g (>= L.o_h1) of the record layout (nfk_fused_impl.h).
+__device__ uint32_t pack_word(const PackArgs& a, int64_t g, const PackScales& ps) {
     const Layout& L = a.L;
+    const float sc1 = ps.sc1, sc2 = ps.sc2, sc3 = ps.sc3, bs2 = ps.bs2, bs3 = ps.bs3;
+    const int kbh = L.KBH;
+    if (g < L.o_h2) {  // layer 1: KB1 f16 k-blocks over the n_lo inputs + unscaled bias
+        const int64_t w = g - L.o_h1;
+        const int blk = (int)(w >> 8), wl = (int)(w & 255);
+        if (blk < L.KB1 * L.HT * 2) {
+            const int part = blk & 1, idx = blk >> 1, kb = idx / L.HT, t = idx - kb * L.HT;
+            const int lane = wl >> 2, j = 2 * (wl & 3);
+            const int f = hid_feature(t, lane & 15, kbh), k0 = 32 * kb + 8 * (lane >> 4) + j;
+            float v0 = 0.0f, v1 = 0.0f;
+            if (f < L.H) {
+                if (k0 < L.n_lo) v0 = a.w0[(int64_t)f * L.n_lo + k0] * sc1;
+                if (k0 + 1 < L.n_lo) v1 = a.w0[(int64_t)f * L.n_lo + k0 + 1] * sc1;
+            }
+            return f16_part_pair(v0, v1, part);
+        } else {
+            const int t = wl >> 4, f = hid_feature(t, wl & 15, kbh);
+            return __float_as_uint((t < L.HT && f < L.H) ? a.b0[f] : 0.0f);
+        }
+    }
+    if (g < L.o_w3) {  // layer 2
+        const int64_t w = g - L.o_h2;
+        return pack_record_word(
+            (int)(w >> 8), (int)(w & 255), L, L.HT, sc2, bs2,
+            [&](int t, int i) -> const float* {
+                const int f = hid_feature(t, i, kbh);
+                return f < L.H ? a.w2 + (int64_t)f * L.H : nullptr;
+            },
+            [&](int t, int i) -> float {
+                const int f = hid_feature(t, i, kbh);
+                return f < L.H ? a.b2[f] : 0.0f;
+            });
+    }
+    // output layer: chunk, phase (W, H, D)
+    const int64_t w3 = g - L.o_w3;
+    const int64_t bl = w3 >> 8;
+    const int chunk = (int)(bl / L.blk_chunk);
+    int b = (int)(bl - (int64_t)chunk * L.blk_chunk);
+    int nt = L.wide ? (L.K + 1) / 2 : L.K, pbase = 0, np = L.K;
+    if (b >= L.blk_w) {
+        b -= L.blk_w;
+        pbase = L.K;
+        if (b >= L.blk_w) {
+            b -= L.blk_w;
+            pbase = 2 * L.K;
+            nt = L.wide ? L.K / 2 : L.K - 1;
+            np = L.K - 1;
+        }
+    }
+    // (coordinate, parameter) of row i of tile t (Layout: wide form or 16-coordinate form)
+    auto coord = [&](int i) { return L.wide ? 8 * chunk + 2 * (i >> 2) + ((i >> 1) & 1) : 16 * chunk + i; };
+    auto param = [&](int t, int i) { return L.wide ? 2 * t + (i & 1) : t; };
+    return pack_record_word(
+        b, (int)(w3 & 255), L, nt, sc3, bs3,
+        [&](int t, int i) -> const float* {
+            const int jc = coord(i), p = param(t, i);
+            return (jc < L.n_up && p < np) ? a.w4 + ((int64_t)jc * L.P + pbase + p) * L.H : nullptr;
+        },
+        [&](int t, int i) -> float {
+            const int jc = coord(i), p = param(t, i);
+            return (jc < L.n_up && p < np) ? a.b4[(int64_t)jc * L.P + pbase + p] : 0.0f;
+        });
+}
+
+// header words: the unscale factors (words 0-2 hold the maxima), and the scales
+__device__ PackScales pack_header(const PackArgs& a, int64_t g) {
     const unsigned int* hdr = reinterpret_cast<const unsigned int*>(a.out);
     const int s1 = scale_exp(__uint_as_float(hdr[0])), s2 = scale_exp(__uint_as_float(hdr[1])),
               s3 = scale_exp(__uint_as_float(hdr[2]));
-    const float sc1 = ldexpf(1.0f, s1), sc2 = ldexpf(1.0f, s2), sc3 = ldexpf(1.0f, s3);
-    const float bs2 = ldexpf(1.0f, s2 + 14), bs3 = ldexpf(1.0f, s3 + 14);
     uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
-    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < L.total;
+    if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -s1));
+    if (g == 4) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
+    if (g == 5) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
+    if (g >= 6 && g < 256) out[g] = 0;
+    return PackScales{ldexpf(1.0f, s1), ldexpf(1.0f, s2), ldexpf(1.0f, s3), ldexpf(1.0f, s2 + 14),
+                      ldexpf(1.0f, s3 + 14)};
+}
+
+// One thread per packed 32-bit word (layout described in nfk_fused_impl.h).
+__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.L.total;
          g += (int64_t)gridDim.x * blockDim.x) {
-        if (g < L.o_h1) {  // header: the unscale factors (words 0-2 hold the maxima)
-            if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -s1));
-            if (g == 4) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
-            if (g == 5) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
-            if (g >= 6) out[g] = 0;
-            continue;
+        const PackScales ps = pack_header(a, g);
+        if (g >= a.L.o_h1) out[g] = pack_word(a, g, ps);
+    }
+}
+
+// Frame stream of the wide kernel (nfk_fused_wide.h): after the header, one
+// 65-block frame per forward sub-step: the sub-record's blocks, zero padding,
+// and at block 64 its record's bias block (every frame carries it; the kernel
+// reads it only for the first sub-record of a record).  Words come from the
+// record layout a.L (wide form) through pack_word.
+__global__ __launch_bounds__(256) void k_pack_frames(PackArgs a, int s1, int ns, int gh, int gc) {
+    const Layout& L = a.L;
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+    const int64_t total = 256 + (int64_t)ns * kWideSlotBlocks * 256;
+    const int s2 = L.KBH / gh, sc = L.KBH / gc;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const PackScales ps = pack_header(a, g);
+        if (g < 256) continue;
+        const int64_t w = g - 256;
+        const int f = (int)(w / (kWideSlotBlocks * 256)), fw = (int)(w - (int64_t)f * kWideSlotBlocks * 256);
+        const int blk = fw >> 8, wl = fw & 255;
+        int64_t rec;
+        int nt, j, nkb, gg;
+        if (f < s1) {
+            rec = L.o_h1, nt = L.HT, j = f, nkb = L.KB1, gg = gh;
+        } else if (f < s1 + s2) {
+            rec = L.o_h2, nt = L.HT, j = f - s1, nkb = L.KBH, gg = gh;
+        } else {
+            const int u = f - s1 - s2, ch = u / (3 * sc), v = u - ch * (3 * sc), part = v / sc;
+            j = v - part * sc;
+            rec = L.o_w3 + ((int64_t)ch * L.blk_chunk + part * L.blk_w) * 256;
+            nt = L.K / 2, nkb = L.KBH, gg = gc;
         }
-        const int kbh = L.KBH;
-        if (g < L.o_h2) {  // layer 1: KB1 f16 k-blocks over the n_lo inputs + unscaled bias
-            const int64_t w = g - L.o_h1;
-            const int blk = (int)(w >> 8), wl = (int)(w & 255);
-            if (blk < L.KB1 * L.HT * 2) {
-                const int part = blk & 1, idx = blk >> 1, kb = idx / L.HT, t = idx - kb * L.HT;
-                const int lane = wl >> 2, j = 2 * (wl & 3);
-                const int f = hid_feature(t, lane & 15, kbh), k0 = 32 * kb + 8 * (lane >> 4) + j;
-                float v0 = 0.0f, v1 = 0.0f;
-                if (f < L.H) {
-                    if (k0 < L.n_lo) v0 = a.w0[(int64_t)f * L.n_lo + k0] * sc1;
-                    if (k0 + 1 < L.n_lo) v1 = a.w0[(int64_t)f * L.n_lo + k0 + 1] * sc1;
-                }
-                out[g] = f16_part_pair(v0, v1, part);
-            } else {
-                const int t = wl >> 4, f = hid_feature(t, wl & 15, kbh);
-                out[g] = __float_as_uint((t < L.HT && f < L.H) ? a.b0[f] : 0.0f);
-            }
-            continue;
-        }
-        if (g < L.o_w3) {  // layer 2
-            const int64_t w = g - L.o_h2;
-            out[g] = pack_record_word(
-                (int)(w >> 8), (int)(w & 255), L, L.HT, sc2, bs2,
-                [&](int t, int i) -> const float* {
-                    const int f = hid_feature(t, i, kbh);
-                    return f < L.H ? a.w2 + (int64_t)f * L.H : nullptr;
-                },
-                [&](int t, int i) -> float {
-                    const int f = hid_feature(t, i, kbh);
-                    return f < L.H ? a.b2[f] : 0.0f;
-                });
-            continue;
-        }
-        // output layer: chunk, phase (W, H, D)
-        const int64_t w3 = g - L.o_w3;
-        const int64_t bl = w3 >> 8;
-        const int chunk = (int)(bl / L.blk_chunk);
-        int b = (int)(bl - (int64_t)chunk * L.blk_chunk);
-        int nt = L.K, pbase = 0;
-        if (b >= L.blk_w) {
-            b -= L.blk_w;
-            pbase = L.K;
-            if (b >= L.blk_w) {
-                b -= L.blk_w;
-                pbase = 2 * L.K;
-                nt = L.K - 1;
-            }
-        }
-        out[g] = pack_record_word(
-            b, (int)(w3 & 255), L, nt, sc3, bs3,
-            [&](int t, int i) -> const float* {
-                const int jc = 16 * chunk + i;
-                return jc < L.n_up ? a.w4 + ((int64_t)jc * L.P + pbase + t) * L.H : nullptr;
-            },
-            [&](int t, int i) -> float {
-                const int jc = 16 * chunk + i;
-                return jc < L.n_up ? a.b4[(int64_t)jc * L.P + pbase + t] : 0.0f;
-            });
+        const int kb0 = gg * j, nk = (nkb - kb0) < gg ? (nkb - kb0) : gg;
+        uint32_t v = 0;
+        if (blk == 64)
+            v = pack_word(a, rec + (int64_t)nkb * nt * 2 * 256 + wl, ps);
+        else if (blk < nk * nt * 2)
+            v = pack_word(a, rec + ((int64_t)kb0 * nt * 2 + blk) * 256 + wl, ps);
+        out[g] = v;
     }
 }
 
@@ -231,31 +289,105 @@ bool shape_ok(int n_lo, int n_up, int H, int K) {
     return kb && kk;
 }
 
+// Shapes of the wide kernel (nfk_fused_wide.h): H = 32 KBH for an instantiated
+// KBH, no f32 tail; layer-1 inputs within the KBH k-blocks; every lower
+// coordinate inside the x tiles (16 lower + 16 upper coordinates per chunk
+// pair); even K; LDS within the CU.
+bool wide_ok(int n_lo, int n_up, int H, int K) {
+    if (n_lo < 1 || n_up < 1 || H < 1 || K < 2 || (K & 1)) return false;
+    const Layout L = make_layout(n_lo, n_up, H, K, 1);
+    if (L.T1 != 0 || L.KB1 > L.KBH || n_lo > 16 * ((L.NCH + 1) / 2)) return false;
+    if (wide_lds_bytes(n_lo, n_up) > (size_t)kLdsBytes) return false;
+    bool kb = false, kk = false;
+#define CHK_KB(h) kb |= (L.KBH == h);
+    NFK_WIDE_KB(CHK_KB)
+#undef CHK_KB
+#define CHK_K(h, k) kk |= (K == k);
+    NFK_WIDE_K(CHK_K, 0)
+#undef CHK_K
+    return kb && kk;
+}
+
+// narrow kernel first (c3-class layers), the wide one for what it rejects
+bool pack_ok(int n_lo, int n_up, int H, int K) { return shape_ok(n_lo, n_up, H, K) || wide_ok(n_lo, n_up, H, K); }
+
+// the record layout of the kernel that will run this shape
+Layout pack_layout(int n_lo, int n_up, int H, int K) {
+    return make_layout(n_lo, n_up, H, K, shape_ok(n_lo, n_up, H, K) ? 0 : 1);
+}
+
+// floats of the pack: the record layout (narrow kernel) or header + frames (wide)
+int64_t pack_floats(int n_lo, int n_up, int H, int K) {
+    const Layout L = pack_layout(n_lo, n_up, H, K);
+    if (!L.wide) return L.total;
+    int s1;
+    const int ns = wide_substeps(L.KB1, L.KBH, K, L.NCH, &s1);
+    return 256 + (int64_t)ns * kWideSlotBlocks * 256;
+}
+
+int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_t st) {
+    WideArgs a;
+    a.x = f.x;
+    a.pack = f.pack;
+    a.up_in = f.up_in;
+    a.up_out = f.up_out;
+    a.lo_in = f.lo_in;
+    a.lo_out = f.lo_out;
+    a.z = f.z;
+    a.logdet = f.logdet;
+    a.status = f.status;
+    a.ldx = f.ldx;
+    a.ldz = f.ldz;
+    a.batch = f.batch;
+    a.n_lo = L.n_lo;
+    a.n_up = L.n_up;
+    a.KB1 = L.KB1;
+    a.NCH = L.NCH;
+    a.mode = f.mode;
+    a.NS = wide_substeps(L.KB1, L.KBH, K, L.NCH, &a.S1);
+    a.c = f.c;
+    const size_t lds = wide_lds_bytes(L.n_lo, L.n_up);
+#define DISPATCH(h, k) \
+    if (L.KBH == h && K == k) return launch_fused_wide<h, k>(a, lds, inv, st);
+#define DISPATCH_KB(h) NFK_WIDE_K(DISPATCH, h)
+    NFK_WIDE_KB(DISPATCH_KB)
+#undef DISPATCH_KB
+#undef DISPATCH
+    return nfk_set_error("nfk_fused_nsf: no wide kernel instance");
+}
+
 }  // namespace
 
 extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
-    return shape_ok(n_lo, n_up, hidden, K) ? 1 : 0;
+    return pack_ok(n_lo, n_up, hidden, K) ? 1 : 0;
 }
 
 extern "C" int64_t nfk_fused_nsf_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
-    if (!shape_ok(n_lo, n_up, hidden, K)) return 0;
-    return make_layout(n_lo, n_up, hidden, K).total;
+    if (!pack_ok(n_lo, n_up, hidden, K)) return 0;
+    return pack_floats(n_lo, n_up, hidden, K);
 }
 
 extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float* w2, const float* b2,
                                   const float* w4, const float* b4, int32_t n_lo, int32_t n_up,
                                   int32_t hidden, int32_t K, float* wpack, nfk_stream_t stream) {
-    if (!shape_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_pack: shape not supported");
+    if (!pack_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_pack: shape not supported");
     if (!w0 || !b0 || !w2 || !b2 || !w4 || !b4 || !wpack)
         return nfk_set_error("nfk_fused_nsf_pack: null pointer");
-    PackArgs a{w0, b0, w2, b2, w4, b4, wpack, make_layout(n_lo, n_up, hidden, K)};
+    PackArgs a{w0, b0, w2, b2, w4, b4, wpack, pack_layout(n_lo, n_up, hidden, K)};
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(wpack, 0, 3 * sizeof(float), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_pack_max, dim3(64), dim3(256), 0, st, a);
-    int64_t g = (a.L.total + 255) / 256;
+    int64_t g = (pack_floats(n_lo, n_up, hidden, K) + 255) / 256;
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, st, a);
+    if (a.L.wide) {
+        int s1;
+        const int ns = wide_substeps(a.L.KB1, a.L.KBH, K, a.L.NCH, &s1);
+        hipLaunchKernelGGL(k_pack_frames, dim3((unsigned)g), dim3(256), 0, st, a, s1, ns,
+                           wide_g(a.L.HT, a.L.KBH), wide_g(K / 2, a.L.KBH));
+    } else {
+        hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, st, a);
+    }
     e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -266,13 +398,14 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
                              int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
                              int32_t K, double tail_bound, int32_t inverse, int32_t* status,
                              nfk_stream_t stream) {
-    if (!shape_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
+    const bool narrow = shape_ok(n_lo, n_up, hidden, K);
+    if (!narrow && !wide_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
     if (batch < 0) return nfk_set_error("nfk_fused_nsf: bad batch");
     if (batch == 0) return 0;
     if (!x || !wpack || !up_in || !up_out || !lo_in || !lo_out || !z)
         return nfk_set_error("nfk_fused_nsf: null pointer");
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf: null logdet");
-    const Layout L = make_layout(n_lo, n_up, hidden, K);
+    const Layout L = pack_layout(n_lo, n_up, hidden, K);
     FusedArgs a;
     a.x = x;
     a.pack = wpack;
@@ -318,9 +451,10 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
         a.c.min_d = sc.min_d;
         a.c.d_edge = sc.d_edge;
     }
-    const size_t lds = lds_bytes(L);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
+    if (!narrow) return launch_wide(a, L, K, inv, st);
+    const size_t lds = lds_bytes(L);
 #define DISPATCH(h, t, k) \
     if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, st);
 #define DISPATCH_KB(h, t) NFK_FUSED_K(DISPATCH, h, t)

@@ -49,8 +49,13 @@ constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 
 // (k = 32kb + 8(l>>4) + j) -- activations never leave registers.  With a
 // tail, tile 2 KBH holds feature 32 KBH + q in register 0 of lane group q:
 // exactly the B operand (k = l>>4) of the f32 tail step.
+// wide = 1 (nfk_fused_wide.h): the output layer in 8-coordinate chunks whose
+//   W/H/D records have ceil(K/2) tiles; row i of tile t = parameter
+//   2t + (i&1) of coordinate 8c + 2(i>>2) + ((i>>1)&1), so lane group q holds
+//   two coordinates with all their parameters in registers 2h, 2h+1 of the
+//   tiles (half the accumulators of the 16-coordinate form).
 struct Layout {
-    int n_lo, n_up, H, K, P, KBH, T1, HT, KB1, NCH;
+    int n_lo, n_up, H, K, P, KBH, T1, HT, KB1, NCH, wide, CW;
     int blk_h1, blk_h2, blk_w, blk_d, blk_chunk, slot_blocks;
     int64_t o_h1, o_h2, o_w3, total;  // offsets / size in floats
 };
@@ -58,8 +63,10 @@ struct Layout {
 // blocks of an f16-split record with nt tiles (+ f32 tail groups, + bias)
 inline int rec_blocks(int kbh, int t1, int nt) { return kbh * nt * 2 + (t1 ? (nt + 3) / 4 : 0) + 1; }
 
-inline Layout make_layout(int n_lo, int n_up, int H, int K) {
+inline Layout make_layout(int n_lo, int n_up, int H, int K, int wide = 0) {
     Layout L;
+    L.wide = wide;
+    L.CW = wide ? 8 : 16;
     L.n_lo = n_lo;
     L.n_up = n_up;
     L.H = H;
@@ -78,11 +85,11 @@ inline Layout make_layout(int n_lo, int n_up, int H, int K) {
     }
     L.HT = 2 * L.KBH + L.T1;
     L.KB1 = (n_lo + 31) / 32;
-    L.NCH = (n_up + 15) / 16;
+    L.NCH = (n_up + L.CW - 1) / L.CW;
     L.blk_h1 = L.KB1 * L.HT * 2 + 1;
     L.blk_h2 = rec_blocks(L.KBH, L.T1, L.HT);
-    L.blk_w = rec_blocks(L.KBH, L.T1, K);
-    L.blk_d = rec_blocks(L.KBH, L.T1, K - 1);
+    L.blk_w = rec_blocks(L.KBH, L.T1, wide ? (K + 1) / 2 : K);
+    L.blk_d = rec_blocks(L.KBH, L.T1, wide ? K / 2 : K - 1);
     L.blk_chunk = 2 * L.blk_w + L.blk_d;
     L.slot_blocks = L.blk_h1;
     if (L.blk_h2 > L.slot_blocks) L.slot_blocks = L.blk_h2;
@@ -369,6 +376,9 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
         const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, c.lo);
         ek[r] = e;
         sk[r] = e1 - e;
+        // wide layers (K = 16): one coordinate at a time, or the scheduler
+        // interleaves the four and runs out of registers
+        if constexpr (K > 8) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
