@@ -325,8 +325,11 @@ int64_t pack_floats(int n_lo, int n_up, int H, int K) {
     return 256 + (int64_t)ns * kWideSlotBlocks * 256;
 }
 
+uint32_t* g_trace = nullptr;  // diagnostic timeline buffer (NFK_TRACE builds)
+
 int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_t st) {
     WideArgs a;
+    a.trace = g_trace;
     a.x = f.x;
     a.pack = f.pack;
     a.up_in = f.up_in;
@@ -357,6 +360,12 @@ int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_
 }
 
 }  // namespace
+
+// Diagnostic: timeline buffer for -DNFK_TRACE builds (not part of include/nfk.h).
+extern "C" int nfk_debug_trace(void* buf) {
+    g_trace = static_cast<uint32_t*>(buf);
+    return 0;
+}
 
 extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
     return pack_ok(n_lo, n_up, hidden, K) ? 1 : 0;

@@ -54,6 +54,42 @@ constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 
 //   2t + (i&1) of coordinate 8c + 2(i>>2) + ((i>>1)&1), so lane group q holds
 //   two coordinates with all their parameters in registers 2h, 2h+1 of the
 //   tiles (half the accumulators of the 16-coordinate form).
+// Diagnostic timeline (-DNFK_TRACE builds only, tools/trace_wide.py): each
+// wave records s_memtime at marked points into lanes of 4 VGPRs (256 marks);
+// every 512th workgroup writes them to a buffer set by nfk_debug_trace().
+struct NfkTrace {
+    uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+    int n = 0;
+};
+#ifdef NFK_TRACE
+__device__ __forceinline__ void nfk_mark(NfkTrace& t) {
+    const uint32_t c = (uint32_t)__builtin_readcyclecounter();
+    const int i = t.n & 255;
+    const bool me = (int)(threadIdx.x & 63) == (i & 63);
+    if (i < 64)
+        t.v0 = me ? c : t.v0;
+    else if (i < 128)
+        t.v1 = me ? c : t.v1;
+    else if (i < 192)
+        t.v2 = me ? c : t.v2;
+    else
+        t.v3 = me ? c : t.v3;
+    ++t.n;
+}
+__device__ __forceinline__ void nfk_trace_flush(const NfkTrace& t, uint32_t* buf, int wid, int lane) {
+    if (buf == nullptr || (blockIdx.x & 511) != 0) return;
+    uint32_t* o = buf + ((size_t)(blockIdx.x >> 9) * 16 + wid) * 260;
+    o[lane] = t.v0;
+    o[64 + lane] = t.v1;
+    o[128 + lane] = t.v2;
+    o[192 + lane] = t.v3;
+    if (lane == 0) o[256] = (uint32_t)t.n;
+}
+#define NFK_MARK(t) nfk_mark(t)
+#else
+#define NFK_MARK(t) ((void)0)
+#endif
+
 struct Layout {
     int n_lo, n_up, H, K, P, KBH, T1, HT, KB1, NCH, wide, CW;
     int blk_h1, blk_h2, blk_w, blk_d, blk_chunk, slot_blocks;

@@ -56,6 +56,7 @@ struct WideArgs {
     int32_t n_lo, n_up, KB1, NCH, mode;
     int32_t S1, NS;  // layer-1 sub-steps, sub-steps per layer
     FusedConst c;
+    uint32_t* trace;  // diagnostic timeline buffer (NFK_TRACE builds), else unused
 };
 
 inline size_t wide_lds_bytes(int n_lo, int n_up) {
@@ -84,6 +85,12 @@ __device__ __forceinline__ void wide_stage(const WideArgs& a, int s, float4* slo
         const int v = (s - a.S1 - S2) % (3 * SC);
         if (v < 2 * SC) f = v < SC ? s + SC : s - SC;
     }
+#ifdef NFK_WABL_L2HOT
+    f &= 1;  // diagnostic: two frames only (every weight read hits L2)
+#endif
+#ifdef NFK_WABL_NOSTAGE
+    if (s >= 2) return;  // diagnostic: no copies after the prologue
+#endif
     float4* slot = (s & 1) ? slot1 : slot0;
     stage_record(a.pack + 256 + (int64_t)f * (kWideSlotBlocks * 256), kWideSlotBlocks, slot, wid, lane);
 }
@@ -151,16 +158,18 @@ __device__ __forceinline__ void gemm_sub(const h8 (&bh)[KBH], const h8 (&bl)[KBH
 template <int KBH, int K, bool INV, int NT>
 __device__ __forceinline__ void wide_phase(const WideArgs& a, int& s, int nsub, int nkb, const h8 (&bh)[KBH],
                                            const h8 (&bl)[KBH], f32x4 (&acc)[NT], float bscale, float4* slot0,
-                                           float4* slot1, int wid, int lane) {
+                                           float4* slot1, int wid, int lane, NfkTrace& tr) {
     constexpr int NS = KBH / wide_g(NT, KBH);
     static_assert(NS <= 4, "at most 4 sub-records per phase");
     auto one = [&](auto Jc) {
         constexpr int J = decltype(Jc)::value;
         if (J < nsub) {
             gemm_sub<KBH, NT, J>(bh, bl, (s & 1) ? slot1 : slot0, lane, acc, nkb, bscale);
+            NFK_MARK(tr);  // GEMM issued
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+            NFK_MARK(tr);  // barrier passed
             wide_stage<KBH, K, INV>(a, s + 2, slot0, slot1, wid, lane);
             ++s;
         }
@@ -176,6 +185,18 @@ __device__ __forceinline__ void wide_phase(const WideArgs& a, int& s, int nsub, 
 template <int K, bool SEARCH>
 __device__ __forceinline__ void knot_phase_w(const f32x4 (&acc)[K / 2], const float (&xv)[2], const FusedConst& c,
                                              float l2e, int (&kb)[2], float (&ek)[2], float (&sk)[2]) {
+#ifdef NFK_WABL_NOEPI
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        float v = 0.0f;
+#pragma unroll
+        for (int p = 0; p < K; ++p) v += acc[p >> 1][2 * h + (p & 1)];
+        if (SEARCH) kb[h] = 0;
+        ek[h] = v;
+        sk[h] = xv[h];
+    }
+    return;
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         float u[K];
@@ -269,6 +290,8 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
     const bool row_ok = sl < nrows;
     const FusedConst& c = a.c;
     const float* pk = a.pack;
+    NfkTrace tr;
+    NFK_MARK(tr);  // start
 
     // ---- prologue: index maps (plain loads, no copy in flight yet)
     for (int i = threadIdx.x; i < a.n_up; i += 64 * kWaves) {
@@ -321,14 +344,15 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
             }
     }
     dma_barrier();  // sub-records 0, 1 and the first x tile landed
+    NFK_MARK(tr);  // prologue done
 
     // ---- layer 1 (S1 sub-steps) and layer 2 (S2 sub-steps)
     float btail;
     {
         f32x4 h[HT];
-        wide_phase<KBH, K, INV, HT>(a, s, a.S1, a.KB1, bh, bl, h, bsc, slot0, slot1, wid, lane);
+        wide_phase<KBH, K, INV, HT>(a, s, a.S1, a.KB1, bh, bl, h, bsc, slot0, slot1, wid, lane, tr);
         act_operands<KBH, false, HT>(h, -2.0f * kL2E * unx, bh, bl, btail);
-        wide_phase<KBH, K, INV, HT>(a, s, S2, KBH, bh, bl, h, 1.0f, slot0, slot1, wid, lane);
+        wide_phase<KBH, K, INV, HT>(a, s, S2, KBH, bh, bl, h, 1.0f, slot0, slot1, wid, lane, tr);
         act_operands<KBH, false, HT>(h, -2.0f * kL2E * un2, bh, bl, btail);
     }
 
@@ -347,7 +371,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
         // ---- searched knots (widths forward / heights inverse)
         {
             f32x4 acc[NTC];
-            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, acc, 1.0f, slot0, slot1, wid, lane);
+            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, acc, 1.0f, slot0, slot1, wid, lane, tr);
             const float4 u = *reinterpret_cast<const float4*>(tile + sl * 32 + tcol - 1);
             xv[0] = u.y;
             xv[1] = u.w;
@@ -357,18 +381,32 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
                 if (jj[h] >= a.n_up) xv[h] = 0.0f;
             }
             knot_phase_w<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k);
+            NFK_MARK(tr);  // epilogue A
         }
         // ---- the other knots, selected at the bin
         {
             f32x4 acc[NTC];
-            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, acc, 1.0f, slot0, slot1, wid, lane);
+            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, acc, 1.0f, slot0, slot1, wid, lane, tr);
             knot_phase_w<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k);
+            NFK_MARK(tr);  // epilogue B
         }
         // ---- derivatives of the bin, evaluate, log|det|
         {
             f32x4 accd[NTC];
-            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, accd, 1.0f, slot0, slot1, wid, lane);
+            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, accd, 1.0f, slot0, slot1, wid, lane, tr);
             float outv[2];
+#ifdef NFK_WABL_NOEPI
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float v = cw_k[h] + w_k[h] + ch_k[h] + h_k[h];
+#pragma unroll
+                for (int t = 0; t < NTC; ++t) v += accd[t][2 * h] + accd[t][2 * h + 1];
+                outv[h] = v;
+                ldsum += v;
+                any_in = true;
+            }
+            if (false)
+#endif
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 // derivative logit j in register 2h + (j & 1) of tile j >> 1;
@@ -423,6 +461,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
             float* tw = tile + sl * 32 + tcol;
             tw[0] = outv[0];  // z back into the upper columns
             tw[2] = outv[1];
+            NFK_MARK(tr);  // epilogue C
         }
         // after a chunk pair: its z, then the next pair's x into the same tile
         // (the stores' data left the tile before the copy is issued)
@@ -452,6 +491,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
                 atomicOr(a.status, bits);
         }
     }
+#ifdef NFK_TRACE
+    NFK_MARK(tr);  // end
+    nfk_trace_flush(tr, a.trace, wid, lane);
+#endif
 }
 
 template <int KBH, int K>
