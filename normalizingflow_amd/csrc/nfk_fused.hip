@@ -416,6 +416,7 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf: null logdet");
     const Layout L = pack_layout(n_lo, n_up, hidden, K);
     FusedArgs a;
+    a.trace = g_trace;
     a.x = x;
     a.pack = wpack;
     a.up_in = up_in;

@@ -7,19 +7,25 @@
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
 
+int nfk_set_error(const char* msg);  // nfk_kernels.hip
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 #ifndef NFK_WAVES
 #define NFK_WAVES 8
 #endif
-#ifndef NFK_PINGPONG
-#define NFK_PINGPONG 0  // 1: waves 4-7 trail waves 0-3 by half a phase (see k_fused_nsf)
+#ifndef NFK_NSF_WAVES
+#define NFK_NSF_WAVES 4  // waves per workgroup of k_fused_nsf (one per SIMD)
+#endif
+#ifndef NFK_LDS_PAD
+#define NFK_LDS_PAD 0  // diagnostic: extra LDS per k_fused_nsf workgroup (fewer per CU)
 #endif
 
 namespace nfk_fused {
 
 constexpr int kWaves = NFK_WAVES;  // waves per workgroup (two per SIMD by default), 16 samples each
+constexpr int kNsfWaves = NFK_NSF_WAVES;
 constexpr int kMaxD = 128;
 constexpr int kLdsBytes = 160 * 1024;
 constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 2^14 <= 2^14)
@@ -66,6 +72,7 @@ __device__ __forceinline__ void nfk_mark(NfkTrace& t) {
     const uint32_t c = (uint32_t)__builtin_readcyclecounter();
     const int i = t.n & 255;
     const bool me = (int)(threadIdx.x & 63) == (i & 63);
+    if (t.n > 255) return;  // first 256 marks only (persistent kernels: the first tiles)
     if (i < 64)
         t.v0 = me ? c : t.v0;
     else if (i < 128)
@@ -146,11 +153,14 @@ inline int x_lo_row(const Layout& L) { return 32 * L.KB1; }
 inline int x_up_row(const Layout& L) { return (L.n_up + 3) & ~3; }
 inline int x_tile_floats(const Layout& L) { return 16 * (x_lo_row(L) + x_up_row(L)); }
 
-// dynamic LDS bytes: two record slots, the index maps, the x tiles of every wave
+// dynamic LDS bytes of k_fused_nsf: the record slot, the index maps, the x
+// tiles of every wave
 inline size_t lds_bytes(const Layout& L) {
     const int D = L.n_lo + L.n_up;
     const size_t maps = (size_t)((2 * D + 3) / 4) * 16;
-    return 2 * (size_t)L.slot_blocks * 1024 + maps + (size_t)kWaves * x_tile_floats(L) * sizeof(float);
+    return (size_t)L.slot_blocks * 1024 + maps + (size_t)kNsfWaves * x_tile_floats(L) * sizeof(float) +
+           (size_t)kNsfWaves * (L.K + 1) * 64 * sizeof(int) +  // bin lookup tables
+           NFK_LDS_PAD;
 }
 
 // hidden feature computed by row i (0..15) of hidden tile t (>= H: padding)
@@ -183,6 +193,7 @@ struct FusedArgs {
     int32_t blk_h1, blk_h2, blk_w, blk_d, blk_chunk;
     int32_t o_h1, o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
     FusedConst c;
+    uint32_t* trace;  // diagnostic timeline buffer (NFK_TRACE builds), else unused
 };
 
 __device__ __forceinline__ f32x4 mfma32(float a, float b, f32x4 c) {
@@ -243,13 +254,35 @@ __device__ __forceinline__ void dma_barrier() {
 }
 
 // Copy one phase record (nblk 1-KiB blocks at src) into an LDS slot: block i
-// goes by wave i % kWaves as one global_load_lds_dwordx4 (LDS destination =
+// goes by wave i % NW as one global_load_lds_dwordx4 (LDS destination =
 // wave-uniform base + 16 B x lane).
+template <int NW = kWaves>
 __device__ __forceinline__ void stage_record(const float* __restrict__ src, int nblk, float4* slot,
                                              int wid, int lane) {
     const uint32_t base = lds_addr(slot);
-    for (int i = wid; i < nblk; i += kWaves) dma16(src + (int64_t)i * 256 + lane * 4, base + i * 1024);
+    for (int i = wid; i < nblk; i += NW) dma16(src + (int64_t)i * 256 + lane * 4, base + i * 1024);
 }
+
+// Walk the elements e = lane, lane + 64, ... of a [rows][row] tile as
+// (r, k) = (e / row, e % row) with one division up front (the loops below ran
+// a VALU integer division per element).
+struct RowWalk {
+    int r, k, dr, dk, row;
+    __device__ __forceinline__ RowWalk(int lane, int row_) : row(row_) {
+        r = lane / row;
+        k = lane - r * row;
+        dr = 64 / row;
+        dk = 64 - dr * row;
+    }
+    __device__ __forceinline__ void next() {
+        k += dk;
+        r += dr;
+        if (k >= row) {
+            k -= row;
+            ++r;
+        }
+    }
+};
 
 // Gather a [16][row] tile of x (rows b0.., columns map[0..n)) into this wave's
 // LDS tile: element e = 64 i + lane of instruction i is (e / row, e % row).
@@ -258,10 +291,10 @@ __device__ __forceinline__ void stage_record(const float* __restrict__ src, int 
 __device__ __forceinline__ void gather_x(const float* __restrict__ x, int64_t ldx, int64_t b0, int nrows,
                                          const int32_t* map, int n, int row, float* tile, int lane) {
     const uint32_t base = lds_addr(tile);
-    for (int i = 0; i < row / 4; ++i) {
-        const int e = 64 * i + lane, r = e / row, k = e - r * row;
-        const int64_t rr = b0 + (r < nrows ? r : 0);
-        dma4(x + rr * ldx + map[k < n ? k : 0], base + i * 256);
+    RowWalk w(lane, row);
+    for (int i = 0; i < row / 4; ++i, w.next()) {
+        const int64_t rr = b0 + (w.r < nrows ? w.r : 0);
+        dma4(x + rr * ldx + map[w.k < n ? w.k : 0], base + i * 256);
     }
 }
 
@@ -374,10 +407,16 @@ __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[
 // the bin of utils.py:20-25 for every x inside the tails (edges are strictly
 // increasing; elements within an ulp of an edge may take the neighbouring
 // bin, where the C1 spline agrees); the other phase selects by k.
+// NFK_LUT (default): the two prefixes at the bin are read back from a per-wave
+// LDS table (row j = prefix j of every lane, one ds_read2st64 at row k)
+// instead of 2 (K-1) selects on compare masks.
+#ifndef NFK_LUT
+#define NFK_LUT 1
+#endif
 template <int K, bool SEARCH>
 __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
                                            const FusedConst& c, float l2e, int (&kb)[4],
-                                           float (&ek)[4], float (&sk)[4]) {
+                                           float (&ek)[4], float (&sk)[4], int* scr, int lane) {
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -397,17 +436,29 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
 #pragma unroll
         for (int t = 0; t < K; ++t) u[t] = acc[t][r];
         nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
-        int p0 = 0, p1 = pre[1 < K ? 1 : 0], k = 0;
-        const int xi = __float2int_rd(__builtin_fmaf(xv[r], c.inv30, -c.lo * c.inv30));
+        int p0 = 0, p1 = pre[1 < K ? 1 : 0];
+        if (SEARCH) {
+            const int xi = __float2int_rd(__builtin_fmaf(xv[r], c.inv30, -c.lo * c.inv30));
+            int k = 0;
 #pragma unroll
-        for (int j = 1; j < K; ++j) {
-            const bool ge = SEARCH ? (xi >= pre[j]) : (kb[r] >= j);
-            p0 = ge ? pre[j] : p0;
-            if (j + 1 < K) p1 = ge ? pre[j + 1] : p1;
-            if (SEARCH) k += ge ? 1 : 0;
+            for (int j = 1; j < K; ++j) k += (xi >= pre[j]) ? 1 : 0;
+            kb[r] = k;
         }
-        if (SEARCH) kb[r] = k;
         const int kk = kb[r];
+        if (NFK_LUT) {
+            // rows 0..K-1 (row K is read, unused, when kk = K - 1)
+#pragma unroll
+            for (int j = 0; j < K; ++j) scr[j * 64 + lane] = pre[j];
+            p0 = scr[kk * 64 + lane];
+            p1 = scr[(kk + 1) * 64 + lane];
+        } else {
+#pragma unroll
+            for (int j = 1; j < K; ++j) {
+                const bool ge = kk >= j;
+                p0 = ge ? pre[j] : p0;
+                if (j + 1 < K) p1 = ge ? pre[j + 1] : p1;
+            }
+        }
         const float e = __builtin_fmaf(c.sp30, (float)p0, c.lo);
         const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, c.lo);
         ek[r] = e;
@@ -425,38 +476,31 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
 #ifdef NFK_ABL_NOSTAGE
 #define NFK_STAGE(...) ((void)0)
 #else
-#define NFK_STAGE(...) stage_record(__VA_ARGS__)
+#define NFK_STAGE(...) stage_record<kNsfWaves>(__VA_ARGS__)
 #endif
 
-// One workgroup = kWaves waves x 16 samples.  A layer is a sequence of NP =
-// 2 + 3 NCH phases (layer 1, layer 2, then per 16-coordinate chunk: searched
-// knots, other knots, derivatives); each phase is a GEMM half (MFMA from an
-// LDS record slot) and an epilogue half (VALU on the accumulators).
-//
-// Half-steps: the GEMM half of phase p is half-step 2p, its epilogue 2p+1.
-// Phase p's record sits in slot p&1; phase p+2's record is copied into that
-// slot at the start of half-step 2p+2 and waited for (vmcnt(0)) at the
-// barrier ending half-step 2p+3.  The loop issues no other global memory
-// operation: x is staged in the prologue and z is collected in LDS.
-// Default (lockstep): all 8 waves run the same half-step; only the end of an
-// epilogue half is a barrier.
-// NFK_PINGPONG=1: waves w and w+4 share a SIMD (tools/simd_map.hip), and a
-// partner's VALU can overlap fp16 MFMAs that alternate accumulators
-// (tools/ubench_coexec2.hip), so waves 4..7 trail waves 0..3 by one half-step
-// (one in its GEMM half while its partner is in its epilogue half) with a
-// barrier after every half-step.  Measured: 13 % slower than lockstep on c3
-// (co-execution stays < 10 % of MFMA cycles and barrier waits double), so it
-// is off.
-// Copy the record of phase p into its slot (p & 1).  Phases: 0 = layer 1,
-// 1 = layer 2, 2 + 3c + {0, 1, 2} = chunk c's searched knots, other knots,
-// derivatives (offA/offB/offC: block offsets of those records in the chunk).
-__device__ __forceinline__ void stage_phase(const FusedArgs& a, int p, int offA, int offB, int offC,
-                                            float4* slot0, float4* slot1, int wid, int lane) {
-    float4* slot = (p & 1) ? slot1 : slot0;
+// One workgroup = kNsfWaves (4) waves, one per SIMD, x 16 samples each; two
+// workgroups share a CU (c3: one 51-KiB record slot + 16 KiB of x tiles), so
+// one's epilogue VALU can run beside the other's MFMAs, and its barrier
+// waits, prologue copies and z stores are covered by the other.
+// A layer is a sequence of NP = 2 + 3 NCH phases (layer 1, layer 2, then per
+// 16-coordinate chunk: searched knots, other knots, derivatives); each phase
+// is a GEMM half (MFMA from the record slot) and an epilogue half (VALU on the
+// accumulators).  Half-steps: GEMM of phase p = half-step 2p, its epilogue
+// 2p+1, each ended by a workgroup barrier.  After the barrier ending GEMM p
+// every wave's reads of the slot have returned, so phase p+1's record is
+// copied into the slot; the copy overlaps epilogue p and is waited for
+// (vmcnt(0)) at the barrier ending it.  The loop issues no other global
+// memory operation: x is staged in the prologue and z is collected in LDS.
+// Measured alternatives: two slots with one 8-wave
+// workgroup per CU, lockstep or ping-pong (4-6 % slower); a persistent form
+// prefetching the next tile's x into registers (no faster, SGPR spills).
+__device__ __forceinline__ void stage_phase(const FusedArgs& a, int p, int offA, int offB, int offC, float4* slot,
+                                            int wid, int lane) {
     if (p == 0) {
-        stage_record(a.pack + a.o_h1, a.blk_h1, slot, wid, lane);
+        stage_record<kNsfWaves>(a.pack + a.o_h1, a.blk_h1, slot, wid, lane);
     } else if (p == 1) {
-        stage_record(a.pack + a.o_h2, a.blk_h2, slot, wid, lane);
+        stage_record<kNsfWaves>(a.pack + a.o_h2, a.blk_h2, slot, wid, lane);
     } else {
         const int ch = (p - 2) / 3, part = (p - 2) - 3 * ch;
         const float* wc = a.pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
@@ -465,80 +509,86 @@ __device__ __forceinline__ void stage_phase(const FusedArgs& a, int p, int offA,
     }
 }
 
-// End of half-step hs: retire this wave's LDS work (and, at odd half-steps,
-// its record copies), workgroup barrier, then issue the copy that the next
-// half-step owns (phase hs/2 + 1 at even hs >= 2).
+// End of half-step hs: retire this wave's LDS reads (and after an epilogue
+// its copies), barrier; after a GEMM half issue the next record's copy.
 __device__ __forceinline__ void half_step(int& hs, int np, const FusedArgs& a, int offA, int offB, int offC,
-                                          float4* slot0, float4* slot1, int wid, int lane) {
-    // in lockstep mode only the end of an epilogue half (odd hs) is a barrier
-    if (NFK_PINGPONG || (hs & 1)) {
-        if (hs & 1)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        else
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifndef NFK_ABL_NOBAR
-        __builtin_amdgcn_s_barrier();
-#endif
-        asm volatile("" ::: "memory");
-    }
+                                          float4* slot, int wid, int lane, NfkTrace& tr) {
+    NFK_MARK(tr);  // half-step's work issued
+    if (hs & 1)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    NFK_MARK(tr);  // barrier passed
+    if (!(hs & 1) && hs / 2 + 1 < np) stage_phase(a, hs / 2 + 1, offA, offB, offC, slot, wid, lane);
     ++hs;
-    if (!(hs & 1) && hs >= 2 && hs / 2 + 1 < np) stage_phase(a, hs / 2 + 1, offA, offB, offC, slot0, slot1, wid, lane);
 }
 
+#ifndef NFK_NSF_WPE
+#define NFK_NSF_WPE 2  // waves per SIMD the register budget is sized for
+#endif
+
 template <int KBH, bool T1, int K, bool INV>
-__global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
+__global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(FusedArgs a) {
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int grp = (NFK_PINGPONG && wid >= kWaves / 2) ? 1 : 0;
     const int q = lane >> 4, sl = lane & 15;
     const int D = a.n_lo + a.n_up;
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
-    float4* slot0 = lds4;
-    float4* slot1 = lds4 + a.slot_blocks * 64;
-    int32_t* m_up_in = reinterpret_cast<int32_t*>(lds4 + 2 * a.slot_blocks * 64);
+    float4* slot = lds4;
+    int32_t* m_up_in = reinterpret_cast<int32_t*>(lds4 + a.slot_blocks * 64);
     int32_t* m_up_out = m_up_in + a.n_up;
     int32_t* m_lo_in = m_up_out + a.n_up;
     int32_t* m_lo_out = m_lo_in + a.n_lo;
     const int XL = 32 * a.KB1;  // lower-x tile row length (n_lo padded to the k-blocks)
     const int XU = a.xup;       // upper-x tile row length (n_up padded to 4)
-    float* xlo = reinterpret_cast<float*>(lds4 + 2 * a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xtile;
+    float* xlo = reinterpret_cast<float*>(lds4 + a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xtile;
     float* xup = xlo + 16 * XL;
-    const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
-    const int64_t rem = a.batch - b0;
-    const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
+    // this wave's bin lookup table: K + 1 rows of 64 lanes, after all x tiles
+    int* scr = reinterpret_cast<int*>(xlo + (kNsfWaves - wid) * a.xtile) + wid * (K + 1) * 64;
     const FusedConst& c = a.c;
     const float* pk = a.pack;
-    const bool row_ok = sl < nrows;
     const int NP = 2 + 3 * a.NCH;
     // execution order of the three records of a chunk: searched knots, other knots, derivatives
     const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
+    const int64_t b0 = ((int64_t)blockIdx.x * kNsfWaves + wid) * 16;
+    const int64_t rem = a.batch - b0;
+    const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
+    const bool row_ok = sl < nrows;
+    int hs = 0;  // half-step
+#define NFK_HALF_STEP() half_step(hs, NP, a, offA, offB, offC, slot, wid, lane, tr)
 
-    int hs = 0;  // global index of the half-step this wave is in
-#define NFK_HALF_STEP() half_step(hs, NP, a, offA, offB, offC, slot0, slot1, wid, lane)
+    NfkTrace tr;
+    NFK_MARK(tr);  // start
 
-    // ---- prologue: index maps (plain loads, before any DMA is in flight),
-    // first two records and both x tiles
-    for (int i = threadIdx.x; i < a.n_up; i += 64 * kWaves) {
+    // ---- prologue: index maps, pack scale factors, the log|det| being
+    // accumulated and the status word (plain loads, before any DMA is in
+    // flight, so the end of the kernel does not wait on them), then the
+    // layer-1 record and both x tiles by LDS-DMA
+    for (int i = threadIdx.x; i < a.n_up; i += 64 * kNsfWaves) {
         m_up_in[i] = a.up_in[i];
         m_up_out[i] = a.up_out[i];
     }
-    for (int i = threadIdx.x; i < a.n_lo; i += 64 * kWaves) {
+    for (int i = threadIdx.x; i < a.n_lo; i += 64 * kNsfWaves) {
         m_lo_in[i] = a.lo_in[i];
         m_lo_out[i] = a.lo_out[i];
     }
-    // factors undoing the fp16 pre-scaling (pack header)
     const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
+    const int st_prev = (a.status != nullptr && lane == 0) ? a.status[0] : 0;
+    const float ld_prev = (q == 0 && row_ok && a.mode == 2) ? a.logdet[b0 + sl] : 0.0f;
     __syncthreads();  // maps visible (no DMA in flight yet)
-    stage_phase(a, 0, offA, offB, offC, slot0, slot1, wid, lane);
+    stage_phase(a, 0, offA, offB, offC, slot, wid, lane);
     if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xlo, lane);
-    stage_phase(a, 1, offA, offB, offC, slot0, slot1, wid, lane);
     if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xup, lane);
-    dma_barrier();  // layer-1 record and the x tiles landed (layer-2 record: by half-step 1's end)
-    if (grp == 1) NFK_HALF_STEP();  // group 1 trails by one half-step
+    dma_barrier();
+    NFK_MARK(tr);  // prologue done
 
-    // ---- phase 0 (slot 0): layer 1, fp16 split.  x has any magnitude, so each
+    bool any_in = false, any_nd = false;
+
+    // ---- phase 0: layer 1, fp16 split.  x has any magnitude, so each
     // wave scales its tile by a power of two 2^sx that puts max|x| just under
     // 2^14 before the split; acc = 2^(s1+sx) W1 x.
     f32x4 h1[HT];
@@ -560,7 +610,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         // accumulators start at b1 2^(s1+sx) (exact power-of-two scaling), so the
         // epilogue only multiplies by 2^-(s1+sx): the bias is read in this GEMM
         // half, before the slot is recycled
-        const float4* s = slot0;
+        const float4* s = slot;
         const float4* bias = s + a.KB1 * HT * 2 * 64;
         const float bsc = ldexpf(1.0f, 14 - ex) / un1;
 #pragma unroll
@@ -595,11 +645,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
     float btail;
     act_operands<KBH, T1, HT>(h1, -2.0f * kL2E * unx, bh, bl, btail);
     NFK_HALF_STEP();
-
-    // ---- phase 1 (slot 1): layer 2, fp16 split: h2^T = tanh(W2 . h1^T + b2)
+    // ---- phase 1: layer 2, fp16 split: h2^T = tanh(W2 . h1^T + b2)
     {
         f32x4 h2[HT];
-        gemm_h<KBH, T1, HT>(bh, bl, btail, slot1, lane, h2);
+        gemm_h<KBH, T1, HT>(bh, bl, btail, slot, lane, h2);
         NFK_HALF_STEP();
         act_operands<KBH, T1, HT>(h2, -2.0f * kL2E * un2, bh, bl, btail);
     }
@@ -607,12 +656,9 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
 
     const float l2e3 = kL2E * un3;
     float ldsum = 0.0f;
-    bool any_in = false, any_nd = false;
     for (int ch = 0; ch < a.NCH; ++ch) {
         const int jbase = 16 * ch;
-        // phase 2 + 3 ch + {0, 1, 2}: slots alternate with the phase parity
-        float4* sA = (ch & 1) ? slot1 : slot0;  // phase 2 + 3ch is even for even ch
-        float4* sB = (ch & 1) ? slot0 : slot1;
+        // phases 2 + 3 ch + {0, 1, 2}
         int jj4[4];
         float xv[4];
         int kb[4];
@@ -621,30 +667,30 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
         // ---- phase A: searched knots (widths forward / heights inverse)
         {
             f32x4 acc[K];
-            gemm_h<KBH, T1, K>(bh, bl, btail, sA, lane, acc);
+            gemm_h<KBH, T1, K>(bh, bl, btail, slot, lane, acc);
             NFK_HALF_STEP();
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 jj4[r] = jbase + 4 * q + r;
                 xv[r] = (jj4[r] < a.n_up) ? xup[sl * XU + jj4[r]] : 0.0f;
             }
-            knot_phase<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k);
+            knot_phase<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
         }
         NFK_HALF_STEP();
 
         // ---- phase B: the other knots, selected at the bin
         {
             f32x4 acc[K];
-            gemm_h<KBH, T1, K>(bh, bl, btail, sB, lane, acc);
+            gemm_h<KBH, T1, K>(bh, bl, btail, slot, lane, acc);
             NFK_HALF_STEP();
-            knot_phase<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k);
+            knot_phase<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
         }
         NFK_HALF_STEP();
 
         // ---- phase C: derivatives of the bin, evaluate, log|det|
         {
             f32x4 accd[DN];
-            gemm_h<KBH, T1, DN>(bh, bl, btail, sA, lane, accd);
+            gemm_h<KBH, T1, DN>(bh, bl, btail, slot, lane, accd);
             NFK_HALF_STEP();
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
@@ -664,15 +710,28 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                 // raw_k = logit k-1, raw_k1 = logit k, by running select on k >= j
                 const int k = kb[r];
                 float raw_k = accd[0][r], raw_k1 = accd[0][r];
+                if (NFK_LUT) {
+                    // row j + 1 = logit j (rows 0 and K unused)
+                    float* fs = reinterpret_cast<float*>(scr);
 #pragma unroll
-                for (int j = 1; j < K - 1; ++j) {
-                    raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
-                    raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
+                    for (int j = 0; j < K - 1; ++j) fs[(j + 1) * 64 + lane] = accd[j][r];
+                    raw_k = fs[k * 64 + lane];
+                    raw_k1 = fs[(k + 1) * 64 + lane];
+                } else {
+#pragma unroll
+                    for (int j = 1; j < K - 1; ++j) {
+                        raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
+                        raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
+                    }
                 }
                 // d = min_d + softplus(softplus(D)) (flows.py:235, utils.py:82), only
                 // at the two knots the bin uses; the padded ends are the constant d_edge
-                const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k * un3, c.min_d);
-                const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1 * un3, c.min_d);
+                // both evaluated, then selected: as a conditional the compiler
+                // branches around the exp/log under an exec mask
+                const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
+                const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
+                const float d_k = (k == 0) ? c.d_edge : dv_k;
+                const float d_k1 = (k == K - 1) ? c.d_edge : dv_k1;
                 const float x = xv[r];
                 // one reciprocal of the bin width for delta and theta
                 const float rw = nfk_rcp_fast(w_k[r]);
@@ -713,49 +772,44 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf(FusedArgs a) {
                 any_nd |= nd && inside && live;
             }
         }
-        if (grp == 0 || ch + 1 < a.NCH) NFK_HALF_STEP();  // group 1 ends one barrier early
+        NFK_HALF_STEP();
     }
+
 
     // ---- z rows of this wave (upper from the tile, lower = identity copy), log|det|
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int i = lane; i < 16 * a.n_up; i += 64) {
-        const int row = i / a.n_up, j = i - row * a.n_up;
-        if (row < nrows) a.z[(b0 + row) * a.ldz + m_up_out[j]] = xup[row * XU + j];
-    }
-    for (int i = lane; i < 16 * a.n_lo; i += 64) {
-        const int row = i / a.n_lo, j = i - row * a.n_lo;
-        if (row < nrows) a.z[(b0 + row) * a.ldz + m_lo_out[j]] = xlo[row * XL + j];
-    }
+    for (RowWalk w(lane, a.n_up); w.r < nrows; w.next())
+        a.z[(b0 + w.r) * a.ldz + m_up_out[w.k]] = xup[w.r * XU + w.k];
+    for (RowWalk w(lane, a.n_lo); w.r < nrows; w.next())
+        a.z[(b0 + w.r) * a.ldz + m_lo_out[w.k]] = xlo[w.r * XL + w.k];
     {
         float v = ldsum;
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        if (q == 0 && row_ok && a.mode != 0) {
-            float* dst = a.logdet + b0 + sl;
-            *dst = (a.mode == 2) ? (*dst + v) : v;
-        }
-    }
-    if (a.status != nullptr) {
-        const int bits = (__any(any_in) ? NFK_ST_INSIDE_SEEN : 0) | (__any(any_nd) ? NFK_ST_NEG_DISC : 0);
-        if (lane == 0 && bits != 0) {
-            if ((__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bits) != bits)
-                atomicOr(a.status, bits);
-        }
+        if (q == 0 && row_ok && a.mode != 0) a.logdet[b0 + sl] = ld_prev + v;  // mode 1: ld_prev = 0
     }
 #undef NFK_HALF_STEP
+    if (a.status != nullptr) {
+        const int bits = (__any(any_in) ? NFK_ST_INSIDE_SEEN : 0) | (__any(any_nd) ? NFK_ST_NEG_DISC : 0);
+        if (lane == 0 && bits != 0 && (st_prev & bits) != bits) atomicOr(a.status, bits);
+    }
+#ifdef NFK_TRACE
+    NFK_MARK(tr);  // end
+    nfk_trace_flush(tr, a.trace, wid, lane);
+#endif
 }
 
 template <int KBH, int T1, int K>
 int launch_fused(const FusedArgs& a, size_t lds, bool inv, hipStream_t st) {
-    const int64_t per_block = (int64_t)kWaves * 16;
+    const int64_t per_block = (int64_t)kNsfWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
     if (inv)
-        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true>), dim3((unsigned)blocks), dim3(64 * kWaves),
-                           lds, st, a);
+        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true>), dim3((unsigned)blocks), dim3(64 * kNsfWaves), lds,
+                           st, a);
     else
-        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, false>), dim3((unsigned)blocks), dim3(64 * kWaves),
-                           lds, st, a);
+        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, false>), dim3((unsigned)blocks), dim3(64 * kNsfWaves), lds,
+                           st, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

@@ -1,6 +1,10 @@
-"""Timeline of the wide fused NSF kernel (c5 layer) from a -DNFK_TRACE build.
+"""Timeline of the fused NSF kernels from a -DNFK_TRACE build.
 
 NFK_LIBRARY=.../libnfk_trace.so python tools/trace_wide.py [--batch N] [--inverse]
+    c5 layer (wide kernel, nfk_fused_wide.h)
+NFK_LIBRARY=.../libnfk_trace.so python tools/trace_wide.py --c3
+    c3 layer (narrow kernel, nfk_fused_impl.h): per phase "gemm" (previous mark
+    -> GEMM issued), "epi" (-> epilogue done), "barrier" (-> barrier passed)
 
 Every 512th workgroup records s_memtime at each mark of every wave
 (nfk_fused_wide.h NFK_MARK): start, prologue done, per sub-step "GEMM
@@ -28,12 +32,16 @@ def main():
     ap.add_argument("--size", type=int, default=128)
     ap.add_argument("--K", type=int, default=16)
     ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--c3", action="store_true")
+    ap.add_argument("--slots1", action="store_true", help="c3 kernel built with NFK_NSF_SLOTS=1")
     args = ap.parse_args()
+    if args.c3:
+        args.size, args.K, args.hidden = 32, 8, 100
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     layer = nff.NSF_CL(size=args.size, dim=2, K=args.K, B=3, hidden_dim=args.hidden, mask=[0]).to(dev)
     x = torch.randn(args.batch, 2 * args.size, device=dev)
-    nwg = (args.batch + 127) // 128
+    nwg = (args.batch + 63) // 64  # workgroups of 4 or 8 waves: sized for 4
     slots = (nwg + 511) // 512
     buf = torch.zeros(slots * 16 * 260, dtype=torch.int32, device=dev)
     lib = _lib.load()
@@ -52,19 +60,27 @@ def main():
     tot = (marks[:, -1] - marks[:, 0]) % (1 << 32)
     # classify the intervals: 0 prologue-to-start... follow the mark order of the kernel
     S1, S2, SC = 2, 4, 2  # c5 shape (H=256, K=16, n_lo=128)
-    if args.hidden != 256 or args.K != 16 or args.size != 128:
-        print("note: categories assume the c5 shape")
     cats = []
-    cats.append("prologue")                       # start -> prologue done
-    for _ in range(S1 + S2):
+    if args.c3:
+        cats.append("prologue")
+        for ph in ["L1", "L2"] + list("ABC") * ((args.size + 15) // 16):
+            cats += (["gemm_" + ph, "bar_gemm", "epi_" + ph, "bar_epi"] if args.slots1
+                     else ["gemm_" + ph, "epi_" + ph, "barrier"])
+        cats.append("tail")
+    elif args.hidden != 256 or args.K != 16 or args.size != 128:
+        print("note: categories assume the c5 shape")
+    for _ in range(0 if args.c3 else 1):
+        cats.append("prologue")                       # start -> prologue done
+    for _ in range(0 if args.c3 else S1 + S2):
         cats += ["gemm_L12", "barrier"]
-    nch = (args.size + 7) // 8
+    nch = 0 if args.c3 else (args.size + 7) // 8
     for _ in range(nch):
         for ph in "ABC":
             for _ in range(SC):
                 cats += ["gemm_" + ph, "barrier"]
             cats.append("epi_" + ph)
-    cats.append("tail")
+    if not args.c3:
+        cats.append("tail")
     cats = cats[:d.shape[1]]
     print("waves traced: %d, marks per wave: %d, mean wave cycles: %.0f" % (len(waves), n, tot.mean()))
     agg = {}
@@ -78,8 +94,8 @@ def main():
     for c, cnt, m, s in rows:
         print("%-10s %6d %12.0f %14.0f %6.1f%%" % (c, cnt, m, s, 100.0 * s / tot.mean()))
     # first chunk's per-interval detail for wave 0 of the first traced workgroup
-    print("chunk-0 intervals (wave mean):", " ".join("%s=%.0f" % (cats[i], d[:, i].mean())
-                                                     for i in range(13, min(28, d.shape[1]))))
+    lo, hi = (0, d.shape[1]) if args.c3 else (13, min(28, d.shape[1]))
+    print("intervals (wave mean):", " ".join("%s=%.0f" % (cats[i], d[:, i].mean()) for i in range(lo, hi)))
 
 
 if __name__ == "__main__":
