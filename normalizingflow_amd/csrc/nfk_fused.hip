@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -464,9 +465,17 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
     if (!narrow) return launch_wide(a, L, K, inv, st);
-    const size_t lds = lds_bytes(L);
+    // split form (sub-records, three workgroups per CU) where it fits;
+    // NFK_FUSED_SPLIT=0 in the environment selects whole records (A/B runs)
+    static const bool split_env = [] {
+        const char* e = std::getenv("NFK_FUSED_SPLIT");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    const bool split = split_env && split_ok(L);
+    if (split) a.slot_blocks = split_slot_blocks(L);
+    const size_t lds = split ? lds_bytes_split(L) : lds_bytes(L);
 #define DISPATCH(h, t, k) \
-    if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, st);
+    if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, split, st);
 #define DISPATCH_KB(h, t) NFK_FUSED_K(DISPATCH, h, t)
     NFK_FUSED_KB(DISPATCH_KB)
 #undef DISPATCH_KB

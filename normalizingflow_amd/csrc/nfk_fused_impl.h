@@ -163,6 +163,20 @@ inline size_t lds_bytes(const Layout& L) {
            NFK_LDS_PAD;
 }
 
+// Split form (NfkSplit): slot of KBH NS 2 + T1 + 1 blocks (at least the
+// layer-1 record); used when three workgroups then fit a CU.
+inline int split_slot_blocks(const Layout& L) {
+    const int ns = L.KBH <= 3 ? 4 : 2;
+    const int sb = L.KBH * ns * 2 + L.T1 + 1;
+    return sb > L.blk_h1 ? sb : L.blk_h1;
+}
+inline size_t lds_bytes_split(const Layout& L) {
+    Layout S = L;
+    S.slot_blocks = split_slot_blocks(L);
+    return lds_bytes(S);
+}
+inline bool split_ok(const Layout& L) { return L.wide == 0 && 3 * lds_bytes_split(L) <= (size_t)kLdsBytes; }
+
 // hidden feature computed by row i (0..15) of hidden tile t (>= H: padding)
 __host__ __device__ inline int hid_feature(int t, int i, int kbh) {
     if (t < 2 * kbh) return 32 * (t >> 1) + 8 * (i >> 2) + 4 * (t & 1) + (i & 3);
@@ -327,30 +341,33 @@ __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, 
 // chain blocks the SIMD partner wave's VALU, two interleaved chains let it
 // overlap (tools/ubench_coexec2.hip, modes 5-6).  A fragments of the next
 // pair are read from the LDS slot while the current pair's MFMAs run.
-template <int KBH, bool T1, int NT>
+// Split form (sub-records, k_fused_nsf<..., SPLIT = true>): the slot holds
+// tiles [T0, T0 + NT) of a record, at a tile stride of NS per k-block, then
+// the tail group holding them and the record's whole bias block; acc has NA
+// tiles and this call fills acc[T0 .. T0 + NT).  Whole records: NS = NA = NT.
+template <int KBH, bool T1, int NT, int NS = NT, int T0 = 0, int NA = NT>
 __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH], float btail,
-                                       const float4* slot, int lane, f32x4 (&acc)[NT]) {
+                                       const float4* slot, int lane, f32x4 (&acc)[NA]) {
     constexpr int NPR = (NT + 1) / 2;  // tile pairs (the last may be a single tile)
     constexpr int N = KBH * NPR;
-    constexpr int NTG = T1 ? (NT + 3) / 4 : 0;
+    constexpr int NTG = T1 ? (NS + 3) / 4 : 0;
     const int q = lane >> 4;
-    const float4* tail = slot + KBH * NT * 2 * 64;
+    const float4* tail = slot + KBH * NS * 2 * 64;
     const float4* bias = tail + NTG * 64;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = as_f32x4(bias[t * 4 + q]);
+    for (int t = 0; t < NT; ++t) acc[T0 + t] = as_f32x4(bias[(T0 + t) * 4 + q]);
     if constexpr (T1) {
 #pragma unroll
-        for (int g = 0; g < NTG; ++g) {
+        for (int t = 0; t < NT; ++t) {
+            const int g = ((T0 + t) >> 2) - (T0 >> 2), e = (T0 + t) & 3;
             const float4 w = tail[g * 64 + lane];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (4 * g + e < NT) acc[4 * g + e] = mfma32(pick4(w, e), btail, acc[4 * g + e]);
+            acc[T0 + t] = mfma32(pick4(w, e), btail, acc[T0 + t]);
         }
     }
     // blocks of pair i = (kb, pr): tile t0 = 2 pr {hi, lo}, tile t0 + 1 {hi, lo}
     auto blk = [](int i, int j) {  // j = 0..3
         const int kb = i / NPR, pr = i - kb * NPR;
-        return (kb * NT + 2 * pr) * 2 + j;
+        return (kb * NS + 2 * pr) * 2 + j;
     };
     float4 ring[2][4];
 #pragma unroll
@@ -358,8 +375,8 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
         if (2 * (0 % NPR) + (j >> 1) < NT) ring[0][j] = slot[blk(0, j) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const int kb = i / NPR, pr = i - kb * NPR, t0 = 2 * pr;
-        const bool two = t0 + 1 < NT;
+        const int kb = i / NPR, pr = i - kb * NPR, t0 = T0 + 2 * pr;
+        const bool two = t0 + 1 < T0 + NT;
         if (i + 1 < N) {
             const int pn = (i + 1) % NPR;
 #pragma unroll
@@ -509,30 +526,93 @@ __device__ __forceinline__ void stage_phase(const FusedArgs& a, int p, int offA,
     }
 }
 
-// End of half-step hs: retire this wave's LDS reads (and after an epilogue
-// its copies), barrier; after a GEMM half issue the next record's copy.
-__device__ __forceinline__ void half_step(int& hs, int np, const FusedArgs& a, int offA, int offB, int offC,
-                                          float4* slot, int wid, int lane, NfkTrace& tr) {
-    NFK_MARK(tr);  // half-step's work issued
-    if (hs & 1)
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+// ---- split form: records cut into sub-records of NS tiles (NfkSplit), so the
+// slot shrinks to KBH NS 2 + 2 blocks and three workgroups share a CU.
+template <int KBH, bool T1, int K, int HT>
+struct NfkSplit {
+    static constexpr int NS = KBH <= 3 ? 4 : 2;      // tiles per sub-record
+    static constexpr int NH2 = (HT + NS - 1) / NS;   // layer-2 sub-records
+    static constexpr int NW = (K + NS - 1) / NS;     // W (or H) logits sub-records
+    static constexpr int ND = (K - 1 + NS - 1) / NS; // derivative logits sub-records
+    static constexpr int SPC = 2 * NW + ND;          // sub-records per chunk
+    static constexpr int slot_blocks = KBH * NS * 2 + (T1 ? 1 : 0) + 1;
+};
+
+// Copy tiles [t0, t0 + NS) (fewer at the record's end) of the record at rec
+// (nt tiles) into the slot at tile stride NS: per k-block NS x {hi, lo}
+// blocks, then the tail group holding them, then the record's bias block.
+template <int KBH, bool T1, int NS>
+__device__ __forceinline__ void stage_tiles(const float* __restrict__ rec, int nt, int t0, float4* slot, int wid,
+                                            int lane) {
+    constexpr int NF = KBH * NS * 2, NB = NF + (T1 ? 1 : 0) + 1;
+    const int nts = (nt - t0) < NS ? (nt - t0) : NS;
+    const uint32_t base = lds_addr(slot);
+    for (int i = wid; i < NB; i += kNsfWaves) {
+        int src;
+        if (i < NF) {
+            const int kb = i / (2 * NS), r = i - kb * 2 * NS;
+            if ((r >> 1) >= nts) continue;
+            src = (kb * nt + t0 + (r >> 1)) * 2 + (r & 1);
+        } else if (T1 && i == NF) {
+            src = KBH * nt * 2 + (t0 >> 2);
+        } else {
+            src = KBH * nt * 2 + (T1 ? (nt + 3) / 4 : 0);
+        }
+        dma16(rec + (int64_t)src * 256 + lane * 4, base + i * 1024);
+    }
+}
+
+// Stage sub-record s of the split sequence: layer 1 (whole), NH2 layer-2
+// sub-records, then per chunk NW searched-knot, NW other-knot and ND
+// derivative sub-records.
+template <int KBH, bool T1, int K, int HT>
+__device__ __forceinline__ void stage_split(const FusedArgs& a, int s, int offA, int offB, int offC, float4* slot,
+                                            int wid, int lane) {
+    using S = NfkSplit<KBH, T1, K, HT>;
+    if (s == 0) {
+        stage_record<kNsfWaves>(a.pack + a.o_h1, a.blk_h1, slot, wid, lane);
+        return;
+    }
+    if (s <= S::NH2) {
+        stage_tiles<KBH, T1, S::NS>(a.pack + a.o_h2, HT, (s - 1) * S::NS, slot, wid, lane);
+        return;
+    }
+    const int u = s - 1 - S::NH2, ch = u / S::SPC, v = u - ch * S::SPC;
+    const float* wc = a.pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
+    if (v < S::NW)
+        stage_tiles<KBH, T1, S::NS>(wc + offA * 256, K, v * S::NS, slot, wid, lane);
+    else if (v < 2 * S::NW)
+        stage_tiles<KBH, T1, S::NS>(wc + offB * 256, K, (v - S::NW) * S::NS, slot, wid, lane);
     else
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    NFK_MARK(tr);  // barrier passed
-    if (!(hs & 1) && hs / 2 + 1 < np) stage_phase(a, hs / 2 + 1, offA, offB, offC, slot, wid, lane);
-    ++hs;
+        stage_tiles<KBH, T1, S::NS>(wc + offC * 256, K - 1, (v - 2 * S::NW) * S::NS, slot, wid, lane);
+}
+
+// GEMM over all parts J, J+1, ... of an NT-tile record: each part is followed
+// by step(last) (barrier, next copy; if not last, wait for it).
+template <int KBH, bool T1, int NT, int NS, int J, class Step>
+__device__ __forceinline__ void gemm_parts(const h8 (&bh)[KBH], const h8 (&bl)[KBH], float btail,
+                                           const float4* slot, int lane, f32x4 (&acc)[NT], Step&& step) {
+    constexpr int T0 = J * NS;
+    constexpr int N = (NT - T0) < NS ? (NT - T0) : NS;
+    constexpr bool last = T0 + NS >= NT;
+    gemm_h<KBH, T1, N, NS, T0, NT>(bh, bl, btail, slot, lane, acc);
+    step(last);
+    if constexpr (!last) gemm_parts<KBH, T1, NT, NS, J + 1>(bh, bl, btail, slot, lane, acc, step);
 }
 
 #ifndef NFK_NSF_WPE
 #define NFK_NSF_WPE 2  // waves per SIMD the register budget is sized for
 #endif
 
-template <int KBH, bool T1, int K, bool INV>
-__global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(FusedArgs a) {
+#ifndef NFK_NSF_WPE_SPLIT
+#define NFK_NSF_WPE_SPLIT 3  // split form: three workgroups per CU
+#endif
+
+template <int KBH, bool T1, int K, bool INV, bool SPLIT>
+__global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF_WPE) void k_fused_nsf(FusedArgs a) {
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
+    using SP = NfkSplit<KBH, T1, K, HT>;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4, sl = lane & 15;
@@ -558,11 +638,54 @@ __global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(Fused
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const bool row_ok = sl < nrows;
-    int hs = 0;  // half-step
-#define NFK_HALF_STEP() half_step(hs, NP, a, offA, offB, offC, slot, wid, lane, tr)
-
+    h8 bh[KBH], bl[KBH];  // B operands (activations) of the current product
+    float btail = 0.0f;
     NfkTrace tr;
+    (void)tr;
     NFK_MARK(tr);  // start
+
+    // Sub-record sequence: whole records (sr = phase) or the split form's
+    // sub-records.  gemm_end ends a GEMM (part): LDS reads retired, barrier,
+    // the next sub-record's copy issued; inside a split record it also waits
+    // for that copy.  epi_end ends an epilogue: the copy has landed, barrier.
+    const int NSR = SPLIT ? 1 + SP::NH2 + a.NCH * SP::SPC : NP;
+    int sr = 0;
+    auto gemm_end = [&](bool last) {
+        NFK_MARK(tr);  // GEMM issued
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        NFK_MARK(tr);  // barrier passed
+        if (sr + 1 < NSR) {
+            if constexpr (SPLIT)
+                stage_split<KBH, T1, K, HT>(a, sr + 1, offA, offB, offC, slot, wid, lane);
+            else
+                stage_phase(a, sr + 1, offA, offB, offC, slot, wid, lane);
+        }
+        ++sr;
+        if (!last) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+    };
+    auto epi_end = [&]() {
+        NFK_MARK(tr);  // epilogue issued
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        NFK_MARK(tr);  // barrier passed
+    };
+    // a GEMM over a whole record (acc: its NT tiles), then the step(s)
+    auto gemm_rec = [&](auto& acc) {
+        constexpr int N = sizeof(acc) / sizeof(f32x4);
+        if constexpr (SPLIT) {
+            gemm_parts<KBH, T1, N, SP::NS, 0>(bh, bl, btail, slot, lane, acc, gemm_end);
+        } else {
+            gemm_h<KBH, T1, N>(bh, bl, btail, slot, lane, acc);
+            gemm_end(true);
+        }
+    };
 
     // ---- prologue: index maps, pack scale factors, the log|det| being
     // accumulated and the status word (plain loads, before any DMA is in
@@ -639,20 +762,17 @@ __global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(Fused
             }
         }
     }
-    NFK_HALF_STEP();
+    gemm_end(true);
     // epilogue 0: tanh of acc 2^-(s1+sx), split -> layer-2 operands
-    h8 bh[KBH], bl[KBH];
-    float btail;
     act_operands<KBH, T1, HT>(h1, -2.0f * kL2E * unx, bh, bl, btail);
-    NFK_HALF_STEP();
+    epi_end();
     // ---- phase 1: layer 2, fp16 split: h2^T = tanh(W2 . h1^T + b2)
     {
         f32x4 h2[HT];
-        gemm_h<KBH, T1, HT>(bh, bl, btail, slot, lane, h2);
-        NFK_HALF_STEP();
+        gemm_rec(h2);
         act_operands<KBH, T1, HT>(h2, -2.0f * kL2E * un2, bh, bl, btail);
     }
-    NFK_HALF_STEP();
+    epi_end();
 
     const float l2e3 = kL2E * un3;
     float ldsum = 0.0f;
@@ -667,8 +787,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(Fused
         // ---- phase A: searched knots (widths forward / heights inverse)
         {
             f32x4 acc[K];
-            gemm_h<KBH, T1, K>(bh, bl, btail, slot, lane, acc);
-            NFK_HALF_STEP();
+            gemm_rec(acc);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 jj4[r] = jbase + 4 * q + r;
@@ -676,22 +795,20 @@ __global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(Fused
             }
             knot_phase<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
         }
-        NFK_HALF_STEP();
+        epi_end();
 
         // ---- phase B: the other knots, selected at the bin
         {
             f32x4 acc[K];
-            gemm_h<KBH, T1, K>(bh, bl, btail, slot, lane, acc);
-            NFK_HALF_STEP();
+            gemm_rec(acc);
             knot_phase<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
         }
-        NFK_HALF_STEP();
+        epi_end();
 
         // ---- phase C: derivatives of the bin, evaluate, log|det|
         {
             f32x4 accd[DN];
-            gemm_h<KBH, T1, DN>(bh, bl, btail, slot, lane, accd);
-            NFK_HALF_STEP();
+            gemm_rec(accd);
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -772,7 +889,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(Fused
                 any_nd |= nd && inside && live;
             }
         }
-        NFK_HALF_STEP();
+        epi_end();
     }
 
 
@@ -788,7 +905,6 @@ __global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(Fused
         v += __shfl_xor(v, 32, 64);
         if (q == 0 && row_ok && a.mode != 0) a.logdet[b0 + sl] = ld_prev + v;  // mode 1: ld_prev = 0
     }
-#undef NFK_HALF_STEP
     if (a.status != nullptr) {
         const int bits = (__any(any_in) ? NFK_ST_INSIDE_SEEN : 0) | (__any(any_nd) ? NFK_ST_NEG_DISC : 0);
         if (lane == 0 && bits != 0 && (st_prev & bits) != bits) atomicOr(a.status, bits);
@@ -800,16 +916,22 @@ __global__ __launch_bounds__(64 * kNsfWaves, NFK_NSF_WPE) void k_fused_nsf(Fused
 }
 
 template <int KBH, int T1, int K>
-int launch_fused(const FusedArgs& a, size_t lds, bool inv, hipStream_t st) {
+int launch_fused(const FusedArgs& a, size_t lds, bool inv, bool split, hipStream_t st) {
     const int64_t per_block = (int64_t)kNsfWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
-    if (inv)
-        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true>), dim3((unsigned)blocks), dim3(64 * kNsfWaves), lds,
-                           st, a);
-    else
-        hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, false>), dim3((unsigned)blocks), dim3(64 * kNsfWaves), lds,
-                           st, a);
+    const dim3 g((unsigned)blocks), b(64 * kNsfWaves);
+    if (split) {
+        if (inv)
+            hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true, true>), g, b, lds, st, a);
+        else
+            hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, false, true>), g, b, lds, st, a);
+    } else {
+        if (inv)
+            hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true, false>), g, b, lds, st, a);
+        else
+            hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, false, false>), g, b, lds, st, a);
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -818,9 +940,9 @@ int launch_fused(const FusedArgs& a, size_t lds, bool inv, hipStream_t st) {
 // per hidden k-block count so make -j compiles them in parallel); nfk_fused.hip
 // sees only the extern declarations.
 #define NFK_FUSED_INSTANCE(KBH, T1, K) \
-    template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
+    template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, hipStream_t st);
 #define NFK_FUSED_EXTERN(KBH, T1, K) \
-    extern template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, hipStream_t st);
+    extern template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, hipStream_t st);
 
 // hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f32 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132
