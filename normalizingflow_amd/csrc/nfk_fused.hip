@@ -327,6 +327,7 @@ int64_t pack_floats(int n_lo, int n_up, int H, int K) {
 }
 
 uint32_t* g_trace = nullptr;  // diagnostic timeline buffer (NFK_TRACE builds)
+int g_form = -1;            // nfk_debug_fused_form
 
 int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_t st) {
     WideArgs a;
@@ -366,6 +367,15 @@ int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_
 extern "C" int nfk_debug_trace(void* buf) {
     g_trace = static_cast<uint32_t*>(buf);
     return 0;
+}
+
+// Diagnostic: form of k_fused_nsf: -1 = automatic (split where it fits unless
+// NFK_FUSED_SPLIT=0), 0 = whole records, 1 = split where it fits.  Returns the
+// previous setting.  Not part of include/nfk.h.
+extern "C" int nfk_debug_fused_form(int form) {
+    const int prev = g_form;
+    g_form = form < 0 ? -1 : (form ? 1 : 0);
+    return prev;
 }
 
 extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
@@ -466,13 +476,18 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     const bool inv = inverse != 0;
     if (!narrow) return launch_wide(a, L, K, inv, st);
     // split form (sub-records, three workgroups per CU) where it fits;
-    // NFK_FUSED_SPLIT=0 in the environment selects whole records (A/B runs)
+    // NFK_FUSED_SPLIT=0 in the environment or nfk_debug_fused_form(0) selects
+    // whole records (A/B runs, tests of both forms)
     static const bool split_env = [] {
         const char* e = std::getenv("NFK_FUSED_SPLIT");
         return !(e != nullptr && e[0] == '0');
     }();
-    const bool split = split_env && split_ok(L);
-    if (split) a.slot_blocks = split_slot_blocks(L);
+    const bool aligned16 = ((uintptr_t)x % 16) == 0 && ((uintptr_t)z % 16) == 0 && ldx % 4 == 0 && ldz % 4 == 0;
+    const bool split = (g_form < 0 ? split_env : g_form == 1) && split_ok(L) && aligned16;
+    if (split) {
+        a.slot_blocks = split_slot_blocks(L);
+        a.xtile = 16 * (n_lo + n_up + 1);
+    }
     const size_t lds = split ? lds_bytes_split(L) : lds_bytes(L);
 #define DISPATCH(h, t, k) \
     if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, split, st);

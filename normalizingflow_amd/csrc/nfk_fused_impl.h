@@ -18,6 +18,12 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef NFK_NSF_WAVES
 #define NFK_NSF_WAVES 4  // waves per workgroup of k_fused_nsf (one per SIMD)
 #endif
+#ifndef NFK_SPLIT_NS
+#define NFK_SPLIT_NS 4  // split form: tiles per sub-record (KBH <= 3)
+#endif
+#ifndef NFK_NSF_WPE_SPLIT
+#define NFK_NSF_WPE_SPLIT 3  // split form: workgroups per CU (waves per SIMD)
+#endif
 #ifndef NFK_LDS_PAD
 #define NFK_LDS_PAD 0  // diagnostic: extra LDS per k_fused_nsf workgroup (fewer per CU)
 #endif
@@ -159,23 +165,30 @@ inline size_t lds_bytes(const Layout& L) {
     const int D = L.n_lo + L.n_up;
     const size_t maps = (size_t)((2 * D + 3) / 4) * 16;
     return (size_t)L.slot_blocks * 1024 + maps + (size_t)kNsfWaves * x_tile_floats(L) * sizeof(float) +
-           (size_t)kNsfWaves * (L.K + 1) * 64 * sizeof(int) +  // bin lookup tables
+           (size_t)kNsfWaves * L.K * 64 * sizeof(int) +  // bin lookup tables
            NFK_LDS_PAD;
 }
 
 // Split form (NfkSplit): slot of KBH NS 2 + T1 + 1 blocks (at least the
 // layer-1 record); used when three workgroups then fit a CU.
 inline int split_slot_blocks(const Layout& L) {
-    const int ns = L.KBH <= 3 ? 4 : 2;
+    const int ns = L.KBH <= 3 ? NFK_SPLIT_NS : 2;
     const int sb = L.KBH * ns * 2 + L.T1 + 1;
     return sb > L.blk_h1 ? sb : L.blk_h1;
 }
+// split-form LDS: the slot, four maps + the output->input column map, each
+// wave's [16][D + 1] tile of whole x rows, the lookup tables
 inline size_t lds_bytes_split(const Layout& L) {
-    Layout S = L;
-    S.slot_blocks = split_slot_blocks(L);
-    return lds_bytes(S);
+    const int D = L.n_lo + L.n_up;
+    return (size_t)split_slot_blocks(L) * 1024 + (size_t)((3 * D + 3) / 4) * 16 +
+           (size_t)kNsfWaves * 16 * (D + 1) * sizeof(float) + (size_t)kNsfWaves * L.K * 64 * sizeof(int) +
+           NFK_LDS_PAD;
 }
-inline bool split_ok(const Layout& L) { return L.wide == 0 && 3 * lds_bytes_split(L) <= (size_t)kLdsBytes; }
+// shape conditions of the split form (the launch also needs 16-B aligned x
+// and z rows: D, ldx, ldz multiples of 4)
+inline bool split_ok(const Layout& L) {
+    return L.wide == 0 && (L.n_lo + L.n_up) % 4 == 0 && NFK_NSF_WPE_SPLIT * lds_bytes_split(L) <= (size_t)kLdsBytes;
+}
 
 // hidden feature computed by row i (0..15) of hidden tile t (>= H: padding)
 __host__ __device__ inline int hid_feature(int t, int i, int kbh) {
@@ -463,11 +476,11 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
         }
         const int kk = kb[r];
         if (NFK_LUT) {
-            // rows 0..K-1 (row K is read, unused, when kk = K - 1)
+            // rows 0..K-1; p1 is unused when kk = K - 1 (e1 = hi below)
 #pragma unroll
             for (int j = 0; j < K; ++j) scr[j * 64 + lane] = pre[j];
             p0 = scr[kk * 64 + lane];
-            p1 = scr[(kk + 1) * 64 + lane];
+            p1 = scr[(kk + 1 < K ? kk + 1 : K - 1) * 64 + lane];
         } else {
 #pragma unroll
             for (int j = 1; j < K; ++j) {
@@ -488,7 +501,7 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
 
 // Ablation hooks for diagnostic builds (tools/ablate_build.sh; never in the
 // product build): NFK_ABL_NOSTAGE drops the chunk-loop record copies,
-// NFK_ABL_NOBAR the half-step barriers, NFK_ABL_NOEPI replaces the spline
+// NFK_ABL_NOEPI replaces the spline
 // epilogue by a sum.
 #ifdef NFK_ABL_NOSTAGE
 #define NFK_STAGE(...) ((void)0)
@@ -530,7 +543,7 @@ __device__ __forceinline__ void stage_phase(const FusedArgs& a, int p, int offA,
 // slot shrinks to KBH NS 2 + 2 blocks and three workgroups share a CU.
 template <int KBH, bool T1, int K, int HT>
 struct NfkSplit {
-    static constexpr int NS = KBH <= 3 ? 4 : 2;      // tiles per sub-record
+    static constexpr int NS = KBH <= 3 ? NFK_SPLIT_NS : 2;  // tiles per sub-record
     static constexpr int NH2 = (HT + NS - 1) / NS;   // layer-2 sub-records
     static constexpr int NW = (K + NS - 1) / NS;     // W (or H) logits sub-records
     static constexpr int ND = (K - 1 + NS - 1) / NS; // derivative logits sub-records
@@ -577,6 +590,9 @@ __device__ __forceinline__ void stage_split(const FusedArgs& a, int s, int offA,
         stage_tiles<KBH, T1, S::NS>(a.pack + a.o_h2, HT, (s - 1) * S::NS, slot, wid, lane);
         return;
     }
+#ifdef NFK_ABL_NOSTAGE
+    return;  // diagnostic: chunk-loop sub-records never copied
+#endif
     const int u = s - 1 - S::NH2, ch = u / S::SPC, v = u - ch * S::SPC;
     const float* wc = a.pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
     if (v < S::NW)
@@ -604,10 +620,6 @@ __device__ __forceinline__ void gemm_parts(const h8 (&bh)[KBH], const h8 (&bl)[K
 #define NFK_NSF_WPE 2  // waves per SIMD the register budget is sized for
 #endif
 
-#ifndef NFK_NSF_WPE_SPLIT
-#define NFK_NSF_WPE_SPLIT 3  // split form: three workgroups per CU
-#endif
-
 template <int KBH, bool T1, int K, bool INV, bool SPLIT>
 __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF_WPE) void k_fused_nsf(FusedArgs a) {
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
@@ -623,12 +635,18 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     int32_t* m_up_out = m_up_in + a.n_up;
     int32_t* m_lo_in = m_up_out + a.n_up;
     int32_t* m_lo_out = m_lo_in + a.n_lo;
+    int32_t* m_src = m_lo_out + a.n_lo;  // split form: input column of each output column
     const int XL = 32 * a.KB1;  // lower-x tile row length (n_lo padded to the k-blocks)
     const int XU = a.xup;       // upper-x tile row length (n_up padded to 4)
-    float* xlo = reinterpret_cast<float*>(lds4 + a.slot_blocks * 64 + (2 * D + 3) / 4) + wid * a.xtile;
+    // split form: xlo is this wave's [16][XS] tile of whole x rows (input column
+    // order, row stride XS = D + 1); the spline writes z's upper values over the
+    // x values they replace
+    const int XS = D + 1;
+    float* xlo = reinterpret_cast<float*>(lds4 + a.slot_blocks * 64 + (SPLIT ? 3 * D + 3 : 2 * D + 3) / 4) +
+                 wid * a.xtile;
     float* xup = xlo + 16 * XL;
     // this wave's bin lookup table: K + 1 rows of 64 lanes, after all x tiles
-    int* scr = reinterpret_cast<int*>(xlo + (kNsfWaves - wid) * a.xtile) + wid * (K + 1) * 64;
+    int* scr = reinterpret_cast<int*>(xlo + (kNsfWaves - wid) * a.xtile) + wid * K * 64;
     const FusedConst& c = a.c;
     const float* pk = a.pack;
     const int NP = 2 + 3 * a.NCH;
@@ -691,25 +709,85 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     // accumulated and the status word (plain loads, before any DMA is in
     // flight, so the end of the kernel does not wait on them), then the
     // layer-1 record and both x tiles by LDS-DMA
-    for (int i = threadIdx.x; i < a.n_up; i += 64 * kNsfWaves) {
-        m_up_in[i] = a.up_in[i];
-        m_up_out[i] = a.up_out[i];
-    }
-    for (int i = threadIdx.x; i < a.n_lo; i += 64 * kNsfWaves) {
-        m_lo_in[i] = a.lo_in[i];
-        m_lo_out[i] = a.lo_out[i];
+    if constexpr (SPLIT) {
+        // split form: whole x rows first (16-B LDS-DMA, no dependency on the
+        // maps; rows past the batch re-read row 0 of the tile), the layer-1
+        // record, then the maps by plain loads; one wait for all of it
+        if (nrows > 0) {
+            // one 4-B-per-lane DMA per 64 columns of a row: rows land at the odd
+            // stride XS = D + 1, so the per-sample reads below are bank-conflict free
+            const uint32_t base = lds_addr(xlo);
+            for (int r = 0; r < 16; ++r) {
+                const float* src = a.x + (b0 + (r < nrows ? r : 0)) * a.ldx;
+                for (int c0 = 0; c0 < D; c0 += 64)
+                    if (c0 + lane < D) dma4(src + c0 + lane, base + (r * XS + c0) * 4);
+            }
+        }
+        stage_phase(a, 0, offA, offB, offC, slot, wid, lane);
+        for (int i = threadIdx.x; i < a.n_up; i += 64 * kNsfWaves) {
+            const int ui = a.up_in[i], uo = a.up_out[i];
+            m_up_in[i] = ui;
+            m_up_out[i] = uo;
+            m_src[uo] = ui;
+        }
+        for (int i = threadIdx.x; i < a.n_lo; i += 64 * kNsfWaves) {
+            const int li = a.lo_in[i], lo = a.lo_out[i];
+            m_lo_in[i] = li;
+            m_lo_out[i] = lo;
+            m_src[lo] = li;
+        }
+    } else {
+        for (int i = threadIdx.x; i < a.n_up; i += 64 * kNsfWaves) {
+            m_up_in[i] = a.up_in[i];
+            m_up_out[i] = a.up_out[i];
+        }
+        for (int i = threadIdx.x; i < a.n_lo; i += 64 * kNsfWaves) {
+            m_lo_in[i] = a.lo_in[i];
+            m_lo_out[i] = a.lo_out[i];
+        }
     }
     const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
     const int st_prev = (a.status != nullptr && lane == 0) ? a.status[0] : 0;
     const float ld_prev = (q == 0 && row_ok && a.mode == 2) ? a.logdet[b0 + sl] : 0.0f;
-    __syncthreads();  // maps visible (no DMA in flight yet)
-    stage_phase(a, 0, offA, offB, offC, slot, wid, lane);
-    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xlo, lane);
-    if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xup, lane);
+    // split form: this lane's layer-1 columns of k-block 0 (8q + j), read from
+    // the global map now so the first operand reads need no map round trip
+    int lo_c0[8];
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lo_c0[j] = (8 * q + j < a.n_lo) ? a.lo_in[8 * q + j] : -1;
+    }
+    if constexpr (!SPLIT) {
+        __syncthreads();  // maps visible (no DMA in flight yet)
+        stage_phase(a, 0, offA, offB, offC, slot, wid, lane);
+        if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xlo, lane);
+        if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xup, lane);
+    }
     dma_barrier();
     NFK_MARK(tr);  // prologue done
 
     bool any_in = false, any_nd = false;
+
+    // layer-1 B operand of k-block kb: lower coordinates 32 kb + 8 q .. + 7 of
+    // sample sl (zero past n_lo in the split form; the whole form's padding
+    // columns hold a valid x, their weights are zero)
+    auto x_operand = [&](int kb, float4& u, float4& v) {
+        if constexpr (SPLIT) {
+            float e[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 32 * kb + 8 * q + j;
+                const int col = kb == 0 ? lo_c0[j] : (k < a.n_lo ? m_lo_in[k] : -1);
+                e[j] = col >= 0 ? xlo[sl * XS + col] : 0.0f;
+            }
+            u = make_float4(e[0], e[1], e[2], e[3]);
+            v = make_float4(e[4], e[5], e[6], e[7]);
+        } else {
+            const float4* xr = reinterpret_cast<const float4*>(xlo + sl * XL + 32 * kb + 8 * q);
+            u = xr[0], v = xr[1];
+        }
+    };
+    // tile position of upper coordinate j of sample sl
+    auto up_pos = [&](int j) { return SPLIT ? sl * XS + m_up_in[j] : sl * XU + j; };
 
     // ---- phase 0: layer 1, fp16 split.  x has any magnitude, so each
     // wave scales its tile by a power of two 2^sx that puts max|x| just under
@@ -718,9 +796,11 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     float unx;
     {
         float mx = 0.0f;
+        float4 u0, v0;  // k-block 0's operand, read once
         for (int kb = 0; kb < a.KB1; ++kb) {
-            const float4* xr = reinterpret_cast<const float4*>(xlo + sl * XL + 32 * kb + 8 * q);
-            const float4 u = xr[0], v = xr[1];
+            float4 u, v;
+            x_operand(kb, u, v);
+            if (kb == 0) u0 = u, v0 = v;
             mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))),
                                  fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
         }
@@ -742,8 +822,8 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
             h1[t] = f32x4{bv.x * bsc, bv.y * bsc, bv.z * bsc, bv.w * bsc};
         }
         for (int kb = 0; kb < a.KB1; ++kb) {
-            const float4* xr = reinterpret_cast<const float4*>(xlo + sl * XL + 32 * kb + 8 * q);
-            const float4 u = xr[0], v = xr[1];
+            float4 u = u0, v = v0;
+            if (kb > 0) x_operand(kb, u, v);
             const float xv8[8] = {u.x * sx, u.y * sx, u.z * sx, u.w * sx, v.x * sx, v.y * sx, v.z * sx, v.w * sx};
             h8 xh, xl8;
 #pragma unroll
@@ -791,7 +871,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 jj4[r] = jbase + 4 * q + r;
-                xv[r] = (jj4[r] < a.n_up) ? xup[sl * XU + jj4[r]] : 0.0f;
+                xv[r] = (jj4[r] < a.n_up) ? (SPLIT ? xlo : xup)[up_pos(jj4[r])] : 0.0f;
             }
             knot_phase<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
         }
@@ -815,7 +895,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                 float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
 #pragma unroll
                 for (int t = 0; t < DN; ++t) v += accd[t][r];
-                if (jj4[r] < a.n_up) xup[sl * XU + jj4[r]] = v;
+                if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = v;
                 ldsum += v;
                 any_in = true;
             }
@@ -828,12 +908,12 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                 const int k = kb[r];
                 float raw_k = accd[0][r], raw_k1 = accd[0][r];
                 if (NFK_LUT) {
-                    // row j + 1 = logit j (rows 0 and K unused)
+                    // row j = logit j; raw_k is unused at k = 0, raw_k1 at k = K - 1
                     float* fs = reinterpret_cast<float*>(scr);
 #pragma unroll
-                    for (int j = 0; j < K - 1; ++j) fs[(j + 1) * 64 + lane] = accd[j][r];
-                    raw_k = fs[k * 64 + lane];
-                    raw_k1 = fs[(k + 1) * 64 + lane];
+                    for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[j][r];
+                    raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
+                    raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
                 } else {
 #pragma unroll
                     for (int j = 1; j < K - 1; ++j) {
@@ -883,7 +963,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                 const bool inside = (x >= c.lo) && (x <= c.hi);
                 const bool live = jj4[r] < a.n_up && row_ok;
                 out = inside ? out : x;
-                if (jj4[r] < a.n_up) xup[sl * XU + jj4[r]] = out;  // z collected in the tile
+                if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = out;  // z collected in the tile
                 ldsum += (inside && live) ? lad : 0.0f;
                 any_in |= inside && live;
                 any_nd |= nd && inside && live;
@@ -895,10 +975,21 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
 
     // ---- z rows of this wave (upper from the tile, lower = identity copy), log|det|
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (RowWalk w(lane, a.n_up); w.r < nrows; w.next())
-        a.z[(b0 + w.r) * a.ldz + m_up_out[w.k]] = xup[w.r * XU + w.k];
-    for (RowWalk w(lane, a.n_lo); w.r < nrows; w.next())
-        a.z[(b0 + w.r) * a.ldz + m_lo_out[w.k]] = xlo[w.r * XL + w.k];
+    if constexpr (SPLIT) {
+        // whole z rows, 16 B per lane: output column o takes tile column m_src[o]
+        const int D4 = D >> 2;
+        for (RowWalk w(lane, D4); w.r < nrows; w.next()) {
+            const float* row = xlo + w.r * XS;
+            const int o = 4 * w.k;
+            *reinterpret_cast<float4*>(a.z + (b0 + w.r) * a.ldz + o) =
+                make_float4(row[m_src[o]], row[m_src[o + 1]], row[m_src[o + 2]], row[m_src[o + 3]]);
+        }
+    } else {
+        for (RowWalk w(lane, a.n_up); w.r < nrows; w.next())
+            a.z[(b0 + w.r) * a.ldz + m_up_out[w.k]] = xup[w.r * XU + w.k];
+        for (RowWalk w(lane, a.n_lo); w.r < nrows; w.next())
+            a.z[(b0 + w.r) * a.ldz + m_lo_out[w.k]] = xlo[w.r * XL + w.k];
+    }
     {
         float v = ldsum;
         v += __shfl_xor(v, 16, 64);

@@ -8,6 +8,5 @@ build() {  # name, defines
   echo "built libnfk_abl_$1.so ($2)"
 }
 build nostage "-DNFK_ABL_NOSTAGE"
-build nostage_nobar "-DNFK_ABL_NOSTAGE -DNFK_ABL_NOBAR"
 build noepi "-DNFK_ABL_NOEPI"
-build mfma_only "-DNFK_ABL_NOEPI -DNFK_ABL_NOSTAGE -DNFK_ABL_NOBAR"
+build nostage_noepi "-DNFK_ABL_NOEPI -DNFK_ABL_NOSTAGE"

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--c3", action="store_true")
     ap.add_argument("--slots1", action="store_true", help="c3 kernel built with NFK_NSF_SLOTS=1")
+    ap.add_argument("--split", type=int, default=0,
+                    help="c3 kernel in the split form with this many tiles per sub-record (NFK_SPLIT_NS)")
     args = ap.parse_args()
     if args.c3:
         args.size, args.K, args.hidden = 32, 8, 100
@@ -61,7 +63,16 @@ def main():
     # classify the intervals: 0 prologue-to-start... follow the mark order of the kernel
     S1, S2, SC = 2, 4, 2  # c5 shape (H=256, K=16, n_lo=128)
     cats = []
-    if args.c3:
+    if args.c3 and args.split:
+        # per GEMM part: "gemm" (previous mark -> GEMM issued; includes the wait
+        # for the part's copy), "bar_gemm"; per record: "epi", "bar_epi"
+        ns = args.split
+        parts = {"L1": 1, "L2": -(-7 // ns), "A": -(-8 // ns), "B": -(-8 // ns), "C": -(-7 // ns)}
+        cats.append("prologue")
+        for ph in ["L1", "L2"] + list("ABC") * ((args.size + 15) // 16):
+            cats += ["gemm_" + ph, "bar_gemm"] * parts[ph] + ["epi_" + ph, "bar_epi"]
+        cats.append("tail")
+    elif args.c3:
         cats.append("prologue")
         for ph in ["L1", "L2"] + list("ABC") * ((args.size + 15) // 16):
             cats += (["gemm_" + ph, "bar_gemm", "epi_" + ph, "bar_epi"] if args.slots1
