@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -23,6 +24,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #endif
 #ifndef NFK_NSF_WPE_SPLIT
 #define NFK_NSF_WPE_SPLIT 3  // split form: workgroups per CU (waves per SIMD)
+#endif
+#ifndef NFK_SPLIT_PIPE
+#define NFK_SPLIT_PIPE 1  // split form: pipelined chunk schedule where it applies
 #endif
 #ifndef NFK_LDS_PAD
 #define NFK_LDS_PAD 0  // diagnostic: extra LDS per k_fused_nsf workgroup (fewer per CU)
@@ -443,13 +447,13 @@ __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[
 #ifndef NFK_LUT
 #define NFK_LUT 1
 #endif
-template <int K, bool SEARCH>
+template <int K, bool SEARCH, int R0 = 0, int R1 = 4>
 __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
                                            const FusedConst& c, float l2e, int (&kb)[4],
                                            float (&ek)[4], float (&sk)[4], int* scr, int lane) {
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = R0; r < R1; ++r) {
         float v = 0.0f;
 #pragma unroll
         for (int t = 0; t < K; ++t) v += acc[t][r];
@@ -460,7 +464,7 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
     return;
 #endif
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = R0; r < R1; ++r) {
         float u[K];
         int pre[K];
 #pragma unroll
@@ -625,6 +629,8 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
     using SP = NfkSplit<KBH, T1, K, HT>;
+    // pipelined chunk schedule: split form with two sub-records per W/H/D record
+    constexpr bool PIPE = SPLIT && NFK_SPLIT_PIPE && SP::NW == 2 && SP::ND == 2;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4, sl = lane & 15;
@@ -856,120 +862,173 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
 
     const float l2e3 = kL2E * un3;
     float ldsum = 0.0f;
-    for (int ch = 0; ch < a.NCH; ++ch) {
-        const int jbase = 16 * ch;
-        // phases 2 + 3 ch + {0, 1, 2}
-        int jj4[4];
-        float xv[4];
-        int kb[4];
-        float cw_k[4], w_k[4], ch_k[4], h_k[4];
-
-        // ---- phase A: searched knots (widths forward / heights inverse)
-        {
-            f32x4 acc[K];
-            gemm_rec(acc);
+    // per-coordinate state of the chunk: lane group q holds coordinates
+    // jbase + 4q + r, r = 0..3, of sample sl
+    int jj4[4];
+    float xv[4];
+    int kb[4];
+    float cw_k[4], w_k[4], ch_k[4], h_k[4];
+    // epilogue A (searched knots: widths forward / heights inverse) for r in [R0, R1)
+    auto epi_a = [&](const f32x4(&acc)[K], int jbase, auto r0c, auto r1c) {
+        constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                jj4[r] = jbase + 4 * q + r;
-                xv[r] = (jj4[r] < a.n_up) ? (SPLIT ? xlo : xup)[up_pos(jj4[r])] : 0.0f;
-            }
-            knot_phase<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
+        for (int r = R0; r < R1; ++r) {
+            jj4[r] = jbase + 4 * q + r;
+            xv[r] = (jj4[r] < a.n_up) ? (SPLIT ? xlo : xup)[up_pos(jj4[r])] : 0.0f;
         }
-        epi_end();
-
-        // ---- phase B: the other knots, selected at the bin
-        {
-            f32x4 acc[K];
-            gemm_rec(acc);
-            knot_phase<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
-        }
-        epi_end();
-
-        // ---- phase C: derivatives of the bin, evaluate, log|det|
-        {
-            f32x4 accd[DN];
-            gemm_rec(accd);
+        knot_phase<K, true, R0, R1>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
+    };
+    // epilogue B: the other knots, selected at the bin
+    auto epi_b = [&](const f32x4(&acc)[K], auto r0c, auto r1c) {
+        constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
+        knot_phase<K, false, R0, R1>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
+    };
+    // epilogue C: derivatives of the bin, evaluate, log|det|
+    auto epi_c = [&](const f32x4(&accd)[DN], auto r0c, auto r1c) {
+        constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
 #ifdef NFK_ABL_NOEPI
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
+        for (int r = R0; r < R1; ++r) {
+            float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
 #pragma unroll
-                for (int t = 0; t < DN; ++t) v += accd[t][r];
-                if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = v;
-                ldsum += v;
-                any_in = true;
-            }
-            if (false)
+            for (int t = 0; t < DN; ++t) v += accd[t][r];
+            if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = v;
+            ldsum += v;
+            any_in = true;
+        }
+        if (false)
 #endif
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                // padded derivative index j+1 holds logit j (utils.py:36-39):
-                // raw_k = logit k-1, raw_k1 = logit k, by running select on k >= j
-                const int k = kb[r];
-                float raw_k = accd[0][r], raw_k1 = accd[0][r];
-                if (NFK_LUT) {
-                    // row j = logit j; raw_k is unused at k = 0, raw_k1 at k = K - 1
-                    float* fs = reinterpret_cast<float*>(scr);
+        for (int r = R0; r < R1; ++r) {
+            // padded derivative index j+1 holds logit j (utils.py:36-39):
+            // raw_k = logit k-1, raw_k1 = logit k
+            const int k = kb[r];
+            float raw_k = accd[0][r], raw_k1 = accd[0][r];
+            if (NFK_LUT) {
+                // row j = logit j; raw_k is unused at k = 0, raw_k1 at k = K - 1
+                float* fs = reinterpret_cast<float*>(scr);
 #pragma unroll
-                    for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[j][r];
-                    raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
-                    raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
-                } else {
+                for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[j][r];
+                raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
+                raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
+            } else {
 #pragma unroll
-                    for (int j = 1; j < K - 1; ++j) {
-                        raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
-                        raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
-                    }
+                for (int j = 1; j < K - 1; ++j) {
+                    raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
+                    raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
                 }
-                // d = min_d + softplus(softplus(D)) (flows.py:235, utils.py:82), only
-                // at the two knots the bin uses; the padded ends are the constant d_edge
-                // both evaluated, then selected: as a conditional the compiler
-                // branches around the exp/log under an exec mask
-                const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
-                const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
-                const float d_k = (k == 0) ? c.d_edge : dv_k;
-                const float d_k1 = (k == K - 1) ? c.d_edge : dv_k1;
-                const float x = xv[r];
-                // one reciprocal of the bin width for delta and theta
-                const float rw = nfk_rcp_fast(w_k[r]);
-                const float delta = h_k[r] * rw;
-                const float gap = (d_k + d_k1) - 2.0f * delta;
-                float out, th;
-                bool nd = false;
-                if (INV) {
-                    const float y = x - ch_k[r];
-                    const float qa = y * gap + h_k[r] * (delta - d_k);
-                    const float qb = h_k[r] * d_k - y * gap;
-                    const float qc = (-delta) * y;
-                    const float disc = qb * qb - (4.0f * qa) * qc;
-                    nd = !(disc >= 0.0f);
-                    const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
-                    out = root * w_k[r] + cw_k[r];
-                    th = root;
-                } else {
-                    th = (x - cw_k[r]) * rw;
-                }
-                const float t1mt = th * (1.0f - th);
-                const float den = delta + gap * t1mt;
-                if (!INV) {
-                    const float num = h_k[r] * (delta * (th * th) + d_k * t1mt);
-                    out = ch_k[r] + nfk_div<true>(num, den);
-                }
-                const float omt = 1.0f - th;
-                const float dnum =
-                    (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
-                float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
-                lad = INV ? -lad : lad;
-                const bool inside = (x >= c.lo) && (x <= c.hi);
-                const bool live = jj4[r] < a.n_up && row_ok;
-                out = inside ? out : x;
-                if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = out;  // z collected in the tile
-                ldsum += (inside && live) ? lad : 0.0f;
-                any_in |= inside && live;
-                any_nd |= nd && inside && live;
             }
+            // d = min_d + softplus(softplus(D)) (flows.py:235, utils.py:82), only
+            // at the two knots the bin uses; the padded ends are the constant d_edge
+            // both evaluated, then selected: as a conditional the compiler
+            // branches around the exp/log under an exec mask
+            const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
+            const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
+            const float d_k = (k == 0) ? c.d_edge : dv_k;
+            const float d_k1 = (k == K - 1) ? c.d_edge : dv_k1;
+            const float x = xv[r];
+            // one reciprocal of the bin width for delta and theta
+            const float rw = nfk_rcp_fast(w_k[r]);
+            const float delta = h_k[r] * rw;
+            const float gap = (d_k + d_k1) - 2.0f * delta;
+            float out, th;
+            bool nd = false;
+            if (INV) {
+                const float y = x - ch_k[r];
+                const float qa = y * gap + h_k[r] * (delta - d_k);
+                const float qb = h_k[r] * d_k - y * gap;
+                const float qc = (-delta) * y;
+                const float disc = qb * qb - (4.0f * qa) * qc;
+                nd = !(disc >= 0.0f);
+                const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
+                out = root * w_k[r] + cw_k[r];
+                th = root;
+            } else {
+                th = (x - cw_k[r]) * rw;
+            }
+            const float t1mt = th * (1.0f - th);
+            const float den = delta + gap * t1mt;
+            if (!INV) {
+                const float num = h_k[r] * (delta * (th * th) + d_k * t1mt);
+                out = ch_k[r] + nfk_div<true>(num, den);
+            }
+            const float omt = 1.0f - th;
+            const float dnum =
+                (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+            float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
+            lad = INV ? -lad : lad;
+            const bool inside = (x >= c.lo) && (x <= c.hi);
+            const bool live = jj4[r] < a.n_up && row_ok;
+            out = inside ? out : x;
+            if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = out;  // z collected in the tile
+            ldsum += (inside && live) ? lad : 0.0f;
+            any_in |= inside && live;
+            any_nd |= nd && inside && live;
         }
-        epi_end();
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+
+    if constexpr (PIPE) {
+        // Pipelined split schedule (two sub-records per record): the copy of a
+        // record's second sub-record is covered by half (two coordinates) of
+        // the previous phase's epilogue, the copy of the next record's first
+        // sub-record by the other half.  Each phase's accumulators stay live
+        // through the first GEMM part of the next phase.
+        constexpr int NSP = SP::NS;
+        f32x4 accd[DN];
+        for (int ch = 0; ch < a.NCH; ++ch) {
+            const int jbase = 16 * ch;
+            f32x4 accA[K], accB[K];
+            gemm_h<KBH, T1, NSP, NSP, 0, K>(bh, bl, btail, slot, lane, accA);
+            gemm_end(true);
+            if (ch > 0) epi_c(accd, I2{}, I4{});  // previous chunk, coordinates 2, 3
+            epi_end();
+            gemm_h<KBH, T1, K - NSP, NSP, NSP, K>(bh, bl, btail, slot, lane, accA);
+            gemm_end(true);
+            epi_a(accA, jbase, I0{}, I2{});
+            epi_end();
+            gemm_h<KBH, T1, NSP, NSP, 0, K>(bh, bl, btail, slot, lane, accB);
+            gemm_end(true);
+            epi_a(accA, jbase, I2{}, I4{});
+            epi_end();
+            gemm_h<KBH, T1, K - NSP, NSP, NSP, K>(bh, bl, btail, slot, lane, accB);
+            gemm_end(true);
+            epi_b(accB, I0{}, I2{});
+            epi_end();
+            gemm_h<KBH, T1, NSP, NSP, 0, DN>(bh, bl, btail, slot, lane, accd);
+            gemm_end(true);
+            epi_b(accB, I2{}, I4{});
+            epi_end();
+            gemm_h<KBH, T1, DN - NSP, NSP, NSP, DN>(bh, bl, btail, slot, lane, accd);
+            gemm_end(true);
+            epi_c(accd, I0{}, I2{});
+            epi_end();
+        }
+        epi_c(accd, I2{}, I4{});  // last chunk, coordinates 2, 3
+    } else {
+        for (int ch = 0; ch < a.NCH; ++ch) {
+            const int jbase = 16 * ch;
+            {
+                f32x4 acc[K];
+                gemm_rec(acc);
+                epi_a(acc, jbase, I0{}, I4{});
+            }
+            epi_end();
+            {
+                f32x4 acc[K];
+                gemm_rec(acc);
+                epi_b(acc, I0{}, I4{});
+            }
+            epi_end();
+            {
+                f32x4 accd[DN];
+                gemm_rec(accd);
+                epi_c(accd, I0{}, I4{});
+            }
+            epi_end();
+        }
     }
 
 

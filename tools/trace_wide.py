@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--slots1", action="store_true", help="c3 kernel built with NFK_NSF_SLOTS=1")
     ap.add_argument("--split", type=int, default=0,
                     help="c3 kernel in the split form with this many tiles per sub-record (NFK_SPLIT_NS)")
+    ap.add_argument("--pipe", action="store_true", help="with --split: the pipelined schedule")
     args = ap.parse_args()
     if args.c3:
         args.size, args.K, args.hidden = 32, 8, 100
@@ -63,7 +64,19 @@ def main():
     # classify the intervals: 0 prologue-to-start... follow the mark order of the kernel
     S1, S2, SC = 2, 4, 2  # c5 shape (H=256, K=16, n_lo=128)
     cats = []
-    if args.c3 and args.split:
+    ap_pipe = args.pipe
+    if args.c3 and args.split and ap_pipe:
+        # pipelined split schedule (NFK_SPLIT_PIPE): every GEMM part is followed
+        # by half an epilogue; layer 2 as the plain split form
+        cats.append("prologue")
+        cats += ["gemm_L1", "bar_gemm", "epi_L1", "bar_epi"]
+        cats += ["gemm_L2", "bar_gemm", "gemm_L2", "bar_gemm", "epi_L2", "bar_epi"]
+        for ch in range((args.size + 15) // 16):
+            for g, e in [("A", "C01prev" if ch else "none"), ("A", "A01"), ("B", "A23"), ("B", "B01"),
+                         ("C", "B23"), ("C", "C01")]:
+                cats += ["gemm_" + g, "bar_gemm", "epi_" + e[0] if e != "none" else "wait", "bar_epi"]
+        cats.append("epiC23+tail")
+    elif args.c3 and args.split:
         # per GEMM part: "gemm" (previous mark -> GEMM issued; includes the wait
         # for the part's copy), "bar_gemm"; per record: "epi", "bar_epi"
         ns = args.split
