@@ -18,8 +18,9 @@ timeout -k 10 300 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"; 
 echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; fatal $rc bench
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace \
-    -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-timer "$@" \
+    -- python3 "$ROOT/bench.py" --no-cpu-baseline "$@" \
     > "$OUT/prof.log" 2>&1; rc=$?
+grep '^{' "$OUT/prof.log" > "$OUT/prof_bench.json" || true   # the bench line of the profiled run
 echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"; fatal $rc rocprof
 find "$OUT/prof" -name "*stats*" | head
 if [ -n "${EXTRA_BENCH:-}" ]; then
