@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -109,7 +110,165 @@ struct RqsArgs {
     NfkSplineConst c;
 };
 
-template <int K, bool INV, bool PRE, bool DFULL, int EPB>
+// ---------------------------------------------------------------------------
+// Streaming form for whole samples per round (n_up <= EPB) with 16-B aligned
+// rows: a persistent grid (a few blocks per CU) walks rounds of S = EPB / n_up
+// samples.  Per round the [S n_up, P] parameter slab and the S x rows are
+// prefetched into registers (16-B loads) while the previous round computes,
+// then stored to LDS; each lane evaluates one element from its LDS
+// parameters; z rows are assembled in LDS (upper values at up_out, lower
+// copies at lo_out) and written whole with 16-B stores, so every z line is
+// written once.  log|det| per sample is summed in the same sequential order
+// as k_rqs_coupling, and the element math is the same function, so both
+// kernels give bitwise identical results.
+// ---------------------------------------------------------------------------
+template <int K, bool INV, bool PRE, bool DFULL, int EPB, bool LEAN>
+__global__ __launch_bounds__(EPB) void k_rqs_stream(RqsArgs a, int D, int64_t nrounds) {
+    constexpr int DN = NfkDN<K, DFULL>::n;
+    constexpr int P = DFULL ? 3 * K + 1 : 3 * K - 1;
+    constexpr int NPF = (EPB * P / 4 + EPB - 1) / EPB;  // param float4s per thread (max)
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* sp = smem;                  // [EPB][P] parameters
+    float* sl = sp + EPB * P;          // [EPB] per-element log|det|
+    float* sx = sl + EPB;              // [S][D] x rows
+    float* sz = sx + a.spb * D;        // [S][D] z rows
+    int* smap = reinterpret_cast<int*>(sz + a.spb * D);  // up_in, up_out, lo_in, lo_out
+    int* cover = smap + 2 * a.n_up + 2 * a.n_lo;          // [2][D] input / output column use counts
+    const int tid = threadIdx.x;
+    const int S = a.spb, n_up = a.n_up, n_lo = a.n_lo, D4 = D >> 2;
+    for (int i = tid; i < 2 * D; i += EPB) cover[i] = 0;
+    bool bad = false;  // a map leaves the first D columns: no whole-row staging
+    for (int i = tid; i < n_up; i += EPB) {
+        smap[i] = a.up_in[i];
+        smap[n_up + i] = a.up_out[i];
+        bad |= (unsigned)a.up_in[i] >= (unsigned)D || (unsigned)a.up_out[i] >= (unsigned)D;
+    }
+    for (int i = tid; i < n_lo; i += EPB) {
+        smap[2 * n_up + i] = a.lo_in[i];
+        smap[2 * n_up + n_lo + i] = a.lo_out[i];
+        bad |= (unsigned)a.lo_in[i] >= (unsigned)D || (unsigned)a.lo_out[i] >= (unsigned)D;
+    }
+    bad = __syncthreads_or(bad);
+    // whole x and z rows only if the input maps and the output maps each hit
+    // every column of [0, D) once (then x and z rows have at least D columns)
+    if (!bad) {
+        for (int i = tid; i < n_up; i += EPB) {
+            atomicAdd(&cover[smap[i]], 1);
+            atomicAdd(&cover[D + smap[n_up + i]], 1);
+        }
+        for (int i = tid; i < n_lo; i += EPB) {
+            atomicAdd(&cover[smap[2 * n_up + i]], 1);
+            atomicAdd(&cover[D + smap[2 * n_up + n_lo + i]], 1);
+        }
+    }
+    __syncthreads();
+    bool hole = false;
+    if (!bad)
+        for (int i = tid; i < 2 * D; i += EPB) hole |= cover[i] != 1;
+    const bool rows = !__syncthreads_or(bad || hole);
+    const int* m_up_in = smap;
+    const int* m_up_out = smap + n_up;
+    const int* m_lo_in = smap + 2 * n_up;
+    const int* m_lo_out = smap + 2 * n_up + n_lo;
+    const int j_el = tid % n_up, s_el = tid / n_up;  // this lane's element of a round
+    typedef float v4 __attribute__((ext_vector_type(4)));  // HIP's float4 struct kept pf in scratch
+    v4 pf[NPF];
+    v4 xf = {0.f, 0.f, 0.f, 0.f};
+    bool any_in = false, any_nd = false;  // status bits, reduced once at the end
+    // prefetch round r into registers (rows past the batch are not read): the
+    // register array stays in VGPRs only with this code inlined and unrolled
+#define NFK_PREFETCH(RR)                                                                              \
+    do {                                                                                             \
+        const int64_t pb0 = (RR) * S;                                                                \
+        const int pnb = (int)((a.batch - pb0) < S ? (a.batch - pb0) : S);                            \
+        const v4* src = reinterpret_cast<const v4*>(a.params + pb0 * n_up * P);                      \
+        const int n4 = pnb * n_up * P / 4; /* S n_up P is a multiple of 4 (host check) */            \
+        /* unconditional loads (clamped index): a conditional one keeps pf out of VGPRs */           \
+        _Pragma("unroll") for (int i = 0; i < NPF; ++i) {                                            \
+            const int pi = i * EPB + tid;                                                            \
+            pf[i] = src[pi < n4 ? pi : n4 - 1];                                                      \
+        }                                                                                            \
+        if (rows) {                                                                                  \
+            const int t4 = tid < pnb * D4 ? tid : 0;                                                 \
+            const int rr = t4 / D4, cc = t4 - rr * D4;                                               \
+            xf = *reinterpret_cast<const v4*>(a.x + (pb0 + rr) * a.ldx + 4 * cc);                    \
+        }                                                                                            \
+    } while (0)
+    int64_t r = blockIdx.x;
+    if (r < nrounds) NFK_PREFETCH(r);
+    for (; r < nrounds; r += gridDim.x) {
+        const int64_t b0 = r * S;
+        const int nb = (int)((a.batch - b0) < S ? (a.batch - b0) : S);
+        const int cnt = nb * n_up;
+        __syncthreads();  // the previous round's LDS reads are done (and the maps visible)
+#pragma unroll
+        for (int i = 0; i < NPF; ++i)
+            if (i * EPB + tid < cnt * P / 4) reinterpret_cast<v4*>(sp)[i * EPB + tid] = pf[i];
+        if (rows && tid < nb * D4) reinterpret_cast<v4*>(sx)[tid] = xf;
+        __syncthreads();
+        if (r + gridDim.x < nrounds) NFK_PREFETCH(r + gridDim.x);  // overlaps the compute below
+        bool ins = false, nd = false;
+        if (tid < cnt) {
+            const float xv = rows ? sx[s_el * D + m_up_in[j_el]] : a.x[(b0 + s_el) * a.ldx + m_up_in[j_el]];
+            float wr[K], hr[K], dr[DN];
+            const float* p = sp + tid * P;
+#pragma unroll
+            for (int i = 0; i < K; ++i) wr[i] = p[i];
+#pragma unroll
+            for (int i = 0; i < K; ++i) hr[i] = p[K + i];
+#pragma unroll
+            for (int i = 0; i < P - 2 * K; ++i) dr[i] = p[2 * K + i];
+            float out, lad;
+            if constexpr (LEAN && PRE && !DFULL)
+                nfk_rqs_element_lean<K, INV>(xv, wr, hr, dr, a.c, out, lad, ins, nd);
+            else
+                nfk_rqs_element<K, INV, PRE, DFULL>(xv, wr, hr, dr, a.c, out, lad, ins, nd);
+            if (rows)
+                sz[s_el * D + m_up_out[j_el]] = out;
+            else
+                a.z[(b0 + s_el) * a.ldz + m_up_out[j_el]] = out;
+            if (a.lad_out != nullptr) a.lad_out[(b0 + s_el) * a.ld_lad + j_el] = lad;
+            sl[tid] = lad;
+        }
+        for (int i = tid; i < nb * n_lo; i += EPB) {
+            const int ss = i / n_lo, qq = i - ss * n_lo;
+            if (rows)
+                sz[ss * D + m_lo_out[qq]] = sx[ss * D + m_lo_in[qq]];
+            else
+                a.z[(b0 + ss) * a.ldz + m_lo_out[qq]] = a.x[(b0 + ss) * a.ldx + m_lo_in[qq]];
+        }
+        any_in |= ins;
+        any_nd |= nd;
+        __syncthreads();  // z rows and per-element log|det| complete
+        if (rows && tid < nb * D4) {
+            const int rr = tid / D4, cc = tid - rr * D4;
+            *reinterpret_cast<float4*>(a.z + (b0 + rr) * a.ldz + 4 * cc) = reinterpret_cast<const float4*>(sz)[tid];
+        }
+        if (a.logdet_mode != 0 && tid < nb) {
+            // sequential sum (k_rqs_coupling's order), read 16 B at a time
+            float sum = 0.0f;
+            const float* q = sl + tid * n_up;
+            int i = 0;
+            if ((n_up & 3) == 0)
+                for (; i < n_up; i += 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(q + i);
+                    sum += v.x;
+                    sum += v.y;
+                    sum += v.z;
+                    sum += v.w;
+                }
+            for (; i < n_up; ++i) sum += q[i];
+            float* dst = a.logdet + b0 + tid;
+            *dst = (a.logdet_mode == 2) ? (*dst + sum) : sum;
+        }
+    }
+    const int st_bits = (__syncthreads_or(any_in) ? NFK_ST_INSIDE_SEEN : 0) |
+                        (__syncthreads_or(any_nd) ? NFK_ST_NEG_DISC : 0);
+    if (tid == 0) status_or(a.status, st_bits);
+#undef NFK_PREFETCH
+}
+
+template <int K, bool INV, bool PRE, bool DFULL, int EPB, bool LEAN = false>
 __global__ __launch_bounds__(EPB) void k_rqs_coupling(RqsArgs a) {
     constexpr int DN = NfkDN<K, DFULL>::n;
     constexpr int P = DFULL ? 3 * K + 1 : 3 * K - 1;
@@ -167,7 +326,10 @@ __global__ __launch_bounds__(EPB) void k_rqs_coupling(RqsArgs a) {
 #pragma unroll
             for (int i = 0; i < P - 2 * K; ++i) dr[i] = p[2 * K + i];
             float out, lad;
-            nfk_rqs_element<K, INV, PRE, DFULL>(xv, wr, hr, dr, a.c, out, lad, ins, nd);
+            if constexpr (LEAN && PRE && !DFULL)
+                nfk_rqs_element_lean<K, INV>(xv, wr, hr, dr, a.c, out, lad, ins, nd);
+            else
+                nfk_rqs_element<K, INV, PRE, DFULL>(xv, wr, hr, dr, a.c, out, lad, ins, nd);
             a.z[b * a.ldz + a.up_out[j]] = out;
             if (a.lad_out != nullptr) a.lad_out[b * a.ld_lad + j] = lad;
             sl[tid] = lad;
@@ -212,6 +374,30 @@ __global__ __launch_bounds__(EPB) void k_rqs_coupling(RqsArgs a) {
     if (tid == 0) status_or(a.status, st_bits);
 }
 
+// NSF_CL's raw-logit mode (PRE) runs the lean element math (nfk_rqs_element_lean,
+// the fused kernel's epilogue) when the spline constants are NSF_CL's (equal x
+// and y ranges, equal minimum bin width and height); NFK_RQS_LEAN=0 in the
+// environment selects the reference-order math everywhere.
+static bool lean_env() {
+    static const bool on = [] {
+        const char* e = std::getenv("NFK_RQS_LEAN");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return on;
+}
+
+// k_rqs_stream applies when a round holds whole samples, the lower and upper
+// maps cover D = n_lo + n_up columns once each (a permutation of x's and z's
+// first D columns, as NSF_CL's are), and rows are 16-B aligned;
+// NFK_RQS_STREAM=0 in the environment selects k_rqs_coupling everywhere.
+static bool stream_env() {
+    static const bool on = [] {
+        const char* e = std::getenv("NFK_RQS_STREAM");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int K, bool INV, bool PRE, bool DFULL>
 static int launch_rqs_k(RqsArgs a, hipStream_t st) {
     constexpr int P = DFULL ? 3 * K + 1 : 3 * K - 1;
@@ -220,8 +406,39 @@ static int launch_rqs_k(RqsArgs a, hipStream_t st) {
     const int64_t blocks = (a.batch + a.spb - 1) / a.spb;
     if (blocks == 0) return 0;
     const size_t lds = (size_t)(EPB * P + EPB) * sizeof(float);
-    hipLaunchKernelGGL((k_rqs_coupling<K, INV, PRE, DFULL, EPB>), dim3((unsigned)blocks),
-                       dim3(EPB), lds, st, a);
+    const bool lean = PRE && !DFULL && lean_env() && a.c.ylo == a.c.lo && a.c.yhi == a.c.hi &&
+                      a.c.min_w == a.c.min_h && a.c.fw == a.c.fh;
+    const int D = a.n_lo + a.n_up;
+    if (stream_env() && a.n_up <= EPB && D % 4 == 0 && a.ldx % 4 == 0 && a.ldz % 4 == 0 &&
+        ((uintptr_t)a.x % 16) == 0 && ((uintptr_t)a.z % 16) == 0 && ((uintptr_t)a.params % 16) == 0 &&
+        (a.spb * a.n_up * P) % 4 == 0 && a.spb * D / 4 <= EPB) {
+        const int64_t nrounds = blocks;
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        static const int bpc = [] {  // resident blocks per CU (NFK_RQS_BPC, default 4)
+            const char* e = std::getenv("NFK_RQS_BPC");
+            const int v = e != nullptr ? std::atoi(e) : 4;
+            return v >= 1 && v <= 16 ? v : 4;
+        }();
+        const int64_t grid = nrounds < (int64_t)ncu * bpc ? nrounds : (int64_t)ncu * bpc;
+        const size_t lds2 = (size_t)(EPB * P + EPB + 2 * a.spb * D) * sizeof(float) +
+                            (size_t)(2 * a.n_up + 2 * a.n_lo + 2 * D) * sizeof(int);
+        if (lean)
+            hipLaunchKernelGGL((k_rqs_stream<K, INV, PRE, DFULL, EPB, PRE && !DFULL>), dim3((unsigned)grid),
+                               dim3(EPB), lds2, st, a, D, nrounds);
+        else
+            hipLaunchKernelGGL((k_rqs_stream<K, INV, PRE, DFULL, EPB, false>), dim3((unsigned)grid), dim3(EPB),
+                               lds2, st, a, D, nrounds);
+        return launch_status("nfk_rqs_coupling");
+    }
+    if (lean)
+        hipLaunchKernelGGL((k_rqs_coupling<K, INV, PRE, DFULL, EPB, PRE && !DFULL>), dim3((unsigned)blocks),
+                           dim3(EPB), lds, st, a);
+    else
+        hipLaunchKernelGGL((k_rqs_coupling<K, INV, PRE, DFULL, EPB>), dim3((unsigned)blocks), dim3(EPB), lds,
+                           st, a);
     return launch_status("nfk_rqs_coupling");
 }
 

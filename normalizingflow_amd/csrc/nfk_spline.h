@@ -384,3 +384,85 @@ __device__ __forceinline__ void nfk_rqs_element(float x, float (&wr)[K], float (
     const float l = logf(dnum) - 2.0f * logf(den);
     lad = INV ? -l : l;
 }
+
+// Lean NSF_CL element (PRE: raw conditioner logits) for the streaming kernel:
+// the fused kernel's epilogue math (nfk_prefix_nsf_lean knots in 2^-30 fixed
+// point, integer bin search, softplus(softplus) identity, fast reciprocals;
+// nfk_fused_impl.h knot_phase / epilogue C) on one element held by one lane.
+// Valid for NSF_CL's constants: x and y knot ranges equal, min bin width =
+// height (the host checks).  Absolute error at the few-ulp level; an element
+// within an ulp of a knot may take the neighbouring bin, where the C1 spline
+// agrees.
+template <int K>
+__device__ __forceinline__ void nfk_lean_bin_edges(const int (&pre)[K], int k, const NfkSplineConst& c,
+                                                   float sp30, float& e0, float& sz) {
+    int p0 = 0, p1 = pre[1 < K ? 1 : 0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+        const bool ge = k >= j;
+        p0 = ge ? pre[j] : p0;
+        if (j + 1 < K) p1 = ge ? pre[j + 1] : p1;
+    }
+    e0 = __builtin_fmaf(sp30, (float)p0, c.lo);
+    const float e1 = (k == K - 1) ? c.hi : __builtin_fmaf(sp30, (float)p1, c.lo);
+    sz = e1 - e0;
+}
+
+template <int K, bool INV>
+__device__ __forceinline__ void nfk_rqs_element_lean(float x, const float (&wr)[K], const float (&hr)[K],
+                                                     const float (&dr)[K - 1 > 0 ? K - 1 : 1],
+                                                     const NfkSplineConst& c, float& out, float& lad,
+                                                     bool& inside, bool& neg_disc) {
+    inside = !c.tails || ((x >= c.lo) && (x <= c.hi));
+    neg_disc = false;
+    const float two30 = 1073741824.0f;
+    const float sp30 = c.span * (1.0f / two30), inv30 = two30 / c.span;
+    const float fb30 = c.fw * two30, mb30 = c.min_w * two30;
+    int pw[K], ph[K];
+    nfk_prefix_nsf_lean<K>(wr, kL2E, c.m2b, fb30, mb30, pw);
+    nfk_prefix_nsf_lean<K>(hr, kL2E, c.m2b, fb30, mb30, ph);
+    const int xi = __float2int_rd(__builtin_fmaf(x, inv30, -c.lo * inv30));
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < K; ++j) k += (xi >= (INV ? ph[j] : pw[j])) ? 1 : 0;
+    float cw_k, w_k, ch_k, h_k;
+    nfk_lean_bin_edges<K>(pw, k, c, sp30, cw_k, w_k);
+    nfk_lean_bin_edges<K>(ph, k, c, sp30, ch_k, h_k);
+    // padded derivative index j+1 holds logit j (utils.py:36-39)
+    float raw_k = dr[0], raw_k1 = dr[0];
+#pragma unroll
+    for (int j = 1; j < K - 1; ++j) {
+        raw_k = (k >= j + 1) ? dr[j] : raw_k;
+        raw_k1 = (k >= j) ? dr[j] : raw_k1;
+    }
+    const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k, c.min_d);
+    const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1, c.min_d);
+    const float rw = nfk_rcp_fast(w_k);
+    const float delta = h_k * rw;
+    const float gap = (d_k + d_k1) - 2.0f * delta;
+    float th;
+    if (INV) {
+        const float y = x - ch_k;
+        const float qa = y * gap + h_k * (delta - d_k);
+        const float qb = h_k * d_k - y * gap;
+        const float qc = (-delta) * y;
+        const float disc = qb * qb - (4.0f * qa) * qc;
+        neg_disc = inside && !(disc >= 0.0f);
+        const float root = nfk_div_fast(2.0f * qc, -qb - sqrtf(disc));
+        out = root * w_k + cw_k;
+        th = root;
+    } else {
+        th = (x - cw_k) * rw;
+    }
+    const float t1mt = th * (1.0f - th);
+    const float den = delta + gap * t1mt;
+    if (!INV) {
+        const float num = h_k * (delta * (th * th) + d_k * t1mt);
+        out = ch_k + nfk_div_fast(num, den);
+    }
+    const float omt = 1.0f - th;
+    const float dnum = (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+    const float l = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
+    lad = inside ? (INV ? -l : l) : 0.0f;
+    out = inside ? out : x;
+}
