@@ -390,12 +390,21 @@ static bool lean_env() {
 // maps cover D = n_lo + n_up columns once each (a permutation of x's and z's
 // first D columns, as NSF_CL's are), and rows are 16-B aligned;
 // NFK_RQS_STREAM=0 in the environment selects k_rqs_coupling everywhere.
+static int g_rqs_form = -1;  // nfk_debug_rqs_form
 static bool stream_env() {
     static const bool on = [] {
         const char* e = std::getenv("NFK_RQS_STREAM");
         return !(e != nullptr && e[0] == '0');
     }();
-    return on;
+    return g_rqs_form < 0 ? on : g_rqs_form == 1;
+}
+
+// Diagnostic (not part of include/nfk.h): -1 = automatic, 0 = k_rqs_coupling
+// only, 1 = k_rqs_stream where it applies.  Returns the previous setting.
+extern "C" int nfk_debug_rqs_form(int form) {
+    const int prev = g_rqs_form;
+    g_rqs_form = form < 0 ? -1 : (form ? 1 : 0);
+    return prev;
 }
 
 template <int K, bool INV, bool PRE, bool DFULL>
