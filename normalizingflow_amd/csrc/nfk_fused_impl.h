@@ -25,6 +25,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #ifndef NFK_NSF_WPE_SPLIT
 #define NFK_NSF_WPE_SPLIT 3  // split form: workgroups per CU (waves per SIMD)
 #endif
+#ifndef NFK_GEMM_PF
+#define NFK_GEMM_PF 1  // gemm_h: prefetch the next tile pair's A fragments (register ring)
+#endif
 #ifndef NFK_SPLIT_PIPE
 #define NFK_SPLIT_PIPE 1  // split form: pipelined chunk schedule where it applies
 #endif
@@ -387,14 +390,20 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
         return (kb * NS + 2 * pr) * 2 + j;
     };
     float4 ring[2][4];
+    if constexpr (NFK_GEMM_PF) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-        if (2 * (0 % NPR) + (j >> 1) < NT) ring[0][j] = slot[blk(0, j) * 64 + lane];
+        for (int j = 0; j < 4; ++j)
+            if (2 * (0 % NPR) + (j >> 1) < NT) ring[0][j] = slot[blk(0, j) * 64 + lane];
+    }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const int kb = i / NPR, pr = i - kb * NPR, t0 = T0 + 2 * pr;
         const bool two = t0 + 1 < T0 + NT;
-        if (i + 1 < N) {
+        if constexpr (!NFK_GEMM_PF) {  // no prefetch: the pair's fragments just before its MFMAs
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (2 * pr + (j >> 1) < NT) ring[i & 1][j] = slot[blk(i, j) * 64 + lane];
+        } else if (i + 1 < N) {
             const int pn = (i + 1) % NPR;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
