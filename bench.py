@@ -261,7 +261,7 @@ def main():
         dom = max(summary.items(), key=lambda kv: kv[1][2])[0] if summary else None
         rl = roofline(args.workload, summary, B, load_traffic(dom, args.workload) if dom else None)
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             cpu = cpu_baseline(args.workload, {k: v.cpu() for k, v in sd.items()})
         desc = WORKLOADS[args.workload][0]
         out = {
