@@ -114,7 +114,7 @@ def cpu_baseline(workload, sd, budget_s=10.0):
                                                             torch.get_num_threads(), dt)}
 
 
-def roofline(workload, timer_summary, per_gpu_batch, traffic):
+def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
     """Roofline of the dominant kernel from live HIP-event timings."""
     if not timer_summary:
         return None
@@ -122,7 +122,9 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic):
     n = n_launch
     desc, kind, kw, D, L = WORKLOADS[workload]
     B = per_gpu_batch
-    if name == "nfk_fused_nsf":
+    if name in ("nfk_fused_nsf", "nfk_fused_nsf_chain"):
+        # layers per launch: all L of a step in one chain launch (or one per launch)
+        per = L * n_steps / n_launch if name == "nfk_fused_nsf_chain" else 1
         H = kw["hidden_dim"]
         n_lo = kw["size"]  # mask of one coordinate per particle (dim=2)
         n_up = kw["size"] * (kw["dim"] - 1)
@@ -134,7 +136,7 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic):
         tail = R if (0 < R <= 4 and kbf >= 1) else 0
         f32 = 2.0 * tail * (H + n_up * P)
         f16 = 2.0 * (n_lo * H + H * H + H * n_up * P) - f32
-        flops = (f16 + f32) * B                  # 173,600/sample (fp32-equivalent)
+        flops = (f16 + f32) * B * per            # 173,600/sample/layer (fp32-equivalent)
         # MFMA-time floor of this formulation at the dense peak of the MFMA each
         # part runs on, expressed as an fp32-equivalent TFLOP/s peak
         t_floor = f32 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * f16 / (PEAK_FP16_TFLOPS * 1e12)
@@ -144,7 +146,8 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic):
                 "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "launches": n, "mean_ms": round(mean_ms, 4),
-                "per_launch": "%d samples x %.0f flop (fp32-equivalent)" % (B, flops / B),
+                "per_launch": "%d samples x %g layers x %.0f flop (fp32-equivalent)"
+                              % (B, per, flops / B / per),
                 "peak_basis": "MFMA floor: %.0f flop/sample as 3 fp16 products (%.1f TF dense) + "
                               "%.0f flop/sample k-tail on f32 MFMA (%.1f TF)"
                               % (f16, PEAK_FP16_TFLOPS, f32, PEAK_FP32_TFLOPS),
@@ -209,6 +212,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timer", action="store_true", help="skip the per-kernel event timer")
     ap.add_argument("--unfused", action="store_true", help="disable the fused MFMA layer kernel")
+    ap.add_argument("--no-chain", action="store_true",
+                    help="one fused launch per layer instead of one chained launch per run of layers")
     args = ap.parse_args()
 
     from normalizingflow_amd import config, dist as nfdist, kernels
@@ -220,6 +225,7 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     config.USE_FUSED = not args.unfused
+    config.USE_CHAIN = not args.no_chain
 
     model, sd, _ = build_model(args.workload, device)
     B = args.batch
@@ -259,7 +265,8 @@ def main():
     if rank == 0:
         value = world * B * args.steps / dt
         dom = max(summary.items(), key=lambda kv: kv[1][2])[0] if summary else None
-        rl = roofline(args.workload, summary, B, load_traffic(dom, args.workload) if dom else None)
+        rl = roofline(args.workload, summary, B, load_traffic(dom, args.workload) if dom else None,
+                      args.steps)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             cpu = cpu_baseline(args.workload, {k: v.cpu() for k, v in sd.items()})
@@ -280,6 +287,7 @@ def main():
             "config": {"workload": args.workload + ": " + desc, "global_batch": world * B,
                        "per_gpu_batch": B, "parallelism": "dp%d (sample sharding)" % world,
                        "fused_layer_kernel": bool(config.USE_FUSED),
+                       "chained_layers": bool(config.USE_FUSED and config.USE_CHAIN),
                        "conditioner_arith": ARITH.get(args.workload) if config.USE_FUSED
                        else "f32 (rocBLAS)"},
             "roofline": rl,

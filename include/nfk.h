@@ -202,6 +202,33 @@ int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t
                   double tail_bound, int32_t inverse, int32_t* status, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Chain of fused NSF coupling layers in one launch: the layer loop of
+ * NormalizingFlowModel.forward/inverse (nf/models.py:13-29) over nlayers
+ * consecutive NSF_CL layers of one shape (n_lo, n_up, hidden, K, tail_bound)
+ * and one direction.  Each wave keeps its 16 x rows in LDS from the first
+ * layer to the last: HBM sees x once, z once and log|det| once per chain.
+ * Results are bitwise those of nlayers nfk_fused_nsf launches (log|det| is
+ * added layer by layer in the same order).
+ *   wpacks: DEVICE array of nlayers pack pointers (nfk_fused_nsf_pack), in
+ *           execution order.
+ *   cmaps:  DEVICE int32 [nlayers * D + D], D = n_lo + n_up: for layer l,
+ *           the tile columns of its lower inputs (n_lo) then of its upper
+ *           inputs (n_up) -- the layer's lo_in/up_in composed with the column
+ *           permutation of the layers before it (the tile keeps x's column
+ *           order; a layer overwrites its upper columns in place) -- then, for
+ *           every output column o of the last layer, the tile column holding it.
+ *   status: nlayers words, one per layer (bits as nfk_rqs_coupling).
+ * nlayers <= nfk_fused_nsf_chain_max() (0: shape not supported by the chain
+ * form); x, z 16-byte aligned with ldx, ldz multiples of 4.
+ * ------------------------------------------------------------------------- */
+int nfk_fused_nsf_chain_max(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K);
+int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* const* wpacks,
+                        const int32_t* cmaps, int32_t nlayers, int32_t n_lo, int32_t n_up,
+                        int32_t hidden, float* z, int64_t ldz, float* logdet,
+                        int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound,
+                        int32_t inverse, int32_t* status, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Fused RealNVP layer: both affine half-couplings with their four FCNN
  * conditioners (s1, t1, s2, t2) in one launch; replaces RealNVP.forward /
  * inverse (flows.py:44-76).  x, z: [batch, 2*half_dim] row-major.

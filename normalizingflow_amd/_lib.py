@@ -69,6 +69,12 @@ SIGNATURES = {
         P, P, I32, I32,                 # lo_in, lo_out, n_lo, hidden
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
         I64, I32, F64, I32, P, P]),     # batch, K, tail_bound, inverse, status, stream
+    "nfk_fused_nsf_chain_max": (ctypes.c_int, [I32, I32, I32, I32]),
+    "nfk_fused_nsf_chain": (ctypes.c_int, [
+        P, I64, P, P, I32,              # x, ldx, wpacks, cmaps, nlayers
+        I32, I32, I32,                  # n_lo, n_up, hidden
+        P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
+        I64, I32, F64, I32, P, P]),     # batch, K, tail_bound, inverse, status, stream
     "nfk_fused_realnvp_supported": (ctypes.c_int, [I32, I32]),
     "nfk_fused_realnvp_pack_elems": (ctypes.c_int64, [I32, I32]),
     "nfk_fused_realnvp_pack": (ctypes.c_int, [P, I32, I32, P, P]),

@@ -8,6 +8,10 @@ STRICT_CHECKS  raise the reference's data-dependent errors (RuntimeError when a
 USE_FUSED      run NSF_CL layers whose conditioner is the stock FCNN through the
                fused MFMA kernel (nfk_fused_nsf) when the shape is supported;
                otherwise conditioner GEMMs + the streaming spline kernel.
+USE_CHAIN      in inference, run consecutive fused NSF_CL layers of one shape as
+               one nfk_fused_nsf_chain launch (x resident in LDS across the
+               layers); results are bitwise those of the per-layer launches.
 """
 STRICT_CHECKS = True
 USE_FUSED = True
+USE_CHAIN = True

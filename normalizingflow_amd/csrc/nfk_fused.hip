@@ -412,20 +412,12 @@ extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float*
     return e == hipSuccess ? 0 : (int)e;
 }
 
-extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
-                             const int32_t* up_out, int32_t n_up, const int32_t* lo_in,
-                             const int32_t* lo_out, int32_t n_lo, int32_t hidden, float* z,
-                             int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
-                             int32_t K, double tail_bound, int32_t inverse, int32_t* status,
-                             nfk_stream_t stream) {
-    const bool narrow = shape_ok(n_lo, n_up, hidden, K);
-    if (!narrow && !wide_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
-    if (batch < 0) return nfk_set_error("nfk_fused_nsf: bad batch");
-    if (batch == 0) return 0;
-    if (!x || !wpack || !up_in || !up_out || !lo_in || !lo_out || !z)
-        return nfk_set_error("nfk_fused_nsf: null pointer");
-    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf: null logdet");
-    const Layout L = pack_layout(n_lo, n_up, hidden, K);
+namespace {
+// kernel arguments shared by nfk_fused_nsf and nfk_fused_nsf_chain
+FusedArgs fused_args(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
+                     const int32_t* up_out, const int32_t* lo_in, const int32_t* lo_out, const Layout& L,
+                     float* z, int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch, int32_t K,
+                     double tail_bound, int32_t* status) {
     FusedArgs a;
     a.trace = g_trace;
     a.x = x;
@@ -440,8 +432,8 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     a.ldx = ldx;
     a.ldz = ldz;
     a.batch = batch;
-    a.n_lo = n_lo;
-    a.n_up = n_up;
+    a.n_lo = L.n_lo;
+    a.n_up = L.n_up;
     a.KB1 = L.KB1;
     a.NCH = L.NCH;
     a.mode = logdet_mode;
@@ -456,6 +448,9 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     a.o_h1 = (int32_t)L.o_h1;
     a.o_h2 = (int32_t)L.o_h2;
     a.o_w3 = (int32_t)L.o_w3;
+    a.packs = nullptr;
+    a.cmaps = nullptr;
+    a.nlayers = 1;
     {
         // NSF_CL's spline constants (flows.py:236-237 defaults), evaluated like the
         // reference's Python scalars (nfk_make_const), folded for the fixed-point knots
@@ -472,6 +467,26 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
         a.c.min_d = sc.min_d;
         a.c.d_edge = sc.d_edge;
     }
+    return a;
+}
+}  // namespace
+
+extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
+                             const int32_t* up_out, int32_t n_up, const int32_t* lo_in,
+                             const int32_t* lo_out, int32_t n_lo, int32_t hidden, float* z,
+                             int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
+                             int32_t K, double tail_bound, int32_t inverse, int32_t* status,
+                             nfk_stream_t stream) {
+    const bool narrow = shape_ok(n_lo, n_up, hidden, K);
+    if (!narrow && !wide_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
+    if (batch < 0) return nfk_set_error("nfk_fused_nsf: bad batch");
+    if (batch == 0) return 0;
+    if (!x || !wpack || !up_in || !up_out || !lo_in || !lo_out || !z)
+        return nfk_set_error("nfk_fused_nsf: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf: null logdet");
+    const Layout L = pack_layout(n_lo, n_up, hidden, K);
+    FusedArgs a = fused_args(x, ldx, wpack, up_in, up_out, lo_in, lo_out, L, z, ldz, logdet, logdet_mode, batch,
+                             K, tail_bound, status);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
     if (!narrow) return launch_wide(a, L, K, inv, st);
@@ -490,10 +505,49 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     }
     const size_t lds = split ? lds_bytes_split(L) : lds_bytes(L);
 #define DISPATCH(h, t, k) \
-    if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, split, st);
+    if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, split, false, st);
 #define DISPATCH_KB(h, t) NFK_FUSED_K(DISPATCH, h, t)
     NFK_FUSED_KB(DISPATCH_KB)
 #undef DISPATCH_KB
 #undef DISPATCH
     return nfk_set_error("nfk_fused_nsf: no kernel instance");
+}
+
+extern "C" int nfk_fused_nsf_chain_max(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
+    if (!shape_ok(n_lo, n_up, hidden, K)) return 0;
+    return chain_max_layers(make_layout(n_lo, n_up, hidden, K));
+}
+
+extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* const* wpacks,
+                                   const int32_t* cmaps, int32_t nlayers, int32_t n_lo, int32_t n_up,
+                                   int32_t hidden, float* z, int64_t ldz, float* logdet,
+                                   int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound,
+                                   int32_t inverse, int32_t* status, nfk_stream_t stream) {
+    if (!shape_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_chain: shape not supported");
+    const Layout L = make_layout(n_lo, n_up, hidden, K);
+    const int nmax = chain_max_layers(L);
+    if (nlayers < 1 || nlayers > nmax) return nfk_set_error("nfk_fused_nsf_chain: bad layer count");
+    if (batch < 0) return nfk_set_error("nfk_fused_nsf_chain: bad batch");
+    if (batch == 0) return 0;
+    if (!x || !wpacks || !cmaps || !z) return nfk_set_error("nfk_fused_nsf_chain: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf_chain: null logdet");
+    if (((uintptr_t)x % 16) != 0 || ((uintptr_t)z % 16) != 0 || ldx % 4 != 0 || ldz % 4 != 0)
+        return nfk_set_error("nfk_fused_nsf_chain: x and z rows must be 16-byte aligned");
+    FusedArgs a = fused_args(x, ldx, nullptr, nullptr, nullptr, nullptr, nullptr, L, z, ldz, logdet, logdet_mode,
+                             batch, K, tail_bound, status);
+    a.slot_blocks = split_slot_blocks(L);
+    a.xtile = 16 * (n_lo + n_up + 1);
+    a.packs = wpacks;
+    a.cmaps = cmaps;
+    a.nlayers = nlayers;
+    const size_t lds = lds_bytes_chain(L, nlayers);
+    hipStream_t st = (hipStream_t)stream;
+    const bool inv = inverse != 0;
+#define DISPATCH(h, t, k) \
+    if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, true, true, st);
+#define DISPATCH_KB(h, t) NFK_FUSED_K(DISPATCH, h, t)
+    NFK_FUSED_KB(DISPATCH_KB)
+#undef DISPATCH_KB
+#undef DISPATCH
+    return nfk_set_error("nfk_fused_nsf_chain: no kernel instance");
 }

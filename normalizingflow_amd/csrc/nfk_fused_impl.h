@@ -191,10 +191,29 @@ inline size_t lds_bytes_split(const Layout& L) {
            (size_t)kNsfWaves * 16 * (D + 1) * sizeof(float) + (size_t)kNsfWaves * L.K * 64 * sizeof(int) +
            NFK_LDS_PAD;
 }
+// chain form: the maps region holds (nl + 1) D ints instead of 3 D
+inline size_t lds_bytes_chain(const Layout& L, int nl) {
+    const int D = L.n_lo + L.n_up;
+    return lds_bytes_split(L) - (size_t)((3 * D + 3) / 4) * 16 + (size_t)((4 * nl + (nl + 1) * D + 15) / 16) * 16;
+}
 // shape conditions of the split form (the launch also needs 16-B aligned x
 // and z rows: D, ldx, ldz multiples of 4)
 inline bool split_ok(const Layout& L) {
     return L.wide == 0 && (L.n_lo + L.n_up) % 4 == 0 && NFK_NSF_WPE_SPLIT * lds_bytes_split(L) <= (size_t)kLdsBytes;
+}
+
+// most layers one chain launch may hold with three workgroups per CU (status
+// bits ride one lane per layer: at most 64); 0 if the split form does not apply
+// (with LDS counted in 1280-byte allocation units, the coarsest granule
+// measured: a chain 32 B over a third of the CU's LDS lost its third
+// workgroup).  Map bytes limit D to 128 (kMaxD).
+constexpr size_t kLdsGranule = 1280;
+inline size_t lds_alloc(size_t b) { return (b + kLdsGranule - 1) / kLdsGranule * kLdsGranule; }
+inline int chain_max_layers(const Layout& L) {
+    if (!split_ok(L) || L.n_lo + L.n_up > 128) return 0;
+    int n = 0;
+    while (n < 64 && NFK_NSF_WPE_SPLIT * lds_alloc(lds_bytes_chain(L, n + 1)) <= (size_t)kLdsBytes) ++n;
+    return n;
 }
 
 // hidden feature computed by row i (0..15) of hidden tile t (>= H: padding)
@@ -228,6 +247,13 @@ struct FusedArgs {
     int32_t o_h1, o_h2, o_w3;  // float offsets into pack (< 2^31 by shape limits)
     FusedConst c;
     uint32_t* trace;  // diagnostic timeline buffer (NFK_TRACE builds), else unused
+    // chain form (k_fused_nsf<..., CHAIN = true>): nlayers layers of one shape in
+    // one launch, x rows resident in the LDS tile from the first layer to the last
+    const float* const* packs;  // device array: the packs of the layers, in execution order
+    const int32_t* cmaps;       // [nlayers][n_lo + n_up] tile columns (lower, then upper)
+                                // of every layer's inputs, then [D] the tile column of
+                                // every output column after the last layer
+    int32_t nlayers;
 };
 
 __device__ __forceinline__ f32x4 mfma32(float a, float b, f32x4 c) {
@@ -538,15 +564,15 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
 // Measured alternatives: two slots with one 8-wave
 // workgroup per CU, lockstep or ping-pong (4-6 % slower); a persistent form
 // prefetching the next tile's x into registers (no faster, SGPR spills).
-__device__ __forceinline__ void stage_phase(const FusedArgs& a, int p, int offA, int offB, int offC, float4* slot,
-                                            int wid, int lane) {
+__device__ __forceinline__ void stage_phase(const FusedArgs& a, const float* __restrict__ pack, int p, int offA,
+                                            int offB, int offC, float4* slot, int wid, int lane) {
     if (p == 0) {
-        stage_record<kNsfWaves>(a.pack + a.o_h1, a.blk_h1, slot, wid, lane);
+        stage_record<kNsfWaves>(pack + a.o_h1, a.blk_h1, slot, wid, lane);
     } else if (p == 1) {
-        stage_record<kNsfWaves>(a.pack + a.o_h2, a.blk_h2, slot, wid, lane);
+        stage_record<kNsfWaves>(pack + a.o_h2, a.blk_h2, slot, wid, lane);
     } else {
         const int ch = (p - 2) / 3, part = (p - 2) - 3 * ch;
-        const float* wc = a.pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
+        const float* wc = pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
         const int off = part == 0 ? offA : (part == 1 ? offB : offC);
         NFK_STAGE(wc + off * 256, part == 2 ? a.blk_d : a.blk_w, slot, wid, lane);
     }
@@ -592,22 +618,22 @@ __device__ __forceinline__ void stage_tiles(const float* __restrict__ rec, int n
 // sub-records, then per chunk NW searched-knot, NW other-knot and ND
 // derivative sub-records.
 template <int KBH, bool T1, int K, int HT>
-__device__ __forceinline__ void stage_split(const FusedArgs& a, int s, int offA, int offB, int offC, float4* slot,
-                                            int wid, int lane) {
+__device__ __forceinline__ void stage_split(const FusedArgs& a, const float* __restrict__ pack, int s, int offA,
+                                            int offB, int offC, float4* slot, int wid, int lane) {
     using S = NfkSplit<KBH, T1, K, HT>;
     if (s == 0) {
-        stage_record<kNsfWaves>(a.pack + a.o_h1, a.blk_h1, slot, wid, lane);
+        stage_record<kNsfWaves>(pack + a.o_h1, a.blk_h1, slot, wid, lane);
         return;
     }
     if (s <= S::NH2) {
-        stage_tiles<KBH, T1, S::NS>(a.pack + a.o_h2, HT, (s - 1) * S::NS, slot, wid, lane);
+        stage_tiles<KBH, T1, S::NS>(pack + a.o_h2, HT, (s - 1) * S::NS, slot, wid, lane);
         return;
     }
 #ifdef NFK_ABL_NOSTAGE
     return;  // diagnostic: chunk-loop sub-records never copied
 #endif
     const int u = s - 1 - S::NH2, ch = u / S::SPC, v = u - ch * S::SPC;
-    const float* wc = a.pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
+    const float* wc = pack + a.o_w3 + (int64_t)ch * a.blk_chunk * 256;
     if (v < S::NW)
         stage_tiles<KBH, T1, S::NS>(wc + offA * 256, K, v * S::NS, slot, wid, lane);
     else if (v < 2 * S::NW)
@@ -633,8 +659,20 @@ __device__ __forceinline__ void gemm_parts(const h8 (&bh)[KBH], const h8 (&bl)[K
 #define NFK_NSF_WPE 2  // waves per SIMD the register budget is sized for
 #endif
 
-template <int KBH, bool T1, int K, bool INV, bool SPLIT>
+// CHAIN (split form only): a.nlayers layers in one launch.  The wave's x rows
+// stay in its LDS tile from the first layer to the last (layer l reads and
+// overwrites the tile columns a.cmaps gives it), log|det| is carried in a
+// register and the status bits in LDS words, and the layer-1 record of layer l + 1 is copied
+// during the last epilogue of layer l: one prologue and one tail per chain.
+template <int KBH, bool T1, int K, bool INV, bool SPLIT, bool CHAIN = false>
 __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF_WPE) void k_fused_nsf(FusedArgs a) {
+    static_assert(SPLIT || !CHAIN, "the chain form is a split-form kernel");
+    // the arguments through a pointer the chain form re-derives opaquely at
+    // every layer, so values loaded from them are not hoisted out of the layer
+    // loop (kept live across it, they spilled)
+    using ArgsK = const __attribute__((address_space(4))) FusedArgs;
+    ArgsK* A = (ArgsK*)__builtin_amdgcn_kernarg_segment_ptr();  // a is the only argument: offset 0
+    (void)a;
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
     constexpr int DN = K - 1 > 0 ? K - 1 : 1;
     using SP = NfkSplit<KBH, T1, K, HT>;
@@ -643,32 +681,47 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4, sl = lane & 15;
-    const int D = a.n_lo + a.n_up;
+    const int D = A->n_lo + A->n_up;
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
     float4* slot = lds4;
-    int32_t* m_up_in = reinterpret_cast<int32_t*>(lds4 + a.slot_blocks * 64);
-    int32_t* m_up_out = m_up_in + a.n_up;
-    int32_t* m_lo_in = m_up_out + a.n_up;
-    int32_t* m_lo_out = m_lo_in + a.n_lo;
-    int32_t* m_src = m_lo_out + a.n_lo;  // split form: input column of each output column
-    const int XL = 32 * a.KB1;  // lower-x tile row length (n_lo padded to the k-blocks)
-    const int XU = a.xup;       // upper-x tile row length (n_up padded to 4)
+    const int NL = CHAIN ? A->nlayers : 1;
+    int32_t* m_up_in = reinterpret_cast<int32_t*>(lds4 + A->slot_blocks * 64);
+    int32_t* m_up_out = m_up_in + A->n_up;
+    int32_t* m_lo_in = m_up_out + A->n_up;
+    int32_t* m_lo_out = m_lo_in + A->n_lo;
+    int32_t* m_src = m_lo_out + A->n_lo;  // split form: input column of each output column
+    // chain form: the maps region holds the status word of each layer (OR-ed
+    // by the waves), then A->cmaps as bytes ((NL + 1) D, D <= 128): small
+    // enough that three workgroups still share a CU
+    int32_t* const cst = reinterpret_cast<int32_t*>(lds4 + A->slot_blocks * 64);
+    uint8_t* const cm = reinterpret_cast<uint8_t*>(cst + NL);
+    const uint8_t* c_lo = cm;  // this layer's lower / upper input columns
+    const uint8_t* c_up = cm;
+    const uint8_t* const c_src = cm + NL * (A->n_lo + A->n_up);
+    // maps by index, in either form
+    auto lo_map = [&](int k) { return CHAIN ? (int)c_lo[k] : m_lo_in[k]; };
+    auto up_map = [&](int j) { return CHAIN ? (int)c_up[j] : m_up_in[j]; };
+    auto src_map = [&](int o) { return CHAIN ? (int)c_src[o] : m_src[o]; };
+    const int XL = 32 * A->KB1;  // lower-x tile row length (n_lo padded to the k-blocks)
+    const int XU = A->xup;       // upper-x tile row length (n_up padded to 4)
     // split form: xlo is this wave's [16][XS] tile of whole x rows (input column
     // order, row stride XS = D + 1); the spline writes z's upper values over the
     // x values they replace
     const int XS = D + 1;
-    float* xlo = reinterpret_cast<float*>(lds4 + a.slot_blocks * 64 + (SPLIT ? 3 * D + 3 : 2 * D + 3) / 4) +
-                 wid * a.xtile;
+    float* xlo = reinterpret_cast<float*>(lds4 + A->slot_blocks * 64 +
+                                          (CHAIN ? (4 * NL + (NL + 1) * D + 15) / 16
+                                                 : (SPLIT ? 3 * D + 3 : 2 * D + 3) / 4)) +
+                 wid * A->xtile;
     float* xup = xlo + 16 * XL;
     // this wave's bin lookup table: K + 1 rows of 64 lanes, after all x tiles
-    int* scr = reinterpret_cast<int*>(xlo + (kNsfWaves - wid) * a.xtile) + wid * K * 64;
-    const FusedConst& c = a.c;
-    const float* pk = a.pack;
-    const int NP = 2 + 3 * a.NCH;
+    int* scr = reinterpret_cast<int*>(xlo + (kNsfWaves - wid) * A->xtile) + wid * K * 64;
+    const float* pk = CHAIN ? A->packs[0] : A->pack;  // this layer's pack
+    int lyr = 0;                                    // chain: the layer running
+    const int NP = 2 + 3 * A->NCH;
     // execution order of the three records of a chunk: searched knots, other knots, derivatives
-    const int offA = INV ? a.blk_w : 0, offB = INV ? 0 : a.blk_w, offC = 2 * a.blk_w;
+    const int offA = INV ? A->blk_w : 0, offB = INV ? 0 : A->blk_w, offC = 2 * A->blk_w;
     const int64_t b0 = ((int64_t)blockIdx.x * kNsfWaves + wid) * 16;
-    const int64_t rem = a.batch - b0;
+    const int64_t rem = A->batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const bool row_ok = sl < nrows;
     h8 bh[KBH], bl[KBH];  // B operands (activations) of the current product
@@ -681,7 +734,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     // sub-records.  gemm_end ends a GEMM (part): LDS reads retired, barrier,
     // the next sub-record's copy issued; inside a split record it also waits
     // for that copy.  epi_end ends an epilogue: the copy has landed, barrier.
-    const int NSR = SPLIT ? 1 + SP::NH2 + a.NCH * SP::SPC : NP;
+    const int NSR = SPLIT ? 1 + SP::NH2 + A->NCH * SP::SPC : NP;
     int sr = 0;
     auto gemm_end = [&](bool last) {
         NFK_MARK(tr);  // GEMM issued
@@ -691,9 +744,13 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
         NFK_MARK(tr);  // barrier passed
         if (sr + 1 < NSR) {
             if constexpr (SPLIT)
-                stage_split<KBH, T1, K, HT>(a, sr + 1, offA, offB, offC, slot, wid, lane);
+                stage_split<KBH, T1, K, HT>(a, pk, sr + 1, offA, offB, offC, slot, wid, lane);
             else
-                stage_phase(a, sr + 1, offA, offB, offC, slot, wid, lane);
+                stage_phase(a, pk, sr + 1, offA, offB, offC, slot, wid, lane);
+        } else if (CHAIN && lyr + 1 < NL) {
+            // the next layer's layer-1 record (its pack pointer loaded here: no
+            // register carries it through the layer)
+            stage_split<KBH, T1, K, HT>(a, A->packs[lyr + 1], 0, offA, offB, offC, slot, wid, lane);
         }
         ++sr;
         if (!last) {
@@ -733,313 +790,353 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
             // stride XS = D + 1, so the per-sample reads below are bank-conflict free
             const uint32_t base = lds_addr(xlo);
             for (int r = 0; r < 16; ++r) {
-                const float* src = a.x + (b0 + (r < nrows ? r : 0)) * a.ldx;
+                const float* src = A->x + (b0 + (r < nrows ? r : 0)) * A->ldx;
                 for (int c0 = 0; c0 < D; c0 += 64)
                     if (c0 + lane < D) dma4(src + c0 + lane, base + (r * XS + c0) * 4);
             }
         }
-        stage_phase(a, 0, offA, offB, offC, slot, wid, lane);
-        for (int i = threadIdx.x; i < a.n_up; i += 64 * kNsfWaves) {
-            const int ui = a.up_in[i], uo = a.up_out[i];
-            m_up_in[i] = ui;
-            m_up_out[i] = uo;
-            m_src[uo] = ui;
-        }
-        for (int i = threadIdx.x; i < a.n_lo; i += 64 * kNsfWaves) {
-            const int li = a.lo_in[i], lo = a.lo_out[i];
-            m_lo_in[i] = li;
-            m_lo_out[i] = lo;
-            m_src[lo] = li;
+        stage_phase(a, pk, 0, offA, offB, offC, slot, wid, lane);
+        if constexpr (CHAIN) {
+            for (int i = threadIdx.x; i < (NL + 1) * D; i += 64 * kNsfWaves) cm[i] = (uint8_t)A->cmaps[i];
+            if ((int)threadIdx.x < NL) cst[threadIdx.x] = 0;
+        } else {
+            for (int i = threadIdx.x; i < A->n_up; i += 64 * kNsfWaves) {
+                const int ui = A->up_in[i], uo = A->up_out[i];
+                m_up_in[i] = ui;
+                m_up_out[i] = uo;
+                m_src[uo] = ui;
+            }
+            for (int i = threadIdx.x; i < A->n_lo; i += 64 * kNsfWaves) {
+                const int li = A->lo_in[i], lo = A->lo_out[i];
+                m_lo_in[i] = li;
+                m_lo_out[i] = lo;
+                m_src[lo] = li;
+            }
         }
     } else {
-        for (int i = threadIdx.x; i < a.n_up; i += 64 * kNsfWaves) {
-            m_up_in[i] = a.up_in[i];
-            m_up_out[i] = a.up_out[i];
+        for (int i = threadIdx.x; i < A->n_up; i += 64 * kNsfWaves) {
+            m_up_in[i] = A->up_in[i];
+            m_up_out[i] = A->up_out[i];
         }
-        for (int i = threadIdx.x; i < a.n_lo; i += 64 * kNsfWaves) {
-            m_lo_in[i] = a.lo_in[i];
-            m_lo_out[i] = a.lo_out[i];
+        for (int i = threadIdx.x; i < A->n_lo; i += 64 * kNsfWaves) {
+            m_lo_in[i] = A->lo_in[i];
+            m_lo_out[i] = A->lo_out[i];
         }
     }
-    const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
-    const int st_prev = (a.status != nullptr && lane == 0) ? a.status[0] : 0;
-    const float ld_prev = (q == 0 && row_ok && a.mode == 2) ? a.logdet[b0 + sl] : 0.0f;
+    // status words: lane l holds layer l's (chain form: one per layer)
+    // (chain form: read in the tail instead, where it costs no register
+    // across the layer loop)
+    int st_prev = (!CHAIN && A->status != nullptr && lane == 0) ? A->status[0] : 0;
+    const float ld_prev = (q == 0 && row_ok && A->mode == 2) ? A->logdet[b0 + sl] : 0.0f;
     // split form: this lane's layer-1 columns of k-block 0 (8q + j), read from
     // the global map now so the first operand reads need no map round trip
+    // (chain form: from the LDS maps, per layer)
     int lo_c0[8];
-    if constexpr (SPLIT) {
+    if constexpr (SPLIT && !CHAIN) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) lo_c0[j] = (8 * q + j < a.n_lo) ? a.lo_in[8 * q + j] : -1;
+        for (int j = 0; j < 8; ++j) lo_c0[j] = (8 * q + j < A->n_lo) ? A->lo_in[8 * q + j] : -1;
     }
     if constexpr (!SPLIT) {
         __syncthreads();  // maps visible (no DMA in flight yet)
-        stage_phase(a, 0, offA, offB, offC, slot, wid, lane);
-        if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_lo_in, a.n_lo, XL, xlo, lane);
-        if (nrows > 0) gather_x(a.x, a.ldx, b0, nrows, m_up_in, a.n_up, XU, xup, lane);
+        stage_phase(a, pk, 0, offA, offB, offC, slot, wid, lane);
+        if (nrows > 0) gather_x(A->x, A->ldx, b0, nrows, m_lo_in, A->n_lo, XL, xlo, lane);
+        if (nrows > 0) gather_x(A->x, A->ldx, b0, nrows, m_up_in, A->n_up, XU, xup, lane);
     }
     dma_barrier();
     NFK_MARK(tr);  // prologue done
 
-    bool any_in = false, any_nd = false;
-
-    // layer-1 B operand of k-block kb: lower coordinates 32 kb + 8 q .. + 7 of
-    // sample sl (zero past n_lo in the split form; the whole form's padding
-    // columns hold a valid x, their weights are zero)
-    auto x_operand = [&](int kb, float4& u, float4& v) {
-        if constexpr (SPLIT) {
-            float e[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = 32 * kb + 8 * q + j;
-                const int col = kb == 0 ? lo_c0[j] : (k < a.n_lo ? m_lo_in[k] : -1);
-                e[j] = col >= 0 ? xlo[sl * XS + col] : 0.0f;
-            }
-            u = make_float4(e[0], e[1], e[2], e[3]);
-            v = make_float4(e[4], e[5], e[6], e[7]);
-        } else {
-            const float4* xr = reinterpret_cast<const float4*>(xlo + sl * XL + 32 * kb + 8 * q);
-            u = xr[0], v = xr[1];
-        }
-    };
-    // tile position of upper coordinate j of sample sl
-    auto up_pos = [&](int j) { return SPLIT ? sl * XS + m_up_in[j] : sl * XU + j; };
-
-    // ---- phase 0: layer 1, fp16 split.  x has any magnitude, so each
-    // wave scales its tile by a power of two 2^sx that puts max|x| just under
-    // 2^14 before the split; acc = 2^(s1+sx) W1 x.
-    f32x4 h1[HT];
-    float unx;
-    {
-        float mx = 0.0f;
-        float4 u0, v0;  // k-block 0's operand, read once
-        for (int kb = 0; kb < a.KB1; ++kb) {
-            float4 u, v;
-            x_operand(kb, u, v);
-            if (kb == 0) u0 = u, v0 = v;
-            mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))),
-                                 fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-        int ex = 0;
-        if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
-        const float sx = ldexpf(1.0f, 14 - ex);
-        unx = ldexpf(un1, ex - 14);
-        // accumulators start at b1 2^(s1+sx) (exact power-of-two scaling), so the
-        // epilogue only multiplies by 2^-(s1+sx): the bias is read in this GEMM
-        // half, before the slot is recycled
-        const float4* s = slot;
-        const float4* bias = s + a.KB1 * HT * 2 * 64;
-        const float bsc = ldexpf(1.0f, 14 - ex) / un1;
-#pragma unroll
-        for (int t = 0; t < HT; ++t) {
-            const float4 bv = bias[t * 4 + q];
-            h1[t] = f32x4{bv.x * bsc, bv.y * bsc, bv.z * bsc, bv.w * bsc};
-        }
-        for (int kb = 0; kb < a.KB1; ++kb) {
-            float4 u = u0, v = v0;
-            if (kb > 0) x_operand(kb, u, v);
-            const float xv8[8] = {u.x * sx, u.y * sx, u.z * sx, u.w * sx, v.x * sx, v.y * sx, v.z * sx, v.w * sx};
-            h8 xh, xl8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const _Float16 hh = (_Float16)xv8[j];
-                xh[j] = hh;
-                xl8[j] = (_Float16)(xv8[j] - (float)hh);
-            }
-#pragma unroll
-            for (int t = 0; t < HT; ++t) {
-                const h8 ahi = __builtin_bit_cast(h8, s[((kb * HT + t) * 2) * 64 + lane]);
-                const h8 alo = __builtin_bit_cast(h8, s[((kb * HT + t) * 2 + 1) * 64 + lane]);
-                h1[t] = mfma16(alo, xh, h1[t]);
-                h1[t] = mfma16(ahi, xl8, h1[t]);
-                h1[t] = mfma16(ahi, xh, h1[t]);
-            }
-        }
+    // log|det| of this lane's sample (lane group 0): the stored value (mode 2)
+    // plus the layer sums one by one, the order of a launch per layer
+    float ld_acc = ld_prev;
+    uint64_t st_bits = 0;  // status bits (chain form: per layer in the LDS words cst)
+    for (int l = 0; l < NL; ++l) {
+    if constexpr (CHAIN) {
+        asm volatile("" : "+s"(A));
+        lyr = l;
+        pk = A->packs[l];
+        c_lo = cm + l * D;
+        c_up = c_lo + A->n_lo;
+        sr = 0;
     }
-    gemm_end(true);
-    // epilogue 0: tanh of acc 2^-(s1+sx), split -> layer-2 operands
-    act_operands<KBH, T1, HT>(h1, -2.0f * kL2E * unx, bh, bl, btail);
-    epi_end();
-    // ---- phase 1: layer 2, fp16 split: h2^T = tanh(W2 . h1^T + b2)
-    {
-        f32x4 h2[HT];
-        gemm_rec(h2);
-        act_operands<KBH, T1, HT>(h2, -2.0f * kL2E * un2, bh, bl, btail);
-    }
-    epi_end();
+    const FusedConst& c = *(const FusedConst*)&A->c;  // (per layer: see A)
+    const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
+        bool any_in = false, any_nd = false;
 
-    const float l2e3 = kL2E * un3;
-    float ldsum = 0.0f;
-    // per-coordinate state of the chunk: lane group q holds coordinates
-    // jbase + 4q + r, r = 0..3, of sample sl
-    int jj4[4];
-    float xv[4];
-    int kb[4];
-    float cw_k[4], w_k[4], ch_k[4], h_k[4];
-    // epilogue A (searched knots: widths forward / heights inverse) for r in [R0, R1)
-    auto epi_a = [&](const f32x4(&acc)[K], int jbase, auto r0c, auto r1c) {
-        constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
-#pragma unroll
-        for (int r = R0; r < R1; ++r) {
-            jj4[r] = jbase + 4 * q + r;
-            xv[r] = (jj4[r] < a.n_up) ? (SPLIT ? xlo : xup)[up_pos(jj4[r])] : 0.0f;
-        }
-        knot_phase<K, true, R0, R1>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
-    };
-    // epilogue B: the other knots, selected at the bin
-    auto epi_b = [&](const f32x4(&acc)[K], auto r0c, auto r1c) {
-        constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
-        knot_phase<K, false, R0, R1>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
-    };
-    // epilogue C: derivatives of the bin, evaluate, log|det|
-    auto epi_c = [&](const f32x4(&accd)[DN], auto r0c, auto r1c) {
-        constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
-#ifdef NFK_ABL_NOEPI
-#pragma unroll
-        for (int r = R0; r < R1; ++r) {
-            float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
-#pragma unroll
-            for (int t = 0; t < DN; ++t) v += accd[t][r];
-            if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = v;
-            ldsum += v;
-            any_in = true;
-        }
-        if (false)
-#endif
-#pragma unroll
-        for (int r = R0; r < R1; ++r) {
-            // padded derivative index j+1 holds logit j (utils.py:36-39):
-            // raw_k = logit k-1, raw_k1 = logit k
-            const int k = kb[r];
-            float raw_k = accd[0][r], raw_k1 = accd[0][r];
-            if (NFK_LUT) {
-                // row j = logit j; raw_k is unused at k = 0, raw_k1 at k = K - 1
-                float* fs = reinterpret_cast<float*>(scr);
-#pragma unroll
-                for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[j][r];
-                raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
-                raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
+        // layer-1 B operand of k-block kb: lower coordinates 32 kb + 8 q .. + 7 of
+        // sample sl (zero past n_lo in the split form; the whole form's padding
+        // columns hold a valid x, their weights are zero)
+        auto x_operand = [&](int kb, float4& u, float4& v) {
+            if constexpr (SPLIT) {
+                float e[8];
+    #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = 32 * kb + 8 * q + j;
+                    const int col = (kb == 0 && !CHAIN) ? lo_c0[j] : (k < A->n_lo ? lo_map(k) : -1);
+                    e[j] = col >= 0 ? xlo[sl * XS + col] : 0.0f;
+                }
+                u = make_float4(e[0], e[1], e[2], e[3]);
+                v = make_float4(e[4], e[5], e[6], e[7]);
             } else {
-#pragma unroll
-                for (int j = 1; j < K - 1; ++j) {
-                    raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
-                    raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
+                const float4* xr = reinterpret_cast<const float4*>(xlo + sl * XL + 32 * kb + 8 * q);
+                u = xr[0], v = xr[1];
+            }
+        };
+        // tile position of upper coordinate j of sample sl
+        auto up_pos = [&](int j) { return SPLIT ? sl * XS + up_map(j) : sl * XU + j; };
+
+        // ---- phase 0: layer 1, fp16 split.  x has any magnitude, so each
+        // wave scales its tile by a power of two 2^sx that puts max|x| just under
+        // 2^14 before the split; acc = 2^(s1+sx) W1 x.
+        f32x4 h1[HT];
+        float unx;
+        {
+            float mx = 0.0f;
+            float4 u0, v0;  // k-block 0's operand, read once
+            for (int kb = 0; kb < A->KB1; ++kb) {
+                float4 u, v;
+                x_operand(kb, u, v);
+                if (kb == 0) u0 = u, v0 = v;
+                mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))),
+                                     fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
+            }
+    #pragma unroll
+            for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+            int ex = 0;
+            if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
+            const float sx = ldexpf(1.0f, 14 - ex);
+            unx = ldexpf(un1, ex - 14);
+            // accumulators start at b1 2^(s1+sx) (exact power-of-two scaling), so the
+            // epilogue only multiplies by 2^-(s1+sx): the bias is read in this GEMM
+            // half, before the slot is recycled
+            const float4* s = slot;
+            const float4* bias = s + A->KB1 * HT * 2 * 64;
+            const float bsc = ldexpf(1.0f, 14 - ex) / un1;
+    #pragma unroll
+            for (int t = 0; t < HT; ++t) {
+                const float4 bv = bias[t * 4 + q];
+                h1[t] = f32x4{bv.x * bsc, bv.y * bsc, bv.z * bsc, bv.w * bsc};
+            }
+            for (int kb = 0; kb < A->KB1; ++kb) {
+                float4 u = u0, v = v0;
+                if (kb > 0) x_operand(kb, u, v);
+                const float xv8[8] = {u.x * sx, u.y * sx, u.z * sx, u.w * sx, v.x * sx, v.y * sx, v.z * sx, v.w * sx};
+                h8 xh, xl8;
+    #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const _Float16 hh = (_Float16)xv8[j];
+                    xh[j] = hh;
+                    xl8[j] = (_Float16)(xv8[j] - (float)hh);
+                }
+    #pragma unroll
+                for (int t = 0; t < HT; ++t) {
+                    const h8 ahi = __builtin_bit_cast(h8, s[((kb * HT + t) * 2) * 64 + lane]);
+                    const h8 alo = __builtin_bit_cast(h8, s[((kb * HT + t) * 2 + 1) * 64 + lane]);
+                    h1[t] = mfma16(alo, xh, h1[t]);
+                    h1[t] = mfma16(ahi, xl8, h1[t]);
+                    h1[t] = mfma16(ahi, xh, h1[t]);
                 }
             }
-            // d = min_d + softplus(softplus(D)) (flows.py:235, utils.py:82), only
-            // at the two knots the bin uses; the padded ends are the constant d_edge
-            // both evaluated, then selected: as a conditional the compiler
-            // branches around the exp/log under an exec mask
-            const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
-            const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
-            const float d_k = (k == 0) ? c.d_edge : dv_k;
-            const float d_k1 = (k == K - 1) ? c.d_edge : dv_k1;
-            const float x = xv[r];
-            // one reciprocal of the bin width for delta and theta
-            const float rw = nfk_rcp_fast(w_k[r]);
-            const float delta = h_k[r] * rw;
-            const float gap = (d_k + d_k1) - 2.0f * delta;
-            float out, th;
-            bool nd = false;
-            if (INV) {
-                const float y = x - ch_k[r];
-                const float qa = y * gap + h_k[r] * (delta - d_k);
-                const float qb = h_k[r] * d_k - y * gap;
-                const float qc = (-delta) * y;
-                const float disc = qb * qb - (4.0f * qa) * qc;
-                nd = !(disc >= 0.0f);
-                const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
-                out = root * w_k[r] + cw_k[r];
-                th = root;
-            } else {
-                th = (x - cw_k[r]) * rw;
-            }
-            const float t1mt = th * (1.0f - th);
-            const float den = delta + gap * t1mt;
-            if (!INV) {
-                const float num = h_k[r] * (delta * (th * th) + d_k * t1mt);
-                out = ch_k[r] + nfk_div<true>(num, den);
-            }
-            const float omt = 1.0f - th;
-            const float dnum =
-                (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
-            float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
-            lad = INV ? -lad : lad;
-            const bool inside = (x >= c.lo) && (x <= c.hi);
-            const bool live = jj4[r] < a.n_up && row_ok;
-            out = inside ? out : x;
-            if (jj4[r] < a.n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = out;  // z collected in the tile
-            ldsum += (inside && live) ? lad : 0.0f;
-            any_in |= inside && live;
-            any_nd |= nd && inside && live;
         }
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I2 = std::integral_constant<int, 2>;
-    using I4 = std::integral_constant<int, 4>;
+        gemm_end(true);
+        // epilogue 0: tanh of acc 2^-(s1+sx), split -> layer-2 operands
+        act_operands<KBH, T1, HT>(h1, -2.0f * kL2E * unx, bh, bl, btail);
+        epi_end();
+        // ---- phase 1: layer 2, fp16 split: h2^T = tanh(W2 . h1^T + b2)
+        {
+            f32x4 h2[HT];
+            gemm_rec(h2);
+            act_operands<KBH, T1, HT>(h2, -2.0f * kL2E * un2, bh, bl, btail);
+        }
+        epi_end();
 
-    if constexpr (PIPE) {
-        // Pipelined split schedule (two sub-records per record): the copy of a
-        // record's second sub-record is covered by half (two coordinates) of
-        // the previous phase's epilogue, the copy of the next record's first
-        // sub-record by the other half.  Each phase's accumulators stay live
-        // through the first GEMM part of the next phase.
-        constexpr int NSP = SP::NS;
-        f32x4 accd[DN];
-        for (int ch = 0; ch < a.NCH; ++ch) {
-            const int jbase = 16 * ch;
-            f32x4 accA[K], accB[K];
-            gemm_h<KBH, T1, NSP, NSP, 0, K>(bh, bl, btail, slot, lane, accA);
-            gemm_end(true);
-            if (ch > 0) epi_c(accd, I2{}, I4{});  // previous chunk, coordinates 2, 3
-            epi_end();
-            gemm_h<KBH, T1, K - NSP, NSP, NSP, K>(bh, bl, btail, slot, lane, accA);
-            gemm_end(true);
-            epi_a(accA, jbase, I0{}, I2{});
-            epi_end();
-            gemm_h<KBH, T1, NSP, NSP, 0, K>(bh, bl, btail, slot, lane, accB);
-            gemm_end(true);
-            epi_a(accA, jbase, I2{}, I4{});
-            epi_end();
-            gemm_h<KBH, T1, K - NSP, NSP, NSP, K>(bh, bl, btail, slot, lane, accB);
-            gemm_end(true);
-            epi_b(accB, I0{}, I2{});
-            epi_end();
-            gemm_h<KBH, T1, NSP, NSP, 0, DN>(bh, bl, btail, slot, lane, accd);
-            gemm_end(true);
-            epi_b(accB, I2{}, I4{});
-            epi_end();
-            gemm_h<KBH, T1, DN - NSP, NSP, NSP, DN>(bh, bl, btail, slot, lane, accd);
-            gemm_end(true);
-            epi_c(accd, I0{}, I2{});
-            epi_end();
+        const float l2e3 = kL2E * un3;
+        float ldsum = 0.0f;
+        // per-coordinate state of the chunk: lane group q holds coordinates
+        // jbase + 4q + r, r = 0..3, of sample sl
+        int jj4[4];
+        float xv[4];
+        int kb[4];
+        float cw_k[4], w_k[4], ch_k[4], h_k[4];
+        // epilogue A (searched knots: widths forward / heights inverse) for r in [R0, R1)
+        auto epi_a = [&](const f32x4(&acc)[K], int jbase, auto r0c, auto r1c) {
+            constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
+    #pragma unroll
+            for (int r = R0; r < R1; ++r) {
+                jj4[r] = jbase + 4 * q + r;
+                xv[r] = (jj4[r] < A->n_up) ? (SPLIT ? xlo : xup)[up_pos(jj4[r])] : 0.0f;
+            }
+            knot_phase<K, true, R0, R1>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
+        };
+        // epilogue B: the other knots, selected at the bin
+        auto epi_b = [&](const f32x4(&acc)[K], auto r0c, auto r1c) {
+            constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
+            knot_phase<K, false, R0, R1>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
+        };
+        // epilogue C: derivatives of the bin, evaluate, log|det|
+        auto epi_c = [&](const f32x4(&accd)[DN], auto r0c, auto r1c) {
+            constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
+    #ifdef NFK_ABL_NOEPI
+    #pragma unroll
+            for (int r = R0; r < R1; ++r) {
+                float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
+    #pragma unroll
+                for (int t = 0; t < DN; ++t) v += accd[t][r];
+                if (jj4[r] < A->n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = v;
+                ldsum += v;
+                any_in = true;
+            }
+            if (false)
+    #endif
+    #pragma unroll
+            for (int r = R0; r < R1; ++r) {
+                // padded derivative index j+1 holds logit j (utils.py:36-39):
+                // raw_k = logit k-1, raw_k1 = logit k
+                const int k = kb[r];
+                float raw_k = accd[0][r], raw_k1 = accd[0][r];
+                if (NFK_LUT) {
+                    // row j = logit j; raw_k is unused at k = 0, raw_k1 at k = K - 1
+                    float* fs = reinterpret_cast<float*>(scr);
+    #pragma unroll
+                    for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[j][r];
+                    raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
+                    raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
+                } else {
+    #pragma unroll
+                    for (int j = 1; j < K - 1; ++j) {
+                        raw_k = (k >= j + 1) ? accd[j][r] : raw_k;
+                        raw_k1 = (k >= j) ? accd[j][r] : raw_k1;
+                    }
+                }
+                // d = min_d + softplus(softplus(D)) (flows.py:235, utils.py:82), only
+                // at the two knots the bin uses; the padded ends are the constant d_edge
+                // both evaluated, then selected: as a conditional the compiler
+                // branches around the exp/log under an exec mask
+                const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
+                const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
+                const float d_k = (k == 0) ? c.d_edge : dv_k;
+                const float d_k1 = (k == K - 1) ? c.d_edge : dv_k1;
+                const float x = xv[r];
+                // one reciprocal of the bin width for delta and theta
+                const float rw = nfk_rcp_fast(w_k[r]);
+                const float delta = h_k[r] * rw;
+                const float gap = (d_k + d_k1) - 2.0f * delta;
+                float out, th;
+                bool nd = false;
+                if (INV) {
+                    const float y = x - ch_k[r];
+                    const float qa = y * gap + h_k[r] * (delta - d_k);
+                    const float qb = h_k[r] * d_k - y * gap;
+                    const float qc = (-delta) * y;
+                    const float disc = qb * qb - (4.0f * qa) * qc;
+                    nd = !(disc >= 0.0f);
+                    const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
+                    out = root * w_k[r] + cw_k[r];
+                    th = root;
+                } else {
+                    th = (x - cw_k[r]) * rw;
+                }
+                const float t1mt = th * (1.0f - th);
+                const float den = delta + gap * t1mt;
+                if (!INV) {
+                    const float num = h_k[r] * (delta * (th * th) + d_k * t1mt);
+                    out = ch_k[r] + nfk_div<true>(num, den);
+                }
+                const float omt = 1.0f - th;
+                const float dnum =
+                    (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+                float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
+                lad = INV ? -lad : lad;
+                const bool inside = (x >= c.lo) && (x <= c.hi);
+                const bool live = jj4[r] < A->n_up && row_ok;
+                out = inside ? out : x;
+                if (jj4[r] < A->n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = out;  // z collected in the tile
+                ldsum += (inside && live) ? lad : 0.0f;
+                any_in |= inside && live;
+                any_nd |= nd && inside && live;
+            }
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I2 = std::integral_constant<int, 2>;
+        using I4 = std::integral_constant<int, 4>;
+
+        if constexpr (PIPE) {
+            // Pipelined split schedule (two sub-records per record): the copy of a
+            // record's second sub-record is covered by half (two coordinates) of
+            // the previous phase's epilogue, the copy of the next record's first
+            // sub-record by the other half.  Each phase's accumulators stay live
+            // through the first GEMM part of the next phase.
+            constexpr int NSP = SP::NS;
+            f32x4 accd[DN];
+            for (int ch = 0; ch < A->NCH; ++ch) {
+                const int jbase = 16 * ch;
+                f32x4 accA[K], accB[K];
+                gemm_h<KBH, T1, NSP, NSP, 0, K>(bh, bl, btail, slot, lane, accA);
+                gemm_end(true);
+                if (ch > 0) epi_c(accd, I2{}, I4{});  // previous chunk, coordinates 2, 3
+                epi_end();
+                gemm_h<KBH, T1, K - NSP, NSP, NSP, K>(bh, bl, btail, slot, lane, accA);
+                gemm_end(true);
+                epi_a(accA, jbase, I0{}, I2{});
+                epi_end();
+                gemm_h<KBH, T1, NSP, NSP, 0, K>(bh, bl, btail, slot, lane, accB);
+                gemm_end(true);
+                epi_a(accA, jbase, I2{}, I4{});
+                epi_end();
+                gemm_h<KBH, T1, K - NSP, NSP, NSP, K>(bh, bl, btail, slot, lane, accB);
+                gemm_end(true);
+                epi_b(accB, I0{}, I2{});
+                epi_end();
+                gemm_h<KBH, T1, NSP, NSP, 0, DN>(bh, bl, btail, slot, lane, accd);
+                gemm_end(true);
+                epi_b(accB, I2{}, I4{});
+                epi_end();
+                gemm_h<KBH, T1, DN - NSP, NSP, NSP, DN>(bh, bl, btail, slot, lane, accd);
+                gemm_end(true);
+                epi_c(accd, I0{}, I2{});
+                epi_end();
+            }
+            epi_c(accd, I2{}, I4{});  // last chunk, coordinates 2, 3
+        } else {
+            for (int ch = 0; ch < A->NCH; ++ch) {
+                const int jbase = 16 * ch;
+                {
+                    f32x4 acc[K];
+                    gemm_rec(acc);
+                    epi_a(acc, jbase, I0{}, I4{});
+                }
+                epi_end();
+                {
+                    f32x4 acc[K];
+                    gemm_rec(acc);
+                    epi_b(acc, I0{}, I4{});
+                }
+                epi_end();
+                {
+                    f32x4 accd[DN];
+                    gemm_rec(accd);
+                    epi_c(accd, I0{}, I4{});
+                }
+                epi_end();
+            }
         }
-        epi_c(accd, I2{}, I4{});  // last chunk, coordinates 2, 3
-    } else {
-        for (int ch = 0; ch < a.NCH; ++ch) {
-            const int jbase = 16 * ch;
-            {
-                f32x4 acc[K];
-                gemm_rec(acc);
-                epi_a(acc, jbase, I0{}, I4{});
-            }
-            epi_end();
-            {
-                f32x4 acc[K];
-                gemm_rec(acc);
-                epi_b(acc, I0{}, I4{});
-            }
-            epi_end();
-            {
-                f32x4 accd[DN];
-                gemm_rec(accd);
-                epi_c(accd, I0{}, I4{});
-            }
-            epi_end();
+
+
+
+    // end of the layer: its log|det| added to the running sum (the order of a
+    // per-layer launch sequence), its status bits kept for the tail
+    {
+        float v = ldsum;
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        ld_acc = ld_acc + v;  // mode 1: ld_prev = 0
+        const int bits = (__any(any_in) ? NFK_ST_INSIDE_SEEN : 0) | (__any(any_nd) ? NFK_ST_NEG_DISC : 0);
+        if constexpr (CHAIN) {
+            if (lane == 0 && bits != 0) atomicOr(cst + l, bits);  // LDS word of layer l
+        } else {
+            st_bits |= (uint64_t)bits;
         }
     }
-
+    }  // layers
 
     // ---- z rows of this wave (upper from the tile, lower = identity copy), log|det|
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1049,38 +1146,46 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
         for (RowWalk w(lane, D4); w.r < nrows; w.next()) {
             const float* row = xlo + w.r * XS;
             const int o = 4 * w.k;
-            *reinterpret_cast<float4*>(a.z + (b0 + w.r) * a.ldz + o) =
-                make_float4(row[m_src[o]], row[m_src[o + 1]], row[m_src[o + 2]], row[m_src[o + 3]]);
+            *reinterpret_cast<float4*>(A->z + (b0 + w.r) * A->ldz + o) =
+                make_float4(row[src_map(o)], row[src_map(o + 1)], row[src_map(o + 2)], row[src_map(o + 3)]);
         }
     } else {
-        for (RowWalk w(lane, a.n_up); w.r < nrows; w.next())
-            a.z[(b0 + w.r) * a.ldz + m_up_out[w.k]] = xup[w.r * XU + w.k];
-        for (RowWalk w(lane, a.n_lo); w.r < nrows; w.next())
-            a.z[(b0 + w.r) * a.ldz + m_lo_out[w.k]] = xlo[w.r * XL + w.k];
+        for (RowWalk w(lane, A->n_up); w.r < nrows; w.next())
+            A->z[(b0 + w.r) * A->ldz + m_up_out[w.k]] = xup[w.r * XU + w.k];
+        for (RowWalk w(lane, A->n_lo); w.r < nrows; w.next())
+            A->z[(b0 + w.r) * A->ldz + m_lo_out[w.k]] = xlo[w.r * XL + w.k];
     }
-    {
-        float v = ldsum;
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        if (q == 0 && row_ok && a.mode != 0) a.logdet[b0 + sl] = ld_prev + v;  // mode 1: ld_prev = 0
-    }
-    if (a.status != nullptr) {
-        const int bits = (__any(any_in) ? NFK_ST_INSIDE_SEEN : 0) | (__any(any_nd) ? NFK_ST_NEG_DISC : 0);
-        if (lane == 0 && bits != 0 && (st_prev & bits) != bits) atomicOr(a.status, bits);
+    if (q == 0 && row_ok && A->mode != 0) A->logdet[b0 + sl] = ld_acc;
+    if constexpr (CHAIN) {
+        // the workgroup's status bits of every layer (LDS words), one global
+        // atomic per layer and workgroup where they add a bit
+        __syncthreads();
+        if (A->status != nullptr && (int)threadIdx.x < NL) {
+            const int bits = cst[threadIdx.x];
+            if (bits != 0 && (A->status[threadIdx.x] & bits) != bits) atomicOr(A->status + threadIdx.x, bits);
+        }
+    } else if (A->status != nullptr) {
+        const int bits = (int)st_bits;
+        if (lane == 0 && bits != 0 && (st_prev & bits) != bits) atomicOr(A->status, bits);
     }
 #ifdef NFK_TRACE
     NFK_MARK(tr);  // end
-    nfk_trace_flush(tr, a.trace, wid, lane);
+    nfk_trace_flush(tr, A->trace, wid, lane);
 #endif
 }
 
 template <int KBH, int T1, int K>
-int launch_fused(const FusedArgs& a, size_t lds, bool inv, bool split, hipStream_t st) {
+int launch_fused(const FusedArgs& a, size_t lds, bool inv, bool split, bool chain, hipStream_t st) {
     const int64_t per_block = (int64_t)kNsfWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
     const dim3 g((unsigned)blocks), b(64 * kNsfWaves);
-    if (split) {
+    if (chain) {
+        if (inv)
+            hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true, true, true>), g, b, lds, st, a);
+        else
+            hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, false, true, true>), g, b, lds, st, a);
+    } else if (split) {
         if (inv)
             hipLaunchKernelGGL((k_fused_nsf<KBH, T1 != 0, K, true, true>), g, b, lds, st, a);
         else
@@ -1099,9 +1204,11 @@ int launch_fused(const FusedArgs& a, size_t lds, bool inv, bool split, hipStream
 // per hidden k-block count so make -j compiles them in parallel); nfk_fused.hip
 // sees only the extern declarations.
 #define NFK_FUSED_INSTANCE(KBH, T1, K) \
-    template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, hipStream_t st);
+    template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, bool chain, \
+                                          hipStream_t st);
 #define NFK_FUSED_EXTERN(KBH, T1, K) \
-    extern template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, hipStream_t st);
+    extern template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, \
+                                                 bool chain, hipStream_t st);
 
 // hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f32 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132

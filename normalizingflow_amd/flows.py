@@ -258,6 +258,7 @@ class _SplineMaps:
         self.lo_in, self.lo_out = mk(lo_in), mk(lo_out)
         self.up_in, self.up_out = mk(up_in), mk(up_out)
         self.lo_in_long = self.lo_in.long()
+        self.lists = (list(lo_in), list(lo_out), list(up_in), list(up_out))
 
 
 class NSF_CL(_HipFlow):
@@ -319,6 +320,15 @@ class NSF_CL(_HipFlow):
         pack = K_.fused_nsf_pack(*params, n_lo, n_up, hidden, self.K)
         self._pack_cache = (key, pack, hidden)
         return pack
+
+    def _chain_shape(self, device):
+        """(n_lo, n_up, hidden, K, B) when this layer runs as the fused kernel
+        (so it may join an nfk_fused_nsf_chain launch with layers of the same
+        shape), else None."""
+        if self._fused_pack(device) is None:
+            return None
+        return (len(self.mask) * self.size, len(self.unmasked) * self.size, self._pack_cache[2], self.K,
+                float(self.B))
 
     def _run(self, x, inverse, logdet, mode, status):
         if x.shape[1] != self.size * self.dim:

@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from . import config
 from . import kernels as K_
-from .flows import _HipFlow, _check_input, _needs_grad, raise_on_status
+from .flows import NSF_CL, _HipFlow, _check_input, _needs_grad, raise_on_status
 
 __all__ = ["NormalizingFlowModel", "NormalizingFlow"]
 
@@ -60,6 +60,28 @@ class _NormalLogProbFn(torch.autograd.Function):
         return g[:, None] * z * (-ctx.inv_var), None, None
 
 
+def _compose_maps(run, D, device):
+    """nfk_fused_nsf_chain's cmaps for a run of NSF_CL layers (include/nfk.h):
+    the chain keeps x's column order in its LDS tile and every layer overwrites
+    its upper columns in place, so output column o of a layer is the tile
+    column its input lo_in[i] / up_in[j] came from (flows.py:239's masked-first
+    concatenation).  perm[c] = tile column of the current logical column c."""
+    perm = list(range(D))
+    out = []
+    for flow in run:
+        lo_in, lo_out, up_in, up_out = flow._maps(device).lists
+        t_lo = [perm[c] for c in lo_in]
+        t_up = [perm[c] for c in up_in]
+        out += t_lo + t_up
+        nxt = [0] * D
+        for o, t in zip(lo_out, t_lo):
+            nxt[o] = t
+        for o, t in zip(up_out, t_up):
+            nxt[o] = t
+        perm = nxt
+    return torch.tensor(out + perm, dtype=torch.int32, device=device)
+
+
 class NormalizingFlowModel(nn.Module):
 
     def __init__(self, prior, flows, device="cpu"):
@@ -69,6 +91,7 @@ class NormalizingFlowModel(nn.Module):
         self.flows = nn.ModuleList(flows)
         self._prior_key = None
         self._prior_iso = None
+        self._chain_cache = {}
 
     # ------------------------------------------------------------------ prior
     def _prior_consts(self):
@@ -116,7 +139,14 @@ class NormalizingFlowModel(nn.Module):
         off = 0
         flows = self.flows[::-1] if inverse else self.flows
         with torch.set_grad_enabled(grad):
-            for flow in flows:
+            for item in self._groups(flows, x.device, grad):
+                if isinstance(item, tuple):  # a run of fused NSF_CL layers: one launch
+                    run, shape = item
+                    k = len(run)
+                    x = self._run_chain(run, shape, x, inverse, logdet, status[off:off + k])
+                    off += k
+                    continue
+                flow = item
                 if isinstance(flow, _HipFlow):
                     k = flow._n_status
                     st = status[off:off + k] if k else None
@@ -134,6 +164,56 @@ class NormalizingFlowModel(nn.Module):
         elif n_st and config.STRICT_CHECKS:
             raise_on_status(status, n_st)
         return x, logdet
+
+    # ------------------------------------------------------- chained launches
+    def _groups(self, flows, device, grad):
+        """The layer sequence with every run of consecutive NSF_CL layers that
+        share one fused-kernel shape replaced by (run, shape) tuples of at most
+        nfk_fused_nsf_chain_max layers (inference only; runs of one stay single)."""
+        if grad or not (config.USE_FUSED and config.USE_CHAIN):
+            return list(flows)
+        out, run, shape = [], [], None
+
+        def flush():
+            nmax = K_.fused_nsf_chain_max(*shape[:4]) if shape is not None else 0
+            i = 0
+            while i < len(run):
+                piece = run[i:i + max(nmax, 1)]
+                out.extend([(piece, shape)] if len(piece) > 1 else piece)
+                i += len(piece)
+
+        for flow in flows:
+            sh = flow._chain_shape(device) if isinstance(flow, NSF_CL) else None
+            if sh is not None and sh == shape:
+                run.append(flow)
+                continue
+            flush()
+            run, shape = ([flow], sh) if sh is not None else ([], None)
+            if sh is None:
+                out.append(flow)
+        flush()
+        return out
+
+    def _run_chain(self, run, shape, x, inverse, logdet, status):
+        n_lo, n_up, hidden, K, B = shape
+        D = n_lo + n_up
+        if x.shape[1] != D or x.data_ptr() % 16 or x.stride(1) != 1 or x.stride(0) % 4:
+            for flow in run:  # not the chain's layout: one launch per layer
+                x = flow._run(x, inverse, logdet, K_.MODE_ACC, status[:1])
+                status = status[1:]
+            return x
+        packs = [f._fused_pack(x.device) for f in run]
+        key = (tuple(id(f) for f in run), bool(inverse), str(x.device))
+        ent = self._chain_cache.get(key)
+        ptrs = tuple(p.data_ptr() for p in packs)
+        if ent is None or ent[0] != ptrs:
+            ent = (ptrs, torch.tensor(ptrs, dtype=torch.int64, device=x.device),
+                   _compose_maps(run, D, x.device))
+            self._chain_cache[key] = ent
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        K_.fused_nsf_chain(x, ent[1], ent[2], len(run), n_lo, n_up, hidden, z, logdet=logdet,
+                           logdet_mode=K_.MODE_ACC, K=K, tail_bound=B, inverse=inverse, status=status)
+        return z
 
     @staticmethod
     def _check(deferred):

@@ -1,0 +1,81 @@
+"""CPU checks of the chained NSF_CL launch (nfk_fused_nsf_chain): the composed
+tile-column maps the host builds (models._compose_maps) and the host-only
+parts of the C ABI (layer-count query, argument validation; no device call).
+
+The map check is independent of the composition code: a run of NSF_CL layers
+evaluated by the CPU oracle (nf/flows.py:227-253) on rows that lie entirely
+outside [-B, B] is the identity per element (nf/utils.py:46-47) but still
+applies the masked-first output permutation of every layer (flows.py:239), so
+z[:, o] = x[:, perm[o]] reveals the column permutation the chain must end on.
+"""
+import pytest
+import torch
+
+import nf.flows as nff
+from normalizingflow_amd import _lib
+from normalizingflow_amd.models import _compose_maps
+from oracle import nf_oracle as orc
+
+
+def _run(size, dim, masks, n_layers):
+    torch.manual_seed(0)
+    return [nff.NSF_CL(size=size, dim=dim, K=4, B=3, hidden_dim=8, mask=masks[i % len(masks)])
+            for i in range(n_layers)]
+
+
+@pytest.mark.parametrize("size,dim,masks,n", [
+    (4, 2, [[0], [1]], 5),        # c3's alternating masks
+    (3, 3, [[1], [0, 2], [2]], 4),  # dim 3, non-prefix and two-coordinate masks
+    (5, 2, [[1]], 3),              # the same non-prefix mask every layer
+])
+def test_composed_maps_match_oracle_permutation(size, dim, masks, n):
+    run = _run(size, dim, masks, n)
+    D = size * dim
+    cm = _compose_maps(run, D, torch.device("cpu")).tolist()
+    assert len(cm) == n * D + D
+    perm = cm[n * D:]
+    assert sorted(perm) == list(range(D))
+    # rows 1.. entirely outside the spline interval: identity values, permuted columns
+    x = torch.empty(3, D)
+    x[0] = 0.1                                  # one inside row (the oracle needs one)
+    x[1:] = 10.0 + torch.arange(D, dtype=torch.float32)
+    specs = [dict(type="NSF_CL", prefix="%d." % i, size=size, dim=dim, K=4, B=3, mask=list(f.mask.tolist()))
+             for i, f in enumerate(run)]
+    sd = {"%d.%s" % (i, k): v for i, f in enumerate(run) for k, v in f.state_dict().items()}
+    z = x
+    for s in specs:
+        z, _ = orc.apply_layer(s, z, sd)
+    assert [int(v) - 10 for v in z[1].tolist()] == perm
+    # every layer's lower/upper tile columns: the layer's inputs under the
+    # permutation of the layers before it
+    p = list(range(D))
+    for i, f in enumerate(run):
+        lo_in, lo_out, up_in, up_out = f._maps(torch.device("cpu")).lists
+        assert cm[i * D:i * D + len(lo_in)] == [p[c] for c in lo_in]
+        assert cm[i * D + len(lo_in):(i + 1) * D] == [p[c] for c in up_in]
+        q = [0] * D
+        for o, c in list(zip(lo_out, lo_in)) + list(zip(up_out, up_in)):
+            q[o] = p[c]
+        p = q
+
+
+def test_chain_layer_count_query_is_host_only():
+    lib = _lib.load()
+    n = lib.nfk_fused_nsf_chain_max(32, 32, 100, 8)   # c3 layer shape
+    assert n >= 8                                      # the c3 model runs as one launch
+    assert lib.nfk_fused_nsf_chain_max(32, 32, 256, 8) == 0   # no narrow kernel for H = 256
+    assert lib.nfk_fused_nsf_chain_max(33, 32, 100, 8) == 0   # D % 4 != 0: no split form
+
+
+def test_chain_argument_validation_is_host_only():
+    lib = _lib.load()
+    nmax = lib.nfk_fused_nsf_chain_max(32, 32, 100, 8)
+    args = lambda nl, x=16, z=16: (x, 64, 16, 16, nl, 32, 32, 100, z, 64, None, 0, 256, 8, 3.0, 0, None,
+                                   None)
+    assert lib.nfk_fused_nsf_chain(*args(0)) == _lib.NFK_EINVAL
+    assert b"layer count" in lib.nfk_last_error()
+    assert lib.nfk_fused_nsf_chain(*args(nmax + 1)) == _lib.NFK_EINVAL
+    assert lib.nfk_fused_nsf_chain(*args(2, x=4)) == _lib.NFK_EINVAL
+    assert b"aligned" in lib.nfk_last_error()
+    rc = lib.nfk_fused_nsf_chain(16, 64, 16, 16, 2, 32, 32, 100, 16, 64, None, 1, 256, 8, 3.0, 0, None, None)
+    assert rc == _lib.NFK_EINVAL and b"null logdet" in lib.nfk_last_error()

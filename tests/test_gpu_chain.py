@@ -1,0 +1,140 @@
+"""GPU parity of the chained fused NSF_CL launch (nfk_fused_nsf_chain,
+k_fused_nsf<..., CHAIN = true> in nfk_fused_impl.h): the model's layer loop
+(nf/models.py:13-29, 37-40) over runs of NSF_CL layers (nf/flows.py:227-253)
+in one launch with x resident in LDS.
+
+* bitwise equal to one nfk_fused_nsf launch per layer (config.USE_CHAIN off):
+  z, log|det| and log_prob, forward and inverse, including runs longer than
+  one launch holds and ragged batches;
+* against the CPU oracle at the fp32 tolerance of the per-layer tests
+  (log_prob rtol 1e-5 / atol 1e-4 as tests/test_gpu_parity.py's c3 test);
+* the reference's data-dependent error (no element inside [-B, B] in some
+  layer, nf/utils.py:63) raised from the chain's per-layer status words.
+"""
+import pytest
+import torch
+
+import nf.flows as nff
+import nf.models as nfm
+from normalizingflow_amd import config
+from normalizingflow_amd import kernels as K_
+from oracle import nf_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(n_layers, size, dim, K, hidden, masks, dev):
+    torch.manual_seed(1234)
+    flows = [nff.NSF_CL(size=size, dim=dim, K=K, B=3, hidden_dim=hidden, mask=masks[i % len(masks)])
+             for i in range(n_layers)]
+    D = size * dim
+    prior = torch.distributions.MultivariateNormal(torch.zeros(D), torch.eye(D))
+    model = nfm.NormalizingFlowModel(prior, flows)
+    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(dev)
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(D, device=dev), torch.eye(D, device=dev))
+    return model, sd
+
+
+def _both(fn):
+    """fn() with the chain on and off -> (chain result, per-layer result)."""
+    prev = config.USE_CHAIN
+    try:
+        config.USE_CHAIN = True
+        a = fn()
+        config.USE_CHAIN = False
+        b = fn()
+    finally:
+        config.USE_CHAIN = prev
+    return a, b
+
+
+def _count_chain_launches(fn):
+    prev = K_.TIMER
+    K_.TIMER = K_.KernelTimer()
+    try:
+        fn()
+        torch.cuda.synchronize()
+        return {k: v[0] for k, v in K_.TIMER.summary().items()}
+    finally:
+        K_.TIMER = prev
+
+
+# (layers, size, dim, K, hidden, masks)
+CASES = [
+    (8, 32, 2, 8, 100, [[0], [1]]),        # c3
+    (21, 32, 2, 8, 100, [[0], [1]]),       # longer than one launch holds (19 at D = 64)
+    (3, 30, 3, 8, 100, [[1], [0, 2]]),     # dim 3, alternating mask sizes: runs split by shape
+    (4, 16, 2, 4, 64, [[1]]),              # KBH 2, the same non-prefix mask every layer
+    (5, 20, 2, 6, 128, [[0], [1]]),        # KBH 4
+]
+
+
+def _ids(c):
+    return "L%d_s%d_d%d_k%d_h%d" % c[:5]
+
+
+@pytest.mark.parametrize("case", CASES, ids=_ids)
+@pytest.mark.parametrize("batch", [4096, 1000])
+def test_chain_bitwise_vs_per_layer_and_oracle(case, batch, hip_device):
+    n, size, dim, K, hidden, masks = case
+    model, sd = _model(n, size, dim, K, hidden, masks, hip_device)
+    D = size * dim
+    x = torch.randn(batch, D, generator=torch.Generator().manual_seed(5)) * 1.3
+    xd = x.to(hip_device)
+    with torch.no_grad():
+        (zc, plc, ldc), (zs, pls, lds) = _both(lambda: model(xd))
+        (lpc,), (lps,) = _both(lambda: (model.log_prob(xd),))
+        (xic, ldic), (xis, ldis) = _both(lambda: model.inverse(xd))
+    for a, b in ((zc, zs), (plc, pls), (ldc, lds), (lpc, lps), (xic, xis), (ldic, ldis)):
+        assert torch.equal(a, b)
+    specs = orc.nsf_cl_specs(n, size, dim, K, 3, masks)
+    ref = orc.model_log_prob(specs, sd, x)
+    torch.testing.assert_close(lpc.cpu(), ref, rtol=1e-5, atol=1e-4)
+    xr, ldr = orc.model_inverse(specs, sd, x)
+    torch.testing.assert_close(xic.cpu(), xr, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(ldic.cpu(), ldr, rtol=1e-5, atol=3e-4)
+
+
+def test_c3_runs_as_one_launch(hip_device):
+    model, _ = _model(8, 32, 2, 8, 100, [[0], [1]], hip_device)
+    x = torch.randn(512, 64, device=hip_device)
+    counts = _count_chain_launches(lambda: model.log_prob(x))
+    assert counts.get("nfk_fused_nsf_chain") == 1 and "nfk_fused_nsf" not in counts
+    # a run longer than one launch holds: two launches
+    nmax = K_.fused_nsf_chain_max(32, 32, 100, 8)
+    model, _ = _model(nmax + 3, 32, 2, 8, 100, [[0], [1]], hip_device)
+    counts = _count_chain_launches(lambda: model.log_prob(x))
+    assert counts.get("nfk_fused_nsf_chain") == 2
+
+
+def test_chain_training_mode_uses_per_layer_nodes(hip_device):
+    model, _ = _model(4, 32, 2, 8, 100, [[0], [1]], hip_device)
+    x = torch.randn(256, 64, device=hip_device)
+    z, lp, ld = model(x)           # grad enabled, parameters require grad
+    (lp + ld).sum().backward()
+    assert model.flows[0].psi.network[0].weight.grad is not None
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_chain_no_element_inside_raises(inverse, hip_device):
+    model, _ = _model(4, 32, 2, 8, 100, [[0], [1]], hip_device)
+    x = torch.full((128, 64), 50.0, device=hip_device)  # every layer: all elements outside [-3, 3]
+    for chain in (True, False):
+        prev = config.USE_CHAIN
+        config.USE_CHAIN = chain
+        try:
+            with pytest.raises(RuntimeError, match="no element inside"):
+                with torch.no_grad():
+                    model.inverse(x) if inverse else model.log_prob(x)
+        finally:
+            config.USE_CHAIN = prev
+
+
+def test_chain_unaligned_input_falls_back(hip_device):
+    model, _ = _model(4, 32, 2, 8, 100, [[0], [1]], hip_device)
+    buf = torch.randn(300 * 64 + 1, device=hip_device)
+    x = buf[1:].view(300, 64)    # 4-byte offset: not 16-byte aligned
+    with torch.no_grad():
+        a, b = _both(lambda: model.log_prob(x))
+    assert torch.equal(a, b)
