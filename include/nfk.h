@@ -218,6 +218,12 @@ int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t
  *           order; a layer overwrites its upper columns in place) -- then, for
  *           every output column o of the last layer, the tile column holding it.
  *   status: nlayers words, one per layer (bits as nfk_rqs_coupling).
+ *   log_prob: optional prior epilogue (NormalizingFlowModel.evaluate,
+ *           models.py:37-40, Normal prior N(0, s^2 I), setup.py:25-30):
+ *           log_prob[b] = log N(z_b; 0, prior_scale^2 I) + log|det|_b with
+ *           prior_half_log_det = sum log(scale_tril diagonal) as torch has it
+ *           (the constants of nfk_normal_logprob).  With log_prob given, z may
+ *           be NULL (not written) and logdet NULL with logdet_mode 0.
  * nlayers <= nfk_fused_nsf_chain_max() (0: shape not supported by the chain
  * form); x, z 16-byte aligned with ldx, ldz multiples of 4.
  * ------------------------------------------------------------------------- */
@@ -226,7 +232,8 @@ int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* const* wpacks,
                         const int32_t* cmaps, int32_t nlayers, int32_t n_lo, int32_t n_up,
                         int32_t hidden, float* z, int64_t ldz, float* logdet,
                         int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound,
-                        int32_t inverse, int32_t* status, nfk_stream_t stream);
+                        int32_t inverse, int32_t* status, float* log_prob, float prior_scale,
+                        float prior_half_log_det, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Fused RealNVP layer: both affine half-couplings with their four FCNN

@@ -32,6 +32,7 @@
 // barrier per phase); each record is read from L2 once per 128 samples.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 
@@ -451,6 +452,8 @@ FusedArgs fused_args(const float* x, int64_t ldx, const float* wpack, const int3
     a.packs = nullptr;
     a.cmaps = nullptr;
     a.nlayers = 1;
+    a.log_prob = nullptr;
+    a.prior_inv_scale = a.prior_c2pi = a.prior_hld = 0.0f;
     {
         // NSF_CL's spline constants (flows.py:236-237 defaults), evaluated like the
         // reference's Python scalars (nfk_make_const), folded for the fixed-point knots
@@ -522,16 +525,18 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
                                    const int32_t* cmaps, int32_t nlayers, int32_t n_lo, int32_t n_up,
                                    int32_t hidden, float* z, int64_t ldz, float* logdet,
                                    int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound,
-                                   int32_t inverse, int32_t* status, nfk_stream_t stream) {
+                                   int32_t inverse, int32_t* status, float* log_prob, float prior_scale,
+                                   float prior_half_log_det, nfk_stream_t stream) {
     if (!shape_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_chain: shape not supported");
     const Layout L = make_layout(n_lo, n_up, hidden, K);
     const int nmax = chain_max_layers(L);
     if (nlayers < 1 || nlayers > nmax) return nfk_set_error("nfk_fused_nsf_chain: bad layer count");
     if (batch < 0) return nfk_set_error("nfk_fused_nsf_chain: bad batch");
     if (batch == 0) return 0;
-    if (!x || !wpacks || !cmaps || !z) return nfk_set_error("nfk_fused_nsf_chain: null pointer");
+    if (!x || !wpacks || !cmaps || (!z && !log_prob)) return nfk_set_error("nfk_fused_nsf_chain: null pointer");
+    if (log_prob && !(prior_scale > 0.0f)) return nfk_set_error("nfk_fused_nsf_chain: bad prior scale");
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf_chain: null logdet");
-    if (((uintptr_t)x % 16) != 0 || ((uintptr_t)z % 16) != 0 || ldx % 4 != 0 || ldz % 4 != 0)
+    if (((uintptr_t)x % 16) != 0 || ((uintptr_t)z % 16) != 0 || ldx % 4 != 0 || (z && ldz % 4 != 0))
         return nfk_set_error("nfk_fused_nsf_chain: x and z rows must be 16-byte aligned");
     FusedArgs a = fused_args(x, ldx, nullptr, nullptr, nullptr, nullptr, nullptr, L, z, ldz, logdet, logdet_mode,
                              batch, K, tail_bound, status);
@@ -540,6 +545,12 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
     a.packs = wpacks;
     a.cmaps = cmaps;
     a.nlayers = nlayers;
+    if (log_prob) {  // the constants of nfk_normal_logprob
+        a.log_prob = log_prob;
+        a.prior_inv_scale = 1.0f / prior_scale;
+        a.prior_c2pi = (float)((n_lo + n_up) * std::log(2.0 * M_PI));
+        a.prior_hld = prior_half_log_det;
+    }
     const size_t lds = lds_bytes_chain(L, nlayers);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;

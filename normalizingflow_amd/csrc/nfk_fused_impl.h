@@ -254,6 +254,10 @@ struct FusedArgs {
                                 // of every layer's inputs, then [D] the tile column of
                                 // every output column after the last layer
     int32_t nlayers;
+    // chain form, optional prior epilogue: log_prob[b] = log N(z_b; 0, s^2 I) +
+    // log|det|_b (z need not be written then: z may be null)
+    float* log_prob;
+    float prior_inv_scale, prior_c2pi, prior_hld;
 };
 
 __device__ __forceinline__ f32x4 mfma32(float a, float b, f32x4 c) {
@@ -1143,6 +1147,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     if constexpr (SPLIT) {
         // whole z rows, 16 B per lane: output column o takes tile column m_src[o]
         const int D4 = D >> 2;
+        if (!CHAIN || A->z != nullptr)
         for (RowWalk w(lane, D4); w.r < nrows; w.next()) {
             const float* row = xlo + w.r * XS;
             const int o = 4 * w.k;
@@ -1156,6 +1161,27 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
             A->z[(b0 + w.r) * A->ldz + m_lo_out[w.k]] = xlo[w.r * XL + w.k];
     }
     if (q == 0 && row_ok && A->mode != 0) A->logdet[b0 + sl] = ld_acc;
+    if constexpr (CHAIN) {
+        // prior epilogue (NormalizingFlowModel.evaluate, models.py:37-40, with the
+        // isotropic Normal prior): log N(z; 0, s^2 I) + log|det| from the tile
+        // row, the 4 lanes of sample sl summing output columns 4(q + 4i) .. + 3
+        // as k_normal_lp4 does (y = z / s)
+        if (A->log_prob != nullptr) {
+            const float* row = xlo + sl * XS;
+            const float il = A->prior_inv_scale;
+            float m = 0.0f;
+            for (int g = q; g < (D >> 2); g += 4) {
+                const int o = 4 * g;
+                const float y0 = row[src_map(o)] * il, y1 = row[src_map(o + 1)] * il;
+                const float y2 = row[src_map(o + 2)] * il, y3 = row[src_map(o + 3)] * il;
+                m += (y0 * y0 + y1 * y1) + (y2 * y2 + y3 * y3);
+            }
+            m += __shfl_xor(m, 16, 64);
+            m += __shfl_xor(m, 32, 64);
+            const float lp = -0.5f * (A->prior_c2pi + m) - A->prior_hld;
+            if (q == 0 && row_ok) A->log_prob[b0 + sl] = lp + ld_acc;
+        }
+    }
     if constexpr (CHAIN) {
         // the workgroup's status bits of every layer (LDS words), one global
         // atomic per layer and workgroup where they add a bit

@@ -328,21 +328,24 @@ def fused_nsf_chain_max(n_lo, n_up, hidden, K):
 
 
 def fused_nsf_chain(x, wpacks, cmaps, nlayers, n_lo, n_up, hidden, z, *, logdet, logdet_mode, K,
-                    tail_bound, inverse=False, status=None):
+                    tail_bound, inverse=False, status=None, log_prob=None, prior_scale=1.0,
+                    prior_hld=0.0):
     """nlayers fused NSF_CL layers in one launch (include/nfk.h nfk_fused_nsf_chain).
     wpacks: int64 device tensor of the layers' pack pointers; cmaps: int32 device
-    tensor [nlayers * D + D] of composed tile columns; status: nlayers words."""
-    dev = _require_hip(x, wpacks, cmaps, z, logdet, status)
+    tensor [nlayers * D + D] of composed tile columns; status: nlayers words.
+    log_prob (optional [batch]): the isotropic-normal prior epilogue, z may be None."""
+    dev = _require_hip(x, wpacks, cmaps, z, logdet, status, log_prob)
     B = x.shape[0]
     D = n_lo + n_up
     if wpacks.dtype != torch.int64 or wpacks.numel() != nlayers:
         raise ValueError("wpacks must hold %d int64 pack pointers" % nlayers)
     _vec(cmaps, nlayers * D + D, "cmaps", torch.int32)
     xp, ldx = _mat(x, "x")
-    zp, ldz = _mat(z, "z")
+    zp, ldz = _mat(z, "z") if z is not None else (None, 0)
     _timed("nfk_fused_nsf_chain", dev, "nfk_fused_nsf_chain", xp, ldx, wpacks.data_ptr(), cmaps.data_ptr(),
            nlayers, n_lo, n_up, hidden, zp, ldz, _vec(logdet, B, "logdet"), logdet_mode, B, K,
-           float(tail_bound), 1 if inverse else 0, _vec(status, nlayers, "status", torch.int32), _stream(dev))
+           float(tail_bound), 1 if inverse else 0, _vec(status, nlayers, "status", torch.int32),
+           _vec(log_prob, B, "log_prob"), float(prior_scale), float(prior_hld), _stream(dev))
 
 
 def fused_realnvp_supported(half_dim, hidden):

@@ -194,14 +194,11 @@ class NormalizingFlowModel(nn.Module):
         flush()
         return out
 
-    def _run_chain(self, run, shape, x, inverse, logdet, status):
-        n_lo, n_up, hidden, K, B = shape
-        D = n_lo + n_up
-        if x.shape[1] != D or x.data_ptr() % 16 or x.stride(1) != 1 or x.stride(0) % 4:
-            for flow in run:  # not the chain's layout: one launch per layer
-                x = flow._run(x, inverse, logdet, K_.MODE_ACC, status[:1])
-                status = status[1:]
-            return x
+    @staticmethod
+    def _chain_layout_ok(x, D):
+        return x.shape[1] == D and x.data_ptr() % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 4 == 0
+
+    def _chain_args(self, run, D, inverse, x):
         packs = [f._fused_pack(x.device) for f in run]
         key = (tuple(id(f) for f in run), bool(inverse), str(x.device))
         ent = self._chain_cache.get(key)
@@ -210,8 +207,45 @@ class NormalizingFlowModel(nn.Module):
             ent = (ptrs, torch.tensor(ptrs, dtype=torch.int64, device=x.device),
                    _compose_maps(run, D, x.device))
             self._chain_cache[key] = ent
+        return ent[1], ent[2]
+
+    def _fused_log_prob(self, x):
+        """evaluate() as ONE launch when the whole model is one chained run of
+        fused NSF_CL layers and the prior is the isotropic Normal: the prior
+        is the chain's epilogue and z never reaches HBM.  None otherwise."""
+        if not (config.USE_FUSED and config.USE_CHAIN) or x.dim() != 2 or not x.is_cuda \
+                or x.dtype != torch.float32:
+            return None
+        iso = self._prior_consts()
+        groups = self._groups(self.flows, x.device, False)
+        if iso is None or len(groups) != 1 or not isinstance(groups[0], tuple):
+            return None
+        run, shape = groups[0]
+        n_lo, n_up, hidden, K, B = shape
+        D = n_lo + n_up
+        if self.prior.loc.shape[0] != D or not self._chain_layout_ok(x, D):
+            return None
+        wp, cm = self._chain_args(run, D, False, x)
+        status = torch.zeros(len(run), dtype=torch.int32, device=x.device)
+        out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+        K_.fused_nsf_chain(x, wp, cm, len(run), n_lo, n_up, hidden, None, logdet=None,
+                           logdet_mode=K_.MODE_NONE, K=K, tail_bound=B, inverse=False, status=status,
+                           log_prob=out, prior_scale=iso[0], prior_hld=iso[1])
+        if config.STRICT_CHECKS:
+            raise_on_status(status, len(run))
+        return out
+
+    def _run_chain(self, run, shape, x, inverse, logdet, status):
+        n_lo, n_up, hidden, K, B = shape
+        D = n_lo + n_up
+        if not self._chain_layout_ok(x, D):
+            for flow in run:  # not the chain's layout: one launch per layer
+                x = flow._run(x, inverse, logdet, K_.MODE_ACC, status[:1])
+                status = status[1:]
+            return x
+        wp, cm = self._chain_args(run, D, inverse, x)
         z = torch.empty_like(x, memory_format=torch.contiguous_format)
-        K_.fused_nsf_chain(x, ent[1], ent[2], len(run), n_lo, n_up, hidden, z, logdet=logdet,
+        K_.fused_nsf_chain(x, wp, cm, len(run), n_lo, n_up, hidden, z, logdet=logdet,
                            logdet_mode=K_.MODE_ACC, K=K, tail_bound=B, inverse=inverse, status=status)
         return z
 
@@ -245,6 +279,9 @@ class NormalizingFlowModel(nn.Module):
 
     @torch.no_grad()
     def evaluate(self, x):
+        out = self._fused_log_prob(x)
+        if out is not None:
+            return out.data
         d = []
         z, log_det = self._chain(x, False, d)
         out = self._prior_log_prob(z, logdet=log_det, sign=1)

@@ -70,12 +70,17 @@ def test_chain_layer_count_query_is_host_only():
 def test_chain_argument_validation_is_host_only():
     lib = _lib.load()
     nmax = lib.nfk_fused_nsf_chain_max(32, 32, 100, 8)
-    args = lambda nl, x=16, z=16: (x, 64, 16, 16, nl, 32, 32, 100, z, 64, None, 0, 256, 8, 3.0, 0, None,
-                                   None)
+    args = lambda nl, x=16, z=16, lp=None, sc=1.0: (x, 64, 16, 16, nl, 32, 32, 100, z, 64, None, 0, 256, 8,
+                                                    3.0, 0, None, lp, sc, 0.0, None)
     assert lib.nfk_fused_nsf_chain(*args(0)) == _lib.NFK_EINVAL
     assert b"layer count" in lib.nfk_last_error()
     assert lib.nfk_fused_nsf_chain(*args(nmax + 1)) == _lib.NFK_EINVAL
     assert lib.nfk_fused_nsf_chain(*args(2, x=4)) == _lib.NFK_EINVAL
     assert b"aligned" in lib.nfk_last_error()
-    rc = lib.nfk_fused_nsf_chain(16, 64, 16, 16, 2, 32, 32, 100, 16, 64, None, 1, 256, 8, 3.0, 0, None, None)
+    rc = lib.nfk_fused_nsf_chain(16, 64, 16, 16, 2, 32, 32, 100, 16, 64, None, 1, 256, 8, 3.0, 0, None,
+                                 None, 1.0, 0.0, None)
     assert rc == _lib.NFK_EINVAL and b"null logdet" in lib.nfk_last_error()
+    assert lib.nfk_fused_nsf_chain(*args(2, z=None)) == _lib.NFK_EINVAL      # neither z nor log_prob
+    assert b"null pointer" in lib.nfk_last_error()
+    assert lib.nfk_fused_nsf_chain(*args(2, z=None, lp=16, sc=0.0)) == _lib.NFK_EINVAL
+    assert b"prior scale" in lib.nfk_last_error()
