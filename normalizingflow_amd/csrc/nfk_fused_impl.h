@@ -486,7 +486,13 @@ __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[
 #ifndef NFK_LUT
 #define NFK_LUT 1
 #endif
-template <int K, bool SEARCH, int R0 = 0, int R1 = 4>
+#ifndef NFK_PK2
+// knot prefixes of coordinate pairs in packed fp32: 7 % fewer VALU
+// instructions per layer, yet c3 measured 1 % slower (6.37 vs 6.30 ms per
+// chain, A/B on one box), so off by default
+#define NFK_PK2 0
+#endif
+template <int K, bool SEARCH, int R0 = 0, int R1 = 4, bool PK = true>
 __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&xv)[4],
                                            const FusedConst& c, float l2e, int (&kb)[4],
                                            float (&ek)[4], float (&sk)[4], int* scr, int lane) {
@@ -502,13 +508,29 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
     }
     return;
 #endif
+    // coordinate pairs (r, r + 1): the knot prefixes of both in packed fp32
+    // (nfk_prefix_nsf_lean2, NFK_PK2; bitwise the per-coordinate result)
+    constexpr bool PAIRS = PK && NFK_PK2 && K <= 8 && (R1 - R0) % 2 == 0;
+    int pre2[K];
 #pragma unroll
     for (int r = R0; r < R1; ++r) {
         float u[K];
         int pre[K];
 #pragma unroll
         for (int t = 0; t < K; ++t) u[t] = acc[t][r];
-        nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
+        if constexpr (PAIRS) {
+            if ((r - R0) % 2 == 0) {
+                float u1[K];
+#pragma unroll
+                for (int t = 0; t < K; ++t) u1[t] = acc[t][r + 1];
+                nfk_prefix_nsf_lean2<K>(u, u1, l2e, c.m2b, c.fb30, c.mb30, pre, pre2);
+            } else {
+#pragma unroll
+                for (int t = 0; t < K; ++t) pre[t] = pre2[t];
+            }
+        } else {
+            nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
+        }
         int p0 = 0, p1 = pre[1 < K ? 1 : 0];
         if (SEARCH) {
             const int xi = __float2int_rd(__builtin_fmaf(xv[r], c.inv30, -c.lo * c.inv30));
@@ -682,6 +704,8 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     using SP = NfkSplit<KBH, T1, K, HT>;
     // pipelined chunk schedule: split form with two sub-records per W/H/D record
     constexpr bool PIPE = SPLIT && NFK_SPLIT_PIPE && SP::NW == 2 && SP::ND == 2;
+    // packed knot prefixes, except in the inverse chain (it spills with them)
+    constexpr bool PK2 = !(INV && CHAIN);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4, sl = lane & 15;
@@ -969,12 +993,12 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                 jj4[r] = jbase + 4 * q + r;
                 xv[r] = (jj4[r] < A->n_up) ? (SPLIT ? xlo : xup)[up_pos(jj4[r])] : 0.0f;
             }
-            knot_phase<K, true, R0, R1>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
+            knot_phase<K, true, R0, R1, PK2>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
         };
         // epilogue B: the other knots, selected at the bin
         auto epi_b = [&](const f32x4(&acc)[K], auto r0c, auto r1c) {
             constexpr int R0 = decltype(r0c)::value, R1 = decltype(r1c)::value;
-            knot_phase<K, false, R0, R1>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
+            knot_phase<K, false, R0, R1, PK2>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k, scr, lane);
         };
         // epilogue C: derivatives of the bin, evaluate, log|det|
         auto epi_c = [&](const f32x4(&accd)[DN], auto r0c, auto r1c) {

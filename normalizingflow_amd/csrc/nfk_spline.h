@@ -185,6 +185,71 @@ __device__ __forceinline__ void nfk_prefix_nsf_lean(const float (&raw)[K], float
     for (int i = 0; i < K - 1; ++i) pre[i + 1] = pre[i] + (int)__builtin_fmaf(e[i], f30, mb30);
 }
 
+// nfk_prefix_nsf_lean for two coordinates at once: the fp32 FMAs, multiplies
+// and sums run as packed pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32,
+// two lanes' worth of work per VALU instruction); max, exp2, rcp and the
+// integer conversion stay scalar.  Every operation is the scalar one applied
+// per component, in the same order, so pre0/pre1 are bitwise those of two
+// nfk_prefix_nsf_lean calls.
+typedef float nfk_f2 __attribute__((ext_vector_type(2)));
+template <int K>
+__device__ __forceinline__ nfk_f2 nfk_sum2(const nfk_f2 (&v)[K]) {
+#if NFK_TREESUM
+    nfk_f2 t[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) t[i] = v[i];
+#pragma unroll
+    for (int w = 1; w < K; w *= 2)
+#pragma unroll
+        for (int i = 0; i + w < K; i += 2 * w) t[i] = t[i] + t[i + w];
+    return t[0];
+#else
+    nfk_f2 s = v[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) s = s + v[i];
+    return s;
+#endif
+}
+
+template <int K>
+__device__ __forceinline__ void nfk_prefix_nsf_lean2(const float (&raw0)[K], const float (&raw1)[K], float l2e,
+                                                     float m2b, float fb30, float mb30, int (&pre0)[K],
+                                                     int (&pre1)[K]) {
+    float m0 = raw0[0], m1 = raw1[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) {
+        m0 = fmaxf(m0, raw0[i]);
+        m1 = fmaxf(m1, raw1[i]);
+    }
+    const nfk_f2 l2 = {l2e, l2e};
+    const nfk_f2 mL = nfk_f2{m0, m1} * l2;
+    nfk_f2 e[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const nfk_f2 a = __builtin_elementwise_fma(nfk_f2{raw0[i], raw1[i]}, l2, -mL);
+        e[i] = nfk_f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+    }
+    const nfk_f2 s1 = nfk_sum2<K>(e);
+    const nfk_f2 mb = {m2b, m2b};
+    const nfk_f2 q = mb * nfk_f2{__builtin_amdgcn_rcpf(s1.x), __builtin_amdgcn_rcpf(s1.y)};
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const nfk_f2 a = __builtin_elementwise_fma(e[i], q, -mb);
+        e[i] = nfk_f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+    }
+    const nfk_f2 s2 = nfk_sum2<K>(e);
+    const nfk_f2 f30 = nfk_f2{fb30, fb30} * nfk_f2{__builtin_amdgcn_rcpf(s2.x), __builtin_amdgcn_rcpf(s2.y)};
+    const nfk_f2 mb30v = {mb30, mb30};
+    pre0[0] = 0;
+    pre1[0] = 0;
+#pragma unroll
+    for (int i = 0; i < K - 1; ++i) {
+        const nfk_f2 f = __builtin_elementwise_fma(e[i], f30, mb30v);
+        pre0[i + 1] = pre0[i] + (int)f.x;
+        pre1[i + 1] = pre1[i] + (int)f.y;
+    }
+}
+
 // min_d + softplus(softplus(v)) of NSF_CL + RQS (flows.py:235, utils.py:82) in
 // one step: e^softplus(v) = 1 + e^v, so softplus(softplus(v)) = log(2 + e^v);
 // torch's threshold 20 passes v through both softplus calls unchanged.
