@@ -11,7 +11,13 @@ USE_FUSED      run NSF_CL layers whose conditioner is the stock FCNN through the
 USE_CHAIN      in inference, run consecutive fused NSF_CL layers of one shape as
                one nfk_fused_nsf_chain launch (x resident in LDS across the
                layers); results are bitwise those of the per-layer launches.
+SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
+               fp16-split products on the fp16 matrix cores (split_gemm.py,
+               fp32-accurate) instead of fp32 GEMMs.  Off: torch.mm with
+               out_dtype=float32 measured 3.5x slower than the fp32 GEMMs
+               (c3 train step 468 vs 135 ms at 2^20).
 """
 STRICT_CHECKS = True
 USE_FUSED = True
 USE_CHAIN = True
+SPLIT_GEMM = False

@@ -38,6 +38,7 @@ import torch.nn.init as init
 
 from . import config
 from . import kernels as K_
+from . import split_gemm
 from . import torch_math
 from ._lib import ST_INSIDE_SEEN, ST_NEG_DISC
 
@@ -353,12 +354,16 @@ class NSF_CL(_HipFlow):
 
     def _vjp(self, x, names, params, gz, gld, inverse, need):
         """Backward: the conditioner is recomputed and differentiated by torch
-        (hipBLASLt GEMMs), the spline by nfk_rqs_coupling_bwd."""
+        (hipBLASLt GEMMs: fp16-split products, split_gemm, for the stock FCNN),
+        the spline by nfk_rqs_coupling_bwd."""
         maps = self._maps(x.device)
         with torch.enable_grad():
             lower = x.detach().index_select(1, maps.lo_in_long).requires_grad_(need[0])
             pd = {n: t.detach().requires_grad_(r) for n, t, r in zip(names, params, need[1:])}
-            raw = torch_math.conditioner(self, pd, "psi", lower)
+            if config.SPLIT_GEMM and _is_stock_fcnn(self.psi):
+                raw = split_gemm.fcnn(pd, "psi.", lower)  # fp16-split GEMMs (fp32-accurate)
+            else:
+                raw = torch_math.conditioner(self, pd, "psi", lower)
         rawc = raw.detach().contiguous()
         gp = torch.empty_like(rawc)
         gx = torch.empty(x.shape, dtype=x.dtype, device=x.device)

@@ -373,3 +373,23 @@ def test_app_train_steps_reduce_nll(hip_device, tmp_path):
     app.load_checkpoint(other, path)
     with torch.no_grad():
         rel_close(other.log_prob(xs[0]), model.log_prob(xs[0]), 0.0, "reloaded log_prob")
+
+
+def test_split_gemm_linear_vs_fp64():
+    """split_gemm.linear (three fp16 GEMMs, fp32 out) forward and backward vs
+    an fp64 nn.Linear, at the c3 conditioner's output-layer shape."""
+    from normalizingflow_amd import split_gemm as sg
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(4096, 100, generator=g).to(DEV).requires_grad_(True)
+    w = (torch.randn(736, 100, generator=g) * 0.1).to(DEV).requires_grad_(True)
+    b = (torch.randn(736, generator=g) * 0.1).to(DEV).requires_grad_(True)
+    gy = torch.randn(4096, 736, generator=g).to(DEV)
+    y = sg.linear(x, w, b)
+    y.backward(gy)
+    xd, wd, bd = (t.detach().double().requires_grad_(True) for t in (x, w, b))
+    yd = F.linear(xd, wd, bd)
+    yd.backward(gy.double())
+    rel_close(y, yd, 2e-6, "y")
+    rel_close(x.grad, xd.grad, 2e-6, "gx")
+    rel_close(w.grad, wd.grad, 2e-6, "gw")
+    rel_close(b.grad, bd.grad, 2e-6, "gb")

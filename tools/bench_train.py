@@ -61,7 +61,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle train step")
+    ap.add_argument("--no-split-gemm", action="store_true",
+                    help="fp32 conditioner GEMMs in the NSF_CL backward (config.SPLIT_GEMM off)")
     args = ap.parse_args()
+    from normalizingflow_amd import config
+    config.SPLIT_GEMM = not args.no_split_gemm
     dev = torch.device("cuda", 0)
     model, sd, _ = bench.build_model(args.workload, dev)
     x = torch.randn(args.batch, bench.WORKLOADS[args.workload][3], device=dev)
@@ -72,7 +76,7 @@ def main():
         return -torch.mean(plp + ld)
 
     res = {"metric": "samples/sec train step (NLL fwd + bwd + Adam)", "workload": args.workload,
-           "batch": args.batch, "steps": args.steps}
+           "batch": args.batch, "steps": args.steps, "split_gemm": config.SPLIT_GEMM}
     t = timed(ours, opt, x, args.steps, args.warmup)
     res["hip"] = {"ms_per_step": round(t * 1e3, 3), "samples_per_s": round(args.batch / t, 1)}
     if not args.no_torch:
