@@ -147,3 +147,17 @@ def test_chain_unaligned_input_falls_back(hip_device):
     with torch.no_grad():
         a, b = _both(lambda: model.log_prob(x))
     assert torch.equal(a, b)
+
+
+def test_chain_sample_vs_oracle(hip_device):
+    """sample() (models.py:31-35): prior draws on the device, then the inverse
+    chain; checked against the oracle's inverse of the SAME draws."""
+    model, sd = _model(8, 32, 2, 8, 100, [[0], [1]], hip_device)
+    torch.manual_seed(7)
+    x, log_px, z = model.sample(2000)
+    specs = orc.nsf_cl_specs(8, 32, 2, 8, 3, [[0], [1]])
+    xr, lpr, _ = orc.model_sample_from(specs, sd, z.cpu())
+    torch.testing.assert_close(x.cpu(), xr, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(log_px.cpu(), lpr, rtol=1e-5, atol=1e-4)
+    counts = _count_chain_launches(lambda: model.sample(64))
+    assert counts.get("nfk_fused_nsf_chain") == 1 and "nfk_fused_nsf" not in counts
