@@ -322,9 +322,16 @@ def fused_nsf(x, wpack, up_in, up_out, lo_in, lo_out, hidden, z, *, logdet, logd
               1 if inverse else 0, _vec(status, 1, "status", torch.int32), _stream(dev))
 
 
+_CHAIN_MAX = {}
+
+
 def fused_nsf_chain_max(n_lo, n_up, hidden, K):
     """Most NSF_CL layers of this shape one nfk_fused_nsf_chain launch holds (0: none)."""
-    return int(_lib.load().nfk_fused_nsf_chain_max(n_lo, n_up, hidden, K))
+    key = (n_lo, n_up, hidden, K)
+    n = _CHAIN_MAX.get(key)
+    if n is None:
+        n = _CHAIN_MAX[key] = int(_lib.load().nfk_fused_nsf_chain_max(n_lo, n_up, hidden, K))
+    return n
 
 
 def fused_nsf_chain(x, wpacks, cmaps, nlayers, n_lo, n_up, hidden, z, *, logdet, logdet_mode, K,

@@ -92,6 +92,7 @@ class NormalizingFlowModel(nn.Module):
         self._prior_key = None
         self._prior_iso = None
         self._chain_cache = {}
+        self._lp_plan_cache = None
 
     # ------------------------------------------------------------------ prior
     def _prior_consts(self):
@@ -216,16 +217,13 @@ class NormalizingFlowModel(nn.Module):
         if not (config.USE_FUSED and config.USE_CHAIN) or x.dim() != 2 or not x.is_cuda \
                 or x.dtype != torch.float32:
             return None
-        iso = self._prior_consts()
-        groups = self._groups(self.flows, x.device, False)
-        if iso is None or len(groups) != 1 or not isinstance(groups[0], tuple):
+        plan = self._lp_plan(x)
+        if plan is None:
             return None
-        run, shape = groups[0]
+        run, shape, iso, wp, cm = plan
         n_lo, n_up, hidden, K, B = shape
-        D = n_lo + n_up
-        if self.prior.loc.shape[0] != D or not self._chain_layout_ok(x, D):
+        if not self._chain_layout_ok(x, n_lo + n_up):
             return None
-        wp, cm = self._chain_args(run, D, False, x)
         status = torch.zeros(len(run), dtype=torch.int32, device=x.device)
         out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
         K_.fused_nsf_chain(x, wp, cm, len(run), n_lo, n_up, hidden, None, logdet=None,
@@ -234,6 +232,25 @@ class NormalizingFlowModel(nn.Module):
         if config.STRICT_CHECKS:
             raise_on_status(status, len(run))
         return out
+
+    def _lp_plan(self, x):
+        """(run, shape, prior consts, wpacks, cmaps) of the one-launch evaluate, or
+        None; cached on the parameters' storage and versions so a log_prob loop
+        pays one key check per call instead of re-deriving the plan."""
+        iso = self._prior_consts()
+        key = (str(x.device), iso, tuple((p.data_ptr(), p._version) for p in self.parameters()))
+        if self._lp_plan_cache is not None and self._lp_plan_cache[0] == key:
+            return self._lp_plan_cache[1]
+        plan = None
+        groups = self._groups(self.flows, x.device, False)
+        if iso is not None and len(groups) == 1 and isinstance(groups[0], tuple):
+            run, shape = groups[0]
+            D = shape[0] + shape[1]
+            if self.prior.loc.shape[0] == D:
+                wp, cm = self._chain_args(run, D, False, x)
+                plan = (run, shape, iso, wp, cm)
+        self._lp_plan_cache = (key, plan)
+        return plan
 
     def _run_chain(self, run, shape, x, inverse, logdet, status):
         n_lo, n_up, hidden, K, B = shape
