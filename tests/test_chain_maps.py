@@ -84,3 +84,39 @@ def test_chain_argument_validation_is_host_only():
     assert b"null pointer" in lib.nfk_last_error()
     assert lib.nfk_fused_nsf_chain(*args(2, z=None, lp=16, sc=0.0)) == _lib.NFK_EINVAL
     assert b"prior scale" in lib.nfk_last_error()
+
+
+def test_layer_grouping(monkeypatch):
+    """NormalizingFlowModel._groups: runs of consecutive same-shape fused NSF_CL
+    layers become (run, shape) items of at most nfk_fused_nsf_chain_max layers;
+    other layers, shape changes and single-layer runs stay per-layer; training
+    (grad) never chains.  Fused-kernel availability is stubbed (no device)."""
+    import nf.models as nfm
+    from normalizingflow_amd import config
+    from normalizingflow_amd import kernels as K_
+    torch.manual_seed(0)
+    a = [nff.NSF_CL(size=4, dim=2, K=4, B=3, hidden_dim=8, mask=[i % 2]) for i in range(5)]
+    b = nff.NSF_CL(size=4, dim=2, K=6, B=3, hidden_dim=8, mask=[0])     # another K
+    r = nff.RealNVP(8, hidden_dim=8)
+    monkeypatch.setattr(nff.NSF_CL, "_chain_shape",
+                        lambda self, dev: (4, 4, 8, self.K, float(self.B)))
+    monkeypatch.setattr(K_, "fused_nsf_chain_max", lambda *s: 3)
+    monkeypatch.setattr(config, "USE_FUSED", True)
+    monkeypatch.setattr(config, "USE_CHAIN", True)
+    flows = [a[0], a[1], r, a[2], a[3], a[4], b, a[0]]
+    m = nfm.NormalizingFlowModel(None, flows)
+    g = m._groups(m.flows, torch.device("cpu"), False)
+    kinds = [("run", [flows.index(f) for f in it[0]]) if isinstance(it, tuple) else ("one", flows.index(it))
+             for it in g]
+    assert kinds == [("run", [0, 1]), ("one", 2), ("run", [3, 4, 5]), ("one", 6), ("one", 0)]
+    assert g[0][1] == (4, 4, 8, 4, 3.0)
+    # longer than one launch: 5 same-shape layers with capacity 3 -> 3 + 2
+    m2 = nfm.NormalizingFlowModel(None, a)
+    g2 = m2._groups(m2.flows, torch.device("cpu"), False)
+    assert [len(it[0]) for it in g2] == [3, 2]
+    # capacity 1 (or 0): no chains at all
+    monkeypatch.setattr(K_, "fused_nsf_chain_max", lambda *s: 0)
+    assert m2._groups(m2.flows, torch.device("cpu"), False) == list(a)
+    assert m._groups(m.flows, torch.device("cpu"), True) == flows
+    monkeypatch.setattr(config, "USE_CHAIN", False)
+    assert m._groups(m.flows, torch.device("cpu"), False) == flows
