@@ -1,20 +1,34 @@
 #!/usr/bin/env python
 """Throughput of the log_prob hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c5]
+                    [--scaling weak|strong] [--batch B] [--global-batch G]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-A step = one NormalizingFlowModel.log_prob pass over one per-GPU batch of
-synthetic x ~ N(0, I) already resident in HBM (c3: 8 NSF_CL RQS coupling
-layers, D=64, K=8, H=100, B = 2^20 per GPU).  With N > 1 every rank owns its
-own 2^20 rows (weak scaling, sample sharding, BASELINE config 4) and the step
-ends with the NLL all-reduce of [sum log p, count] over RCCL.
+A step = one NormalizingFlowModel.log_prob pass over this rank's rows of
+synthetic x ~ N(0, I), already resident in HBM (c3: 8 NSF_CL RQS coupling
+layers, D=64, K=8, H=100).  Sample sharding, replicated weights:
+  --scaling weak   (default) every rank owns --batch rows (2^20): BASELINE
+                   config c4 (8M rows over 8 GPUs);
+  --scaling strong the --global-batch rows (2^20) are split over the ranks
+                   (dist.shard_range): the north star's strong-scaling target.
+With N > 1 each step ends with the NLL all-reduce of [sum log p, count]
+(RCCL; --backend gloo runs the same path over gloo, e.g. N ranks on one
+device in a test).  Status checks run deferred (config.STRICT_CHECKS =
+"deferred": no host sync per step; flushed, and raised, after the timed loop).
 
-Rank 0 prints ONE JSON line; `roofline` is computed for the dominant kernel
-from HIP events recorded live around its launches inside the timed region, and
-`cpu_baseline` times the CPU oracle (torch-CPU fp32 restatement of the
-reference path) on a bounded sample of the same workload on this host.
+Rank 0 prints ONE JSON line with:
+  roofline      the dominant kernel's time from HIP events recorded live on
+                its launch stream, against its binding floor: the larger of
+                the MFMA floor of its formulation and the VALU-issue floor
+                from its committed PMC instruction counts
+                (profiles/pmc_insts.json); traffic = PMC HBM bytes per launch
+  parity        the oracle's log_prob on the first --parity-rows rows of the
+                benched x and weights vs the values the timed kernel produced
+                (outside the timed region)
+  cpu_baseline  the CPU oracle (torch-CPU fp32 restatement of the reference
+                path) on a bounded sample of the same workload, best of 3
 """
 from __future__ import annotations
 
@@ -60,6 +74,18 @@ ARITH = {
     "c2": _SPLIT + "; 4-feature k-tail on f32 MFMA (nfk_fused_rnvp.hip)",
     "c5": _SPLIT + " (nfk_fused_wide.h)",
 }
+# the line's dtype: what the path computes in (fp32 values and outputs; the
+# conditioner's products on the fp16 matrix cores as a two-way split)
+DTYPE_FUSED = "fp32 (conditioner GEMMs: 3x fp16-split MFMA, fp32 accumulate; spline fp32)"
+PARITY_RTOL = 1e-5   # BASELINE.json north star: log_prob within 1e-5 relative (fp32)
+PARITY_ATOL = 1e-5   # ... with this absolute floor for values near 0 (tests/test_gpu_parity.py)
+CLOCK_GHZ = 2.4      # MI355X_MICROARCH.md: max engine clock
+N_SIMD = 1024        # 256 CUs x 4 SIMDs
+# VALU issue cost per wave64 instruction on one SIMD-32 with several waves
+# resident (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
+# cycles; transcendentals at twice the issue cost of v_fma_f32; an MFMA holds
+# the SIMD's vector issue for 8 cycles)
+VALU_CYC, TRANS_CYC, MFMA_HOLD_CYC = 2.0, 4.0, 8.0
 
 
 def build_model(workload, device):
@@ -89,8 +115,21 @@ def specs_for(workload):
     return orc.realnvp_specs(L, kw["dim"])
 
 
-def cpu_baseline(workload, sd, budget_s=10.0):
-    """Time the CPU oracle on a bounded sample (about budget_s of CPU work)."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(workload, sd, budget_s=15.0):
+    """Time the CPU oracle on a bounded sample (about budget_s of CPU work):
+    one warm-up that sizes the sample, then the best of 3 timed runs
+    (BASELINE.md's CPU-baseline plan)."""
     from oracle import nf_oracle as orc
     D = WORKLOADS[workload][3]
     specs = specs_for(workload)
@@ -100,74 +139,123 @@ def cpu_baseline(workload, sd, budget_s=10.0):
         t0 = time.perf_counter()
         orc.model_log_prob(specs, sd, x)  # warm-up + rate estimate
         t_w = time.perf_counter() - t0
-        n = int(max(4096, min(1 << 20, 4096 * budget_s / max(t_w, 1e-3))))
+        n = int(max(4096, min(1 << 20, 4096 * (budget_s / 3) / max(t_w, 1e-3))))
         n = (n // 4096) * 4096
         x = torch.randn(n, D, generator=g)
-        t0 = time.perf_counter()
-        orc.model_log_prob(specs, sd, x)
-        dt = time.perf_counter() - t0
+        runs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            orc.model_log_prob(specs, sd, x)
+            runs.append(time.perf_counter() - t0)
+    dt = min(runs)
     return {"value": n / dt, "unit": "samples/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "kind": "port", "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
+            "runs_s": [round(r, 3) for r in runs],
             "sample": "%s log_prob of %d x %d rows (seed 0) by the CPU oracle (oracle/nf_oracle.py: "
                       "torch-CPU fp32 restatement of nf/models.py:37 evaluate), %d threads, "
-                      "1 warm-up + 1 timed run, %.1f s" % (workload, n, D,
-                                                            torch.get_num_threads(), dt)}
+                      "1 warm-up + best of 3 timed runs (%.1f s best)"
+                      % (workload, n, D, torch.get_num_threads(), dt)}
+
+
+def parity(workload, sd, x_rows, lp_rows):
+    """The oracle on the first rows of the benched x (same weights) vs the
+    log_prob the benched kernel produced for them."""
+    from oracle import nf_oracle as orc
+    with torch.inference_mode():
+        ref = orc.model_log_prob(specs_for(workload), sd, x_rows)
+    d = (lp_rows.double() - ref.double()).abs()
+    rel = d / ref.double().abs().clamp_min(1e-30)
+    ok = bool((d <= PARITY_ATOL + PARITY_RTOL * ref.double().abs()).all())
+    return {"rows": int(x_rows.shape[0]), "max_rel_dlog_prob": float(rel.max()),
+            "max_abs_dlog_prob": float(d.max()), "rtol": PARITY_RTOL, "atol": PARITY_ATOL,
+            "pass": ok, "reference": "oracle/nf_oracle.py model_log_prob (pinned by tests/golden)"}
+
+
+def load_insts(kernel, workload):
+    """Per-launch PMC instruction counts of the kernel (profiles/pmc_insts.json,
+    entries "<workload>:<kernel>"), or None."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_insts.json")) as f:
+            return json.load(f).get("%s:%s" % (workload, kernel))
+    except (OSError, ValueError):
+        return None
+
+
+def valu_floor_ms(insts, per_launch_scale=1.0):
+    """VALU-issue floor of one launch: every SIMD's vector issue port busy for
+    the launch's VALU instructions (transcendentals at their higher cost) and
+    the cycles each MFMA holds it, spread over the 1024 SIMDs at the max clock."""
+    if not insts:
+        return None
+    cyc = (VALU_CYC * (insts["valu"] - insts["valu_trans"]) + TRANS_CYC * insts["valu_trans"]
+           + MFMA_HOLD_CYC * insts["mfma"]) * per_launch_scale
+    return cyc / N_SIMD / (CLOCK_GHZ * 1e9) * 1e3
+
+
+def _floors(flops_f16, flops_f32, B, per, insts, name, workload, n_steps):
+    """(bound, t_floor_ms, floors) of a fused kernel launch: the MFMA floor of
+    its formulation (every fp16-split product as 3 MFMAs at the dense fp16
+    rate, the k-tail on f32 MFMA) and, when its PMC instruction counts are
+    committed, the VALU-issue floor; the binding floor is the larger."""
+    t_mfma = (flops_f32 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * flops_f16 / (PEAK_FP16_TFLOPS * 1e12)) \
+        * B * per * 1e3
+    floors = {"mfma_ms": round(t_mfma, 4)}
+    t_valu = None
+    if insts:
+        scale = (B / insts["batch"]) * (per / insts.get("layers", 1))
+        t_valu = valu_floor_ms(insts, scale)
+        floors["valu_issue_ms"] = round(t_valu, 4)
+        floors["valu_basis"] = ("%.0f VALU (%.0f transcendental) + %.0f MFMA per launch of %d samples x "
+                                "%g layers (%s); %g cyc per VALU, %g per transcendental, %g per MFMA "
+                                "issue hold, on 1024 SIMDs at %.1f GHz"
+                                % (insts["valu"], insts["valu_trans"], insts["mfma"], insts["batch"],
+                                   insts.get("layers", 1), insts.get("source", "PMC"), VALU_CYC,
+                                   TRANS_CYC, MFMA_HOLD_CYC, CLOCK_GHZ))
+    if t_valu is not None and t_valu > t_mfma:
+        return "valu-issue", t_valu, floors
+    return "mfma", t_mfma, floors
 
 
 def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
-    """Roofline of the dominant kernel from live HIP-event timings."""
+    """Roofline of the dominant kernel from live HIP-event timings, against
+    the kernel's binding floor (see _floors)."""
     if not timer_summary:
         return None
     name, (n_launch, mean_ms, tot) = max(timer_summary.items(), key=lambda kv: kv[1][2])
-    n = n_launch
     desc, kind, kw, D, L = WORKLOADS[workload]
     B = per_gpu_batch
-    if name in ("nfk_fused_nsf", "nfk_fused_nsf_chain"):
-        # layers per launch: all L of a step in one chain launch (or one per launch)
-        per = L * n_steps / n_launch if name == "nfk_fused_nsf_chain" else 1
+    insts = load_insts(name, workload)
+    if name in ("nfk_fused_nsf", "nfk_fused_nsf_chain", "nfk_fused_realnvp"):
         H = kw["hidden_dim"]
-        n_lo = kw["size"]  # mask of one coordinate per particle (dim=2)
-        n_up = kw["size"] * (kw["dim"] - 1)
-        P = 3 * kw["K"] - 1
-        # the kernel's formulation (nfk_fused_impl.h): every product runs as a
-        # two-way fp16 split (3 MFMA products) except, when H = 32 KBH + R with
-        # 0 < R <= 4, the R-feature k-tail of layers 2-3 on exact f32 MFMA
         kbf, R = divmod(H, 32)
         tail = R if (0 < R <= 4 and kbf >= 1) else 0
-        f32 = 2.0 * tail * (H + n_up * P)
-        f16 = 2.0 * (n_lo * H + H * H + H * n_up * P) - f32
-        flops = (f16 + f32) * B * per            # SURVEY 8(d): 173,600/sample/layer (fp32-equivalent)
-        # MFMA-time floor of this formulation at the dense peak of the MFMA each
-        # part runs on, expressed as an fp32-equivalent TFLOP/s peak
-        t_floor = f32 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * f16 / (PEAK_FP16_TFLOPS * 1e12)
-        peak = (f16 + f32) / t_floor / 1e12
+        if name == "nfk_fused_realnvp":
+            per = 1
+            n = kw["dim"] // 2
+            f32 = 4 * 2.0 * tail * (H + n)                       # k-tails of layers 2-3, 4 nets
+            f16 = 4 * 2.0 * (n * H + H * H + H * n) - f32         # SURVEY 8(d): 131,200/sample
+        else:
+            # layers per launch: all L of a step in one chain launch (or one per launch)
+            per = L * n_steps / n_launch if name == "nfk_fused_nsf_chain" else 1
+            n_lo = kw["size"]  # mask of one coordinate per particle (dim=2)
+            n_up = kw["size"] * (kw["dim"] - 1)
+            P = 3 * kw["K"] - 1
+            f32 = 2.0 * tail * (H + n_up * P)
+            f16 = 2.0 * (n_lo * H + H * H + H * n_up * P) - f32  # SURVEY 8(d): 173,600/sample/layer
+        flops = (f16 + f32) * B * per
+        bound, t_floor, floors = _floors(f16, f32, B, per, insts, name, workload, n_steps)
         achieved = flops / (mean_ms * 1e-3) / 1e12
-        return {"kernel": name, "bound": "mfma", "achieved": round(achieved, 2),
-                "peak": round(peak, 1), "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic,
-                "launches": n, "mean_ms": round(mean_ms, 4),
+        peak = flops / (t_floor * 1e-3) / 1e12
+        return {"kernel": name, "bound": bound, "achieved": round(achieved, 2),
+                "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": traffic, "launches": n_launch, "mean_ms": round(mean_ms, 4),
+                "floor_ms": round(t_floor, 4), "floors": floors,
                 "per_launch": "%d samples x %g layers x %.0f flop (fp32-equivalent)"
                               % (B, per, flops / B / per),
-                "peak_basis": "MFMA floor: %.0f flop/sample as 3 fp16 products (%.1f TF dense) + "
-                              "%.0f flop/sample k-tail on f32 MFMA (%.1f TF)"
-                              % (f16, PEAK_FP16_TFLOPS, f32, PEAK_FP32_TFLOPS),
+                "peak_basis": "fp32-equivalent flop per launch / the binding floor; MFMA floor: "
+                              "%.0f flop/sample/layer as 3 fp16 products (%.1f TF dense) + %.0f on "
+                              "f32 MFMA (%.1f TF)" % (f16, PEAK_FP16_TFLOPS, f32, PEAK_FP32_TFLOPS),
                 "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
-    if name == "nfk_fused_realnvp":
-        H, n = kw["hidden_dim"], kw["dim"] // 2
-        kbf, R = divmod(H, 32)
-        tail = R if (0 < R <= 4 and kbf >= 1) else 0
-        f32 = 4 * 2.0 * tail * (H + n)                       # k-tails of layers 2-3, 4 nets
-        f16 = 4 * 2.0 * (n * H + H * H + H * n) - f32         # SURVEY 8(d): 131,200/sample
-        flops = (f16 + f32) * B
-        t_floor = f32 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * f16 / (PEAK_FP16_TFLOPS * 1e12)
-        peak = (f16 + f32) / t_floor / 1e12
-        achieved = flops / (mean_ms * 1e-3) / 1e12
-        return {"kernel": name, "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                "launches": n_launch, "mean_ms": round(mean_ms, 4),
-                "per_launch": "%d samples x %.0f flop (fp32-equivalent)" % (B, flops / B),
-                "peak_basis": "MFMA floor: %.0f flop/sample as 3 fp16 products + %.0f on f32 MFMA"
-                              % (f16, f32)}
     if name == "nfk_rqs_coupling":
         n_up = kw["size"] * (kw["dim"] - 1)
         P = 3 * kw["K"] - 1
@@ -182,7 +270,7 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
     achieved = byts / (mean_ms * 1e-3) / 1e9
     return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-            "launches": n, "mean_ms": round(mean_ms, 4),
+            "launches": n_launch, "mean_ms": round(mean_ms, 4),
             "per_launch": "%d samples x %.0f B" % (B, byts / B)}
 
 
@@ -208,40 +296,63 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--batch", type=int, default=1 << 20, help="samples per GPU")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: --batch rows per GPU; strong: --global-batch rows split over the GPUs")
+    ap.add_argument("--batch", type=int, default=1 << 20, help="samples per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=1 << 20, help="samples in all (strong scaling)")
+    ap.add_argument("--backend", default=None, choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (default: nccl = RCCL)")
+    ap.add_argument("--parity-rows", type=int, default=None,
+                    help="rows checked against the CPU oracle after the timed loop (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timer", action="store_true", help="skip the per-kernel event timer")
     ap.add_argument("--unfused", action="store_true", help="disable the fused MFMA layer kernel")
     ap.add_argument("--no-chain", action="store_true",
                     help="one fused launch per layer instead of one chained launch per run of layers")
+    ap.add_argument("--sync-checks", action="store_true",
+                    help="status checks with a host sync per call (config.STRICT_CHECKS = True)")
     args = ap.parse_args()
 
     from normalizingflow_amd import config, dist as nfdist, kernels
+    from normalizingflow_amd import flush_status_checks
     import torch.distributed as dist
 
-    rank, world, local = nfdist.init_from_env()
+    rank, world, local = nfdist.init_from_env(backend=args.backend)
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    device = torch.device("cuda", local)
+    # gloo runs share one device when there are fewer devices than ranks (tests)
+    ndev = torch.cuda.device_count()
+    device = torch.device("cuda", local if local < ndev else local % max(ndev, 1))
     torch.cuda.set_device(device)
     config.USE_FUSED = not args.unfused
     config.USE_CHAIN = not args.no_chain
+    config.STRICT_CHECKS = True if args.sync_checks else "deferred"
 
     model, sd, _ = build_model(args.workload, device)
-    B = args.batch
     D = WORKLOADS[args.workload][3]
+    if args.scaling == "strong":
+        lo, hi = nfdist.shard_range(args.global_batch, rank, world)
+        B = hi - lo
+        total = args.global_batch
+    else:
+        B = args.batch
+        total = world * B
     g = torch.Generator(device=device).manual_seed(rank)
     x = torch.randn(B, D, generator=g, device=device)  # resident in HBM before timing
 
+    nll = None
+
     def step():
+        nonlocal nll
         lp = model.log_prob(x)
         if world > 1:
-            nfdist.nll_allreduce(lp)
+            nll = nfdist.nll_allreduce(lp)
         return lp
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    flush_status_checks()
     timer = None
     if not args.no_timer:
         timer = kernels.TIMER = kernels.KernelTimer()
@@ -250,12 +361,13 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        lp = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     kernels.TIMER = None
+    flush_status_checks()  # the reference's errors, if any step raised one
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -263,13 +375,20 @@ def main():
     summary = timer.summary() if timer is not None else {}
 
     if rank == 0:
-        value = world * B * args.steps / dt
+        value = total * args.steps / dt
         dom = max(summary.items(), key=lambda kv: kv[1][2])[0] if summary else None
         rl = roofline(args.workload, summary, B, load_traffic(dom, args.workload) if dom else None,
                       args.steps)
+        sd_cpu = {k: v.cpu() for k, v in sd.items()}
+        n_par = args.parity_rows if args.parity_rows is not None else \
+            (4096 if args.workload == "c5" else 16384)
+        par = None
+        if n_par > 0:
+            n_par = min(n_par, B)
+            par = parity(args.workload, sd_cpu, x[:n_par].cpu(), lp[:n_par].cpu())
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
-            cpu = cpu_baseline(args.workload, {k: v.cpu() for k, v in sd.items()})
+            cpu = cpu_baseline(args.workload, sd_cpu)
         desc = WORKLOADS[args.workload][0]
         out = {
             "metric": METRICS[args.workload],
@@ -280,18 +399,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": DTYPE_FUSED if config.USE_FUSED else "fp32",
             "data": "synthetic x ~ N(0, I) resident in HBM; random-init weights (seed 1234)",
-            "config": {"workload": args.workload + ": " + desc, "global_batch": world * B,
+            "config": {"workload": args.workload + ": " + desc, "global_batch": total,
                        "per_gpu_batch": B, "parallelism": "dp%d (sample sharding)" % world,
+                       "scaling": args.scaling,
+                       "backend": (args.backend or "nccl") if world > 1 else None,
                        "fused_layer_kernel": bool(config.USE_FUSED),
                        "chained_layers": bool(config.USE_FUSED and config.USE_CHAIN),
+                       "status_checks": "sync per call" if args.sync_checks else
+                       "deferred (no host sync per step; flushed after the timed loop)",
                        "conditioner_arith": ARITH.get(args.workload) if config.USE_FUSED
                        else "f32 (rocBLAS)"},
             "roofline": rl,
+            "parity": par,
             "cpu_baseline": cpu,
+            "nll": None if nll is None else float(nll),
             "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4)} for k, v in summary.items()},
         }
         print(json.dumps(out), flush=True)

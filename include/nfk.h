@@ -31,7 +31,7 @@ extern "C" {
 
 typedef void* nfk_stream_t; /* hipStream_t */
 
-#define NFK_ABI_VERSION 1
+#define NFK_ABI_VERSION 2
 #define NFK_EINVAL (-1)
 
 /* status bits, OR-ed into *status by the kernels */
@@ -39,6 +39,9 @@ typedef void* nfk_stream_t; /* hipStream_t */
                                 RuntimeError from torch.min of an empty tensor (utils.py:63) */
 #define NFK_ST_NEG_DISC 2    /* negative discriminant in an inverse spline: the
                                 reference's AssertionError (utils.py:121) */
+#define NFK_ST_NAN_Z 4       /* a NaN in z reached the Normal prior: the reference's
+                                ValueError from torch's MultivariateNormal argument
+                                validation (prior.log_prob, nf/models.py:19) */
 
 int nfk_abi_version(void);
 const char* nfk_last_error(void);
@@ -169,10 +172,12 @@ int nfk_radial_apply(const float* x, int64_t ldx, const float* x0, const float* 
  *            + sign * logdet[b]          (logdet nullable; sign = +1 or -1)
  * scale = the prior's Cholesky diagonal sqrt(var) (its scale_tril), and
  * half_log_det = sum_i log(scale) are passed in as torch evaluates them.
+ *   status: nullable; NFK_ST_NAN_Z is OR-ed in when a row of z holds a NaN
+ *           (torch validates the prior's argument: ValueError).
  * ------------------------------------------------------------------------- */
 int nfk_normal_logprob(const float* z, int64_t ldz, const float* logdet, float* out,
                        int64_t batch, int32_t dim, float scale, float half_log_det,
-                       int32_t sign, nfk_stream_t stream);
+                       int32_t sign, int32_t* status, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * NSF_AR conditioner features (nf/flows.py:172-173, 183):
@@ -223,7 +228,8 @@ int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t
  *           log_prob[b] = log N(z_b; 0, prior_scale^2 I) + log|det|_b with
  *           prior_half_log_det = sum log(scale_tril diagonal) as torch has it
  *           (the constants of nfk_normal_logprob).  With log_prob given, z may
- *           be NULL (not written) and logdet NULL with logdet_mode 0.
+ *           be NULL (not written) and logdet NULL with logdet_mode 0; a NaN in
+ *           z ORs NFK_ST_NAN_Z into status[0].
  * nlayers <= nfk_fused_nsf_chain_max() (0: shape not supported by the chain
  * form); x, z 16-byte aligned with ldx, ldz multiples of 4.
  * ------------------------------------------------------------------------- */

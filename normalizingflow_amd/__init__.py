@@ -10,6 +10,7 @@ from . import config  # noqa: F401
 from ._lib import LIB_PATH, load as load_library  # noqa: F401
 from .flows import FCNN, NSF_AR, NSF_CL, Planar, Radial, RealNVP  # noqa: F401
 from .flows import MAF, ActNorm, OneByOneConv  # noqa: F401
+from .flows import flush_status_checks  # noqa: F401
 from .models import NormalizingFlow, NormalizingFlowModel  # noqa: F401
 
 __version__ = "0.1.0"

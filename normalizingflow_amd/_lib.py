@@ -11,11 +11,12 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NFK_LIBRARY", os.path.join(_HERE, "libnfk.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 NFK_EINVAL = -1
 ST_INSIDE_SEEN = 1
 ST_NEG_DISC = 2
+ST_NAN_Z = 4
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
@@ -58,7 +59,7 @@ SIGNATURES = {
     "nfk_radial_workspace_elems": (ctypes.c_int64, []),
     "nfk_radial_sumsq": (ctypes.c_int, [P, I64, P, I64, I32, P, P, P]),
     "nfk_radial_apply": (ctypes.c_int, [P, I64, P, P, P, P, P, I64, P, P, I32, I64, I32, P]),
-    "nfk_normal_logprob": (ctypes.c_int, [P, I64, P, P, I64, I32, F32, F32, I32, P]),
+    "nfk_normal_logprob": (ctypes.c_int, [P, I64, P, P, I64, I32, F32, F32, I32, P, P]),
     "nfk_trig_features": (ctypes.c_int, [P, I64, P, I64, I64, I32, F64, P]),
     "nfk_fused_nsf_supported": (ctypes.c_int, [I32, I32, I32, I32]),
     "nfk_fused_nsf_pack_elems": (ctypes.c_int64, [I32, I32, I32, I32]),

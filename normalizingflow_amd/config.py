@@ -2,9 +2,14 @@
 
 STRICT_CHECKS  raise the reference's data-dependent errors (RuntimeError when a
                spline layer has no element inside [-B, B], AssertionError on a
-               negative discriminant) after each top-level call.  Costs one
-               device->host read of the status words per call; the kernels
-               themselves never sync.
+               negative discriminant, ValueError when a NaN z reaches a
+               validating Normal prior) from the kernels' status words.
+               True: after each top-level call (one device->host read, which
+               waits for the call's kernels).  "deferred": the words are copied
+               to pinned memory without a sync and their errors raised at a
+               later call once they have landed, or by
+               flows.flush_status_checks() -- the device queue never drains for
+               a check (bench.py's mode).  False: never checked.
 USE_FUSED      run NSF_CL layers whose conditioner is the stock FCNN through the
                fused MFMA kernel (nfk_fused_nsf) when the shape is supported;
                otherwise conditioner GEMMs + the streaming spline kernel.

@@ -512,10 +512,12 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
     // (nfk_prefix_nsf_lean2, NFK_PK2; bitwise the per-coordinate result)
     constexpr bool PAIRS = PK && NFK_PK2 && K <= 8 && (R1 - R0) % 2 == 0;
     int pre2[K];
+    float s2b = 0.0f;
 #pragma unroll
     for (int r = R0; r < R1; ++r) {
         float u[K];
         int pre[K];
+        float s2;  // the second softmax's sum: NaN iff a logit was NaN
 #pragma unroll
         for (int t = 0; t < K; ++t) u[t] = acc[t][r];
         if constexpr (PAIRS) {
@@ -523,14 +525,20 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
                 float u1[K];
 #pragma unroll
                 for (int t = 0; t < K; ++t) u1[t] = acc[t][r + 1];
-                nfk_prefix_nsf_lean2<K>(u, u1, l2e, c.m2b, c.fb30, c.mb30, pre, pre2);
+                const nfk_f2 s = nfk_prefix_nsf_lean2<K>(u, u1, l2e, c.m2b, c.fb30, c.mb30, pre, pre2);
+                s2 = s.x;
+                s2b = s.y;
             } else {
 #pragma unroll
                 for (int t = 0; t < K; ++t) pre[t] = pre2[t];
+                s2 = s2b;
             }
         } else {
-            nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
+            s2 = nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
         }
+        // the knot range's left end, NaN iff the logits were: the reference's NaN
+        // cumsum makes every edge NaN (the integer prefixes would drop it)
+        const float lo = __builtin_fmaf(s2, 0.0f, c.lo);
         int p0 = 0, p1 = pre[1 < K ? 1 : 0];
         if (SEARCH) {
             const int xi = __float2int_rd(__builtin_fmaf(xv[r], c.inv30, -c.lo * c.inv30));
@@ -554,8 +562,8 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
                 if (j + 1 < K) p1 = ge ? pre[j + 1] : p1;
             }
         }
-        const float e = __builtin_fmaf(c.sp30, (float)p0, c.lo);
-        const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, c.lo);
+        const float e = __builtin_fmaf(c.sp30, (float)p0, lo);
+        const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, lo);
         ek[r] = e;
         sk[r] = e1 - e;
         // wide layers (K = 16): one coordinate at a time, or the scheduler
@@ -1204,6 +1212,8 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
             m += __shfl_xor(m, 32, 64);
             const float lp = -0.5f * (A->prior_c2pi + m) - A->prior_hld;
             if (q == 0 && row_ok) A->log_prob[b0 + sl] = lp + ld_acc;
+            // a NaN in z (m NaN): the prior's argument validation raises (NFK_ST_NAN_Z)
+            if (__any(row_ok && m != m) && lane == 0) atomicOr(cst, NFK_ST_NAN_Z);
         }
     }
     if constexpr (CHAIN) {

@@ -203,7 +203,8 @@ __device__ __forceinline__ void knot_phase_w(const f32x4 (&acc)[K / 2], const fl
         int pre[K];
 #pragma unroll
         for (int p = 0; p < K; ++p) u[p] = acc[p >> 1][2 * h + (p & 1)];
-        nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
+        const float s2 = nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
+        const float lo = __builtin_fmaf(s2, 0.0f, c.lo);  // NaN iff the logits were (knot_phase)
         int p0 = 0, p1 = pre[1 < K ? 1 : 0], k = 0;
         const int xi = __float2int_rd(__builtin_fmaf(xv[h], c.inv30, -c.lo * c.inv30));
 #pragma unroll
@@ -215,8 +216,8 @@ __device__ __forceinline__ void knot_phase_w(const f32x4 (&acc)[K / 2], const fl
         }
         if (SEARCH) kb[h] = k;
         const int kk = kb[h];
-        const float e = __builtin_fmaf(c.sp30, (float)p0, c.lo);
-        const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, c.lo);
+        const float e = __builtin_fmaf(c.sp30, (float)p0, lo);
+        const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, lo);
         ek[h] = e;
         sk[h] = e1 - e;
         if constexpr (K > 8) __builtin_amdgcn_sched_barrier(0);  // one coordinate's temporaries at a time

@@ -823,7 +823,7 @@ template <int W>
 __global__ __launch_bounds__(256) void k_normal_lp(const float* __restrict__ z, int64_t ldz,
                                                    const float* __restrict__ logdet, float* out,
                                                    int64_t batch, int dim, float lii, float c2pi,
-                                                   float hld, int sign) {
+                                                   float hld, int sign, int32_t* status) {
     NFK_ROW_PROLOGUE(W)
     for (int64_t r0 = wave * RPW; r0 < batch; r0 += nwave * RPW) {
         const int64_t b = r0 + sub;
@@ -840,6 +840,9 @@ __global__ __launch_bounds__(256) void k_normal_lp(const float* __restrict__ z, 
             if (logdet) lp = (sign >= 0) ? (lp + logdet[b]) : (lp - logdet[b]);
             out[b] = lp;
         }
+        // a NaN in the row makes m NaN (squares of infinities stay infinite)
+        if (__any(ok && c0 == 0 && m != m) && status != nullptr && (threadIdx.x & 63) == 0)
+            atomicOr(status, NFK_ST_NAN_Z);
     }
 }
 
@@ -849,7 +852,7 @@ template <int W>
 __global__ __launch_bounds__(256) void k_normal_lp4(const float4* __restrict__ z4, int64_t ldz4,
                                                     const float* __restrict__ logdet, float* out,
                                                     int64_t batch, int dim4, float inv_l, float c2pi,
-                                                    float hld, int sign) {
+                                                    float hld, int sign, int32_t* status) {
     NFK_ROW_PROLOGUE(W)
     for (int64_t r0 = wave * RPW; r0 < batch; r0 += nwave * RPW) {
         const int64_t b = r0 + sub;
@@ -867,12 +870,15 @@ __global__ __launch_bounds__(256) void k_normal_lp4(const float4* __restrict__ z
             if (logdet) lp = (sign >= 0) ? (lp + logdet[b]) : (lp - logdet[b]);
             out[b] = lp;
         }
+        // a NaN in the row makes m NaN (squares of infinities stay infinite)
+        if (__any(ok && c0 == 0 && m != m) && status != nullptr && (threadIdx.x & 63) == 0)
+            atomicOr(status, NFK_ST_NAN_Z);
     }
 }
 
 extern "C" int nfk_normal_logprob(const float* z, int64_t ldz, const float* logdet, float* out,
                                   int64_t batch, int32_t dim, float scale, float half_log_det,
-                                  int32_t sign, nfk_stream_t stream) {
+                                  int32_t sign, int32_t* status, nfk_stream_t stream) {
     if (batch < 0 || dim <= 0 || !(scale > 0.0f)) return nfk_set_error("nfk_normal_logprob: bad args");
     if (batch == 0) return 0;
     if (!z || !out) return nfk_set_error("nfk_normal_logprob: null pointer");
@@ -886,7 +892,7 @@ extern "C" int nfk_normal_logprob(const float* z, int64_t ldz, const float* logd
         const float inv_l = 1.0f / lii;
 #define CALL4(W)                                                                                   \
     hipLaunchKernelGGL((k_normal_lp4<W>), dim3(g4), dim3(256), 0, st, (const float4*)z, ldz / 4, logdet, \
-                       out, batch, dim4, inv_l, c2pi, half_log_det, sign);
+                       out, batch, dim4, inv_l, c2pi, half_log_det, sign, status);
         NFK_W_DISPATCH(w4, CALL4)
 #undef CALL4
         return launch_status("nfk_normal_logprob");
@@ -895,7 +901,7 @@ extern "C" int nfk_normal_logprob(const float* z, int64_t ldz, const float* logd
     const unsigned g = grid_for_rows(batch, w);
 #define CALL(W)                                                                                 \
     hipLaunchKernelGGL((k_normal_lp<W>), dim3(g), dim3(256), 0, st, z, ldz, logdet, out, batch, dim, \
-                       lii, c2pi, half_log_det, sign);
+                       lii, c2pi, half_log_det, sign, status);
     NFK_W_DISPATCH(w, CALL)
 #undef CALL
     return launch_status("nfk_normal_logprob");

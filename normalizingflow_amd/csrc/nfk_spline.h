@@ -165,9 +165,14 @@ __device__ __forceinline__ float nfk_sum(const float (&v)[K]) {
 #endif
 }
 
+// Returns the second softmax's sum s2 (in [1, K] for finite logits, NaN if a
+// logit is NaN): the integer prefixes cannot carry a NaN, so callers place the
+// knot edges at fma(s2, 0, lo) + ..., which is lo exactly unless the logits
+// were NaN -- then the edges, and everything the reference computes from its
+// NaN cumsum (utils.py:73-91), are NaN too.
 template <int K>
-__device__ __forceinline__ void nfk_prefix_nsf_lean(const float (&raw)[K], float l2e, float m2b,
-                                                    float fb30, float mb30, int (&pre)[K]) {
+__device__ __forceinline__ float nfk_prefix_nsf_lean(const float (&raw)[K], float l2e, float m2b,
+                                                     float fb30, float mb30, int (&pre)[K]) {
     float m = raw[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) m = fmaxf(m, raw[i]);
@@ -183,6 +188,7 @@ __device__ __forceinline__ void nfk_prefix_nsf_lean(const float (&raw)[K], float
     pre[0] = 0;
 #pragma unroll
     for (int i = 0; i < K - 1; ++i) pre[i + 1] = pre[i] + (int)__builtin_fmaf(e[i], f30, mb30);
+    return s2;
 }
 
 // nfk_prefix_nsf_lean for two coordinates at once: the fp32 FMAs, multiplies
@@ -212,9 +218,9 @@ __device__ __forceinline__ nfk_f2 nfk_sum2(const nfk_f2 (&v)[K]) {
 }
 
 template <int K>
-__device__ __forceinline__ void nfk_prefix_nsf_lean2(const float (&raw0)[K], const float (&raw1)[K], float l2e,
-                                                     float m2b, float fb30, float mb30, int (&pre0)[K],
-                                                     int (&pre1)[K]) {
+__device__ __forceinline__ nfk_f2 nfk_prefix_nsf_lean2(const float (&raw0)[K], const float (&raw1)[K], float l2e,
+                                                       float m2b, float fb30, float mb30, int (&pre0)[K],
+                                                       int (&pre1)[K]) {
     float m0 = raw0[0], m1 = raw1[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) {
@@ -248,6 +254,7 @@ __device__ __forceinline__ void nfk_prefix_nsf_lean2(const float (&raw0)[K], con
         pre0[i + 1] = pre0[i] + (int)f.x;
         pre1[i + 1] = pre1[i] + (int)f.y;
     }
+    return s2;
 }
 
 // min_d + softplus(softplus(v)) of NSF_CL + RQS (flows.py:235, utils.py:82) in
@@ -460,7 +467,8 @@ __device__ __forceinline__ void nfk_rqs_element(float x, float (&wr)[K], float (
 // agrees.
 template <int K>
 __device__ __forceinline__ void nfk_lean_bin_edges(const int (&pre)[K], int k, const NfkSplineConst& c,
-                                                   float sp30, float& e0, float& sz) {
+                                                   float sp30, float s2, float& e0, float& sz) {
+    const float lo = __builtin_fmaf(s2, 0.0f, c.lo);  // NaN iff the logits were (nfk_prefix_nsf_lean)
     int p0 = 0, p1 = pre[1 < K ? 1 : 0];
 #pragma unroll
     for (int j = 1; j < K; ++j) {
@@ -468,8 +476,8 @@ __device__ __forceinline__ void nfk_lean_bin_edges(const int (&pre)[K], int k, c
         p0 = ge ? pre[j] : p0;
         if (j + 1 < K) p1 = ge ? pre[j + 1] : p1;
     }
-    e0 = __builtin_fmaf(sp30, (float)p0, c.lo);
-    const float e1 = (k == K - 1) ? c.hi : __builtin_fmaf(sp30, (float)p1, c.lo);
+    e0 = __builtin_fmaf(sp30, (float)p0, lo);
+    const float e1 = (k == K - 1) ? c.hi : __builtin_fmaf(sp30, (float)p1, lo);
     sz = e1 - e0;
 }
 
@@ -484,15 +492,15 @@ __device__ __forceinline__ void nfk_rqs_element_lean(float x, const float (&wr)[
     const float sp30 = c.span * (1.0f / two30), inv30 = two30 / c.span;
     const float fb30 = c.fw * two30, mb30 = c.min_w * two30;
     int pw[K], ph[K];
-    nfk_prefix_nsf_lean<K>(wr, kL2E, c.m2b, fb30, mb30, pw);
-    nfk_prefix_nsf_lean<K>(hr, kL2E, c.m2b, fb30, mb30, ph);
+    const float sw = nfk_prefix_nsf_lean<K>(wr, kL2E, c.m2b, fb30, mb30, pw);
+    const float sh = nfk_prefix_nsf_lean<K>(hr, kL2E, c.m2b, fb30, mb30, ph);
     const int xi = __float2int_rd(__builtin_fmaf(x, inv30, -c.lo * inv30));
     int k = 0;
 #pragma unroll
     for (int j = 1; j < K; ++j) k += (xi >= (INV ? ph[j] : pw[j])) ? 1 : 0;
     float cw_k, w_k, ch_k, h_k;
-    nfk_lean_bin_edges<K>(pw, k, c, sp30, cw_k, w_k);
-    nfk_lean_bin_edges<K>(ph, k, c, sp30, ch_k, h_k);
+    nfk_lean_bin_edges<K>(pw, k, c, sp30, sw, cw_k, w_k);
+    nfk_lean_bin_edges<K>(ph, k, c, sp30, sh, ch_k, h_k);
     // padded derivative index j+1 holds logit j (utils.py:36-39)
     float raw_k = dr[0], raw_k1 = dr[0];
 #pragma unroll

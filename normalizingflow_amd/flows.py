@@ -27,6 +27,8 @@ gradient checkpointing).  Hand-written backward kernels are the next step.
 """
 from __future__ import annotations
 
+import collections
+
 import math
 import warnings
 
@@ -40,7 +42,7 @@ from . import config
 from . import kernels as K_
 from . import split_gemm
 from . import torch_math
-from ._lib import ST_INSIDE_SEEN, ST_NEG_DISC
+from ._lib import ST_INSIDE_SEEN, ST_NAN_Z, ST_NEG_DISC
 
 __all__ = ["FCNN", "RealNVP", "NSF_AR", "NSF_CL", "Planar", "Radial", "MAF", "ActNorm",
            "OneByOneConv", "functional_derivatives"]
@@ -109,17 +111,99 @@ def _check_input(x, what="x"):
     return x
 
 
-def raise_on_status(status, n_slots=None):
-    """Reference-compatible errors from the kernels' status words (one sync)."""
+def raise_on_status(status, n_slots=None, prior=None):
+    """Reference-compatible errors from the kernels' status words (one sync).
+
+    Slots [0, n_slots) are the spline layers' words in execution order; each
+    raises what its reference layer would, in the reference's order: no
+    element inside the tails first (torch.min of an empty tensor in RQS,
+    utils.py:63), then a negative discriminant (utils.py:121).  NFK_ST_NAN_Z
+    in any word (a NaN in z reached the Normal prior) raises torch's
+    ValueError when ``prior`` validates its arguments (MultivariateNormal's
+    support check in prior.log_prob, models.py:19), after every layer."""
     if status is None:
         return
-    st = status[:n_slots].cpu() if n_slots is not None else status.cpu()
-    if bool(((st & ST_NEG_DISC) != 0).any()):
-        raise AssertionError("negative discriminant in the inverse rational-quadratic spline "
-                             "(nf/utils.py:121)")
-    if bool(((st & ST_INSIDE_SEEN) == 0).any()):
-        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
-                           "(no element inside the spline interval [-B, B], nf/utils.py:63)")
+    st = status.cpu().tolist()
+    n = len(st) if n_slots is None else n_slots
+    for w in st[:n]:
+        if not w & ST_INSIDE_SEEN:
+            raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
+                               "(no element inside the spline interval [-B, B], nf/utils.py:63)")
+        if w & ST_NEG_DISC:
+            raise AssertionError("negative discriminant in the inverse rational-quadratic spline "
+                                 "(nf/utils.py:121)")
+    if prior is not None and getattr(prior, "_validate_args", False) \
+            and any(w & ST_NAN_Z for w in st):
+        raise ValueError("Expected value argument to be within the support (IndependentConstraint("
+                         "Real(), 1)) of the distribution %s, but found invalid values (NaN in z)"
+                         % type(prior).__name__)
+
+
+class _StatusQueue:
+    """config.STRICT_CHECKS == "deferred": a call's status words are copied to
+    pinned host memory without a sync (a copy and an event on the call's
+    stream); the errors they hold are raised at the start of a later checked
+    call once the copy has landed, or by flush_status_checks().  The GPU queue
+    is never drained for a check, so back-to-back calls keep the device busy."""
+
+    MAX_PENDING = 64
+
+    def __init__(self):
+        self.pending = collections.deque()
+        self.free = {}
+
+    def _host(self, n):
+        lst = self.free.get(n)
+        return lst.pop() if lst else torch.empty(n, dtype=torch.int32, pin_memory=True)
+
+    def push(self, status, n_slots, prior):
+        h = self._host(status.numel())
+        h.copy_(status, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(status.device))
+        self.pending.append((ev, h, n_slots, prior))
+        if len(self.pending) > self.MAX_PENDING:
+            self.poll(block=True, upto=len(self.pending) - self.MAX_PENDING)
+
+    def poll(self, block=False, upto=None):
+        done = 0
+        while self.pending and (upto is None or done < upto):
+            ev, h, n, prior = self.pending[0]
+            if not block and not ev.query():
+                break
+            ev.synchronize()
+            self.pending.popleft()
+            done += 1
+            vals = h.clone()
+            self.free.setdefault(h.numel(), []).append(h)
+            raise_on_status(vals, n, prior)
+
+
+_STATUS_QUEUE = _StatusQueue()
+
+
+def check_status(status, n_slots=None, prior=None):
+    """Raise the reference's errors for ``status`` per config.STRICT_CHECKS:
+    True -> now (one device->host read, which waits for the kernels);
+    "deferred" -> at a later call or flush_status_checks(); False -> never."""
+    mode = config.STRICT_CHECKS
+    if not mode or status is None:
+        return
+    if mode == "deferred":
+        _STATUS_QUEUE.poll()
+        _STATUS_QUEUE.push(status, n_slots, prior)
+    else:
+        raise_on_status(status, n_slots, prior)
+
+
+def flush_status_checks():
+    """Wait for every deferred status check and raise the first error found."""
+    _STATUS_QUEUE.poll(block=True)
+
+
+def _invalidate_after_load(module, _incompatible_keys):
+    """load_state_dict post-hook (a module-level function, so modules still pickle)."""
+    module.invalidate_caches()
 
 
 class _HipFlow(nn.Module):
@@ -131,6 +215,23 @@ class _HipFlow(nn.Module):
     are needed per call (spline layers only).
     """
     _n_status = 0
+
+    def __init__(self):
+        super().__init__()
+        # load_state_dict copies in place (a version bump the caches see), but
+        # assign=True swaps tensors: drop the derived state either way
+        self.register_load_state_dict_post_hook(_invalidate_after_load)
+
+    def invalidate_caches(self):
+        """Drop state derived from the parameters (fused weight packs, cached
+        inverses).  The caches are keyed on each parameter's storage and
+        version counter, which every autograd-visible in-place update
+        (optimizer steps, ``with torch.no_grad(): p.add_(...)``,
+        ``load_state_dict``) bumps.  Writes through ``p.data`` do not bump it:
+        call this (or NormalizingFlowModel.invalidate_caches) after them."""
+        for name in ("_pack_cache", "_winv_key"):
+            if name in self.__dict__:
+                self.__dict__[name] = None
 
     def _run(self, x, inverse, logdet, mode, status):
         raise NotImplementedError
@@ -154,8 +255,8 @@ class _HipFlow(nn.Module):
                                        *(t for _, t in named))
         else:
             z, logdet = self._eval(x, inverse, st)
-        if status is None and st is not None and config.STRICT_CHECKS:
-            raise_on_status(st)
+        if status is None and st is not None:
+            check_status(st)
         return z, logdet
 
 

@@ -277,12 +277,13 @@ def iso_normal_consts(var, dim):
     return float(L[0, 0]), float(L.diagonal().log().sum())
 
 
-def normal_logprob(z, out, *, scale=1.0, hld=0.0, logdet=None, sign=1):
-    dev = _require_hip(z, out, logdet)
+def normal_logprob(z, out, *, scale=1.0, hld=0.0, logdet=None, sign=1, status=None):
+    """``status`` (optional int32 word): NFK_ST_NAN_Z is OR-ed in when z holds a NaN."""
+    dev = _require_hip(z, out, logdet, status)
     B, D = z.shape
     zp, ldz = _mat(z, "z")
     _timed("nfk_normal_logprob", dev, "nfk_normal_logprob", zp, ldz, _vec(logdet, B, "logdet"), _vec(out, B, "out"), B, D,
-              float(scale), float(hld), int(sign), _stream(dev))
+              float(scale), float(hld), int(sign), _vec(status, 1, "status", torch.int32), _stream(dev))
 
 
 def trig_features(x, feat, B):

@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from . import config
 from . import kernels as K_
-from .flows import NSF_CL, _HipFlow, _check_input, _needs_grad, raise_on_status
+from .flows import NSF_CL, _HipFlow, _check_input, _invalidate_after_load, _needs_grad, check_status
 
 __all__ = ["NormalizingFlowModel", "NormalizingFlow"]
 
@@ -47,9 +47,9 @@ class _NormalLogProbFn(torch.autograd.Function):
     z: d/dz = -z / s^2 (the values are those of the inference path)."""
 
     @staticmethod
-    def forward(ctx, z, scale, hld):
+    def forward(ctx, z, scale, hld, status):
         out = torch.empty(z.shape[0], dtype=torch.float32, device=z.device)
-        K_.normal_logprob(z, out, scale=scale, hld=hld)
+        K_.normal_logprob(z, out, scale=scale, hld=hld, status=status)
         ctx.save_for_backward(z)
         ctx.inv_var = 1.0 / (scale * scale)
         return out
@@ -57,7 +57,7 @@ class _NormalLogProbFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         z, = ctx.saved_tensors
-        return g[:, None] * z * (-ctx.inv_var), None, None
+        return g[:, None] * z * (-ctx.inv_var), None, None, None
 
 
 def _compose_maps(run, D, device):
@@ -93,6 +93,22 @@ class NormalizingFlowModel(nn.Module):
         self._prior_iso = None
         self._chain_cache = {}
         self._lp_plan_cache = None
+        self.register_load_state_dict_post_hook(_invalidate_after_load)
+
+    def invalidate_caches(self):
+        """Drop every cached derivative of the parameters and the prior: the
+        layers' fused weight packs, the chained-launch arguments and the
+        one-launch log_prob plan.  Needed only after writes the version
+        counters cannot see (``p.data.copy_(...)``, ``p.data -= lr * g``, EMA
+        updates through ``.data``); optimizer steps and load_state_dict are
+        tracked automatically."""
+        for f in self.flows:
+            if isinstance(f, _HipFlow):
+                f.invalidate_caches()
+        self._chain_cache = {}
+        self._lp_plan_cache = None
+        self._prior_key = None
+        self._prior_iso = None
 
     # ------------------------------------------------------------------ prior
     def _prior_consts(self):
@@ -104,15 +120,20 @@ class NormalizingFlowModel(nn.Module):
             self._prior_key = key
         return self._prior_iso
 
-    def _prior_log_prob(self, z, logdet=None, sign=1):
+    def _prior_log_prob(self, z, logdet=None, sign=1, status=None):
+        """log prior(z) (+ sign * logdet).  The kernel path ORs NFK_ST_NAN_Z into
+        ``status`` (one int32 word) on a NaN z, which the caller's status check
+        turns into the ValueError of torch's argument validation; any other
+        prior is called as is and validates by itself."""
         iso = self._prior_consts()
         if iso is not None and z.shape[1] == self.prior.loc.shape[0]:
             if not (torch.is_grad_enabled() and z.requires_grad):
                 out = torch.empty(z.shape[0], dtype=torch.float32, device=z.device)
-                K_.normal_logprob(z, out, scale=iso[0], hld=iso[1], logdet=logdet, sign=sign)
+                K_.normal_logprob(z, out, scale=iso[0], hld=iso[1], logdet=logdet, sign=sign,
+                                  status=status)
                 return out
             if not (self.prior.loc.requires_grad or self.prior.scale_tril.requires_grad):
-                lp = _NormalLogProbFn.apply(z, iso[0], iso[1])
+                lp = _NormalLogProbFn.apply(z, iso[0], iso[1], status)
                 return lp if logdet is None else (lp + logdet if sign >= 0 else lp - logdet)
         lp = self.prior.log_prob(z)
         if logdet is None:
@@ -121,8 +142,9 @@ class NormalizingFlowModel(nn.Module):
 
     # ------------------------------------------------------------------ chain
     def _status(self, device):
+        """One status word per spline-layer slot, plus one for the prior (last)."""
         n = sum(f._n_status for f in self.flows if isinstance(f, _HipFlow))
-        return torch.zeros(max(n, 1), dtype=torch.int32, device=device), n
+        return torch.zeros(n + 1, dtype=torch.int32, device=device), n
 
     def _chain(self, x, inverse, deferred=None):
         """Run the layer chain.  With ``deferred`` (a list) the status check is
@@ -162,9 +184,14 @@ class NormalizingFlowModel(nn.Module):
                     logdet = logdet + ld if grad else logdet.add_(ld)
         if deferred is not None:
             deferred.append((status, n_st))
-        elif n_st and config.STRICT_CHECKS:
-            raise_on_status(status, n_st)
+        elif n_st:
+            check_status(status, n_st)
         return x, logdet
+
+    @staticmethod
+    def _prior_word(deferred):
+        status, n_st = deferred[-1]
+        return status[n_st:n_st + 1]
 
     # ------------------------------------------------------- chained launches
     def _groups(self, flows, device, grad):
@@ -229,8 +256,7 @@ class NormalizingFlowModel(nn.Module):
         K_.fused_nsf_chain(x, wp, cm, len(run), n_lo, n_up, hidden, None, logdet=None,
                            logdet_mode=K_.MODE_NONE, K=K, tail_bound=B, inverse=False, status=status,
                            log_prob=out, prior_scale=iso[0], prior_hld=iso[1])
-        if config.STRICT_CHECKS:
-            raise_on_status(status, len(run))
+        check_status(status, len(run), prior=self.prior)
         return out
 
     def _lp_plan(self, x):
@@ -238,18 +264,25 @@ class NormalizingFlowModel(nn.Module):
         None; cached on the parameters' storage and versions so a log_prob loop
         pays one key check per call instead of re-deriving the plan."""
         iso = self._prior_consts()
-        key = (str(x.device), iso, tuple((p.data_ptr(), p._version) for p in self.parameters()))
+        # the structure the plan depends on besides the parameters: the layer
+        # objects (a parameter-free layer appended changes the run), each spline
+        # layer's tail bound, bin count and mask object (part of the chain shape
+        # and maps), and the prior's dimension (checked again outside the cache)
+        struct = tuple((id(f), getattr(f, "B", None), getattr(f, "K", None), id(getattr(f, "mask", None)))
+                       for f in self.flows)
+        key = (str(x.device), iso, struct, tuple((p.data_ptr(), p._version) for p in self.parameters()))
         if self._lp_plan_cache is not None and self._lp_plan_cache[0] == key:
-            return self._lp_plan_cache[1]
-        plan = None
-        groups = self._groups(self.flows, x.device, False)
-        if iso is not None and len(groups) == 1 and isinstance(groups[0], tuple):
-            run, shape = groups[0]
-            D = shape[0] + shape[1]
-            if self.prior.loc.shape[0] == D:
-                wp, cm = self._chain_args(run, D, False, x)
+            plan = self._lp_plan_cache[1]
+        else:
+            plan = None
+            groups = self._groups(self.flows, x.device, False)
+            if iso is not None and len(groups) == 1 and isinstance(groups[0], tuple):
+                run, shape = groups[0]
+                wp, cm = self._chain_args(run, shape[0] + shape[1], False, x)
                 plan = (run, shape, iso, wp, cm)
-        self._lp_plan_cache = (key, plan)
+            self._lp_plan_cache = (key, plan)
+        if plan is not None and self.prior.loc.shape[0] != plan[1][0] + plan[1][1]:
+            return None  # the prior's dimension does not match: the generic path raises like torch
         return plan
 
     def _run_chain(self, run, shape, x, inverse, logdet, status):
@@ -266,18 +299,19 @@ class NormalizingFlowModel(nn.Module):
                            logdet_mode=K_.MODE_ACC, K=K, tail_bound=B, inverse=inverse, status=status)
         return z
 
-    @staticmethod
-    def _check(deferred):
+    def _check(self, deferred, prior=False):
+        """The deferred status check of a chain (+ its prior word when
+        ``prior``: the NaN-z ValueError of the prior's argument validation)."""
         for status, n_st in deferred:
-            if n_st and config.STRICT_CHECKS:
-                raise_on_status(status, n_st)
+            if n_st or prior:
+                check_status(status, n_st, prior=self.prior if prior else None)
 
     # ------------------------------------------------------------------ API
     def forward(self, x):
         d = []
         z, log_det = self._chain(x, False, d)
-        lp = self._prior_log_prob(z)
-        self._check(d)
+        lp = self._prior_log_prob(z, status=self._prior_word(d))
+        self._check(d, prior=True)
         return z, lp, log_det
 
     def inverse(self, z):
@@ -290,8 +324,8 @@ class NormalizingFlowModel(nn.Module):
         z = self.prior.sample((n_samples,))
         d = []
         x, log_det = self._chain(z, True, d)
-        log_px = self._prior_log_prob(z, logdet=log_det, sign=-1)
-        self._check(d)
+        log_px = self._prior_log_prob(z, logdet=log_det, sign=-1, status=self._prior_word(d))
+        self._check(d, prior=True)
         return x.data, log_px.data, z.data
 
     @torch.no_grad()
@@ -301,8 +335,8 @@ class NormalizingFlowModel(nn.Module):
             return out.data
         d = []
         z, log_det = self._chain(x, False, d)
-        out = self._prior_log_prob(z, logdet=log_det, sign=1)
-        self._check(d)
+        out = self._prior_log_prob(z, logdet=log_det, sign=1, status=self._prior_word(d))
+        self._check(d, prior=True)
         return out.data
 
     def log_prob(self, x):

@@ -233,12 +233,33 @@ def onebyone(layer, x, p, inverse):
     return x @ P @ L @ US, ld
 
 
+def nsf_ar_flows1(layer, x, p, inverse):
+    """nf/flows_1.py's NSF_AR (flows_1.py:395-465): net i reads the first i
+    coordinates of the INPUT in both directions (a zero column for i = 0),
+    through cos/sin(pi v / B) when periodic."""
+    dim, K, B = layer.dim, layer.K, layer.B
+    cols, ld = [], torch.zeros(x.shape[0], dtype=x.dtype, device=x.device)
+    for i in range(dim):
+        src = torch.zeros(x.shape[0], 1, dtype=x.dtype, device=x.device) if i == 0 else x[:, :i]
+        if layer.periodic:
+            src = torch.cat([torch.cos(math.pi * src / B), torch.sin(math.pi * src / B)], dim=-1)
+        W, H, D = _nsf_params(conditioner(layer, p, "layers.%d" % i, src), K, B)
+        zi, l = unconstrained_rq_spline(x[:, i], W, H, D, inverse, float(B))
+        cols.append(zi)
+        ld = ld + l
+    return torch.stack(cols, dim=1), ld
+
+
 _BY_CLASS = {"NSF_CL": nsf_cl, "RealNVP": realnvp, "NSF_AR": nsf_ar, "Planar": planar,
              "Radial": radial, "MAF": maf, "ActNorm": actnorm, "OneByOneConv": onebyone}
 
 
 def layer_forward(layer, x, p, inverse):
-    """Dispatch on the layer class (normalizingflow_amd.flows, or a subclass)."""
+    """Dispatch on the layer class (normalizingflow_amd.flows, or a subclass);
+    a class naming its restatement in ``_torch_math`` (flows_1.NSF_AR) wins."""
+    own = getattr(type(layer), "_torch_math", None)
+    if own is not None:
+        return globals()[own](layer, x, p, inverse)
     for cls in type(layer).__mro__:
         fn = _BY_CLASS.get(cls.__name__)
         if fn is not None:

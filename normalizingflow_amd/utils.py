@@ -12,7 +12,7 @@ import torch
 
 from . import config
 from . import kernels as K_
-from .flows import raise_on_status
+from .flows import check_status
 
 __all__ = ["DEFAULT_MIN_BIN_WIDTH", "DEFAULT_MIN_BIN_HEIGHT", "DEFAULT_MIN_DERIVATIVE",
            "searchsorted", "unconstrained_RQS", "RQS"]
@@ -61,8 +61,7 @@ def _spline(inputs, w, h, d, inverse, left, right, bottom, top, tails, mode, mbw
     K_.rqs_coupling(x, params, col, col, out, lad_out=lad, K=K, left=left, right=right,
                     bottom=bottom, top=top, tails=tails, min_bin_width=mbw, min_bin_height=mbh,
                     min_derivative=mbd, param_mode=mode, inverse=inverse, status=st)
-    if config.STRICT_CHECKS:
-        raise_on_status(st)
+    check_status(st)
     return out.reshape(inputs.shape), lad.reshape(inputs.shape)
 
 

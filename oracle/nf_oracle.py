@@ -246,6 +246,31 @@ def nsf_ar(x, sd, prefix, dim, K, B, inverse=False, strict=True):
     return out, logdet
 
 
+def nsf_ar_flows1(x, sd, prefix, dim, K, B, periodic=True, inverse=False, strict=True):
+    """nf/flows_1.py's NSF_AR (its last definition, flows_1.py:395-465): dim
+    conditioner nets and no init_param.  Net i reads the INPUT's first i
+    coordinates in both directions (x in forward, z in inverse,
+    flows_1.py:428-433, 450-455), a zero column for i = 0; periodic=True maps
+    them through cos/sin(pi*v/B) first (width 2i, or 2 for i = 0)."""
+    n = x.shape[0]
+    out = torch.zeros_like(x)
+    logdet = torch.zeros(n, dtype=x.dtype)
+    pi = torch.tensor(np.pi)
+    for i in range(dim):
+        src = torch.zeros(n, 1, dtype=x.dtype) if i == 0 else x[:, :i]
+        if periodic:
+            src = torch.cat((torch.cos(pi * src / B), torch.sin(pi * src / B)), axis=-1)
+        raw = fcnn(src, sd, prefix + "layers.%d." % i)
+        uw, uh, ud = torch.split(raw, K, dim=1)
+        uw = 2 * B * torch.softmax(uw, dim=1)
+        uh = 2 * B * torch.softmax(uh, dim=1)
+        ud = F.softplus(ud)
+        out[:, i], lad = unconstrained_rq_spline(x[:, i], uw, uh, ud, inverse=inverse,
+                                                 tail_bound=B, strict=strict)
+        logdet += lad
+    return out, logdet
+
+
 _PLANAR_DERIV = {
     # flows_1.py:12-18 (note the reference's -0.01 for leaky_relu's negative side)
     "tanh": lambda v: 1 - torch.pow(torch.tanh(v), 2),
@@ -344,6 +369,9 @@ def apply_layer(spec, x, sd, inverse=False, strict=True):
         return realnvp(x, sd, p, spec["dim"], inverse=inverse)
     if t == "NSF_AR":
         return nsf_ar(x, sd, p, spec["dim"], spec["K"], spec["B"], inverse=inverse, strict=strict)
+    if t == "NSF_AR_flows1":
+        return nsf_ar_flows1(x, sd, p, spec["dim"], spec["K"], spec["B"],
+                             periodic=spec.get("periodic", True), inverse=inverse, strict=strict)
     if t == "Planar":
         if inverse:
             raise NotImplementedError("Planar flow has no algebraic inverse.")

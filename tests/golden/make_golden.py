@@ -87,7 +87,7 @@ def case_rqs(name, n, K, scale, tail, seed):
 
 
 # ---------------------------------------------------------------- layers
-def case_layer(name, ctor, kwargs, x, inverse=True, f64=True, init=None, seed=1234):
+def case_layer(name, ctor, kwargs, x, inverse=True, f64=True, init=None, seed=1234, type_name=None):
     torch.manual_seed(seed)
     layer = ctor(**kwargs)
     if init is not None:
@@ -105,7 +105,7 @@ def case_layer(name, ctor, kwargs, x, inverse=True, f64=True, init=None, seed=12
             l64 = _f64(layer)
             z64, ld64 = l64.forward(x.double())
             arrays.update(z_f64=z64, ld_f64=ld64)
-    meta = dict(kind="layer", type=ctor.__name__, kwargs={k: v for k, v in kwargs.items()
+    meta = dict(kind="layer", type=type_name or ctor.__name__, kwargs={k: v for k, v in kwargs.items()
                                                          if k not in ("nonlinearity",)},
                 seed=seed)
     if "nonlinearity" in kwargs:
@@ -211,6 +211,137 @@ def extra_cases():
         (rflows.RealNVP, dict(dim=8, hidden_dim=16))], dim=8, var=1.0, n=128, init=init_glow)
 
 
+# ------------------------------------------------- negative discriminant (utils.py:121)
+def _knot_stack(u, K, tb):
+    """The cumulative knots RQS builds from unnormalised logits u (utils.py:73-91
+    op for op: softmax, floor, padded cumsum, affine map, pinned ends), used
+    only to place inputs a few ulps below a bin's top knot."""
+    w = torch.softmax(u, dim=-1)
+    w = 1e-3 + (1 - 1e-3 * K) * w
+    c = F.pad(torch.cumsum(w, dim=-1), pad=(1, 0), mode="constant", value=0.0)
+    c = 2 * tb * c - tb
+    c[..., 0] = -tb
+    c[..., -1] = tb
+    return c
+
+
+def _below(v, j):
+    """v stepped down by j[i] ulps (fp32), elementwise."""
+    out = v.clone()
+    for i in range(v.shape[0]):
+        for _ in range(int(j[i])):
+            out[i] = torch.nextafter(out[i], torch.tensor(-1e30))
+    return out
+
+
+def _asserts(fn):
+    try:
+        fn()
+    except AssertionError:
+        return True
+    return False
+
+
+def negdisc_cases():
+    """Inputs for which the reference's inverse hits `assert (discriminant >=
+    0).all()` (utils.py:121): fp32 cancellation in b^2 - 4ac when the input
+    sits a few ulps below the top knot of a bin whose slope delta = h/w is
+    huge.  Three fixtures: raw unconstrained_RQS (min derivative 1e-3, random
+    extreme logits), one NSF_CL layer and a 2-layer NSF_CL model (B=6, so the
+    double softmax of NSF_CL still reaches delta ~ e^12; the last FCNN layer
+    has zero weights and a crafted bias, so every row has the same knots)."""
+    K, tb, n = 8, 3.0, 4096
+    g = torch.Generator().manual_seed(77)
+    uw = torch.randn(n, K, generator=g) * 6
+    uh = torch.randn(n, K, generator=g) * 6
+    ud = torch.full((n, K - 1), -30.0) + torch.randn(n, K - 1, generator=g)
+    cw, ch = _knot_stack(uw, K, tb), _knot_stack(uh, K, tb)
+    kb = ((ch[:, 1:] - ch[:, :-1]) / (cw[:, 1:] - cw[:, :-1])).argmax(1)
+    top = ch.gather(1, (kb + 1)[:, None])[:, 0]
+    x = _below(top, torch.randint(1, 6, (n,), generator=g))
+    ok = _asserts(lambda: rutils.unconstrained_RQS(x.clone(), uw.clone(), uh.clone(), ud.clone(),
+                                                   inverse=True, tail_bound=tb))
+    row_neg = [i for i in range(n) if _asserts(lambda: rutils.unconstrained_RQS(
+        x[i:i + 1].clone(), uw[i:i + 1].clone(), uh[i:i + 1].clone(), ud[i:i + 1].clone(),
+        inverse=True, tail_bound=tb))]
+    assert ok and row_neg, "reference did not assert"
+    _save("err_rqs_negdisc", dict(kind="negdisc_rqs", K=K, tail_bound=tb, seed=77),
+          dict(x=x, uw=uw, uh=uh, ud=ud, ref_asserts=np.array(ok),
+               row_neg=np.array(row_neg, dtype=np.int64)))
+
+    # NSF_CL layer and model: a diverged conditioner (one NaN weight in the
+    # output layer of psi).  The reference's forward then yields NaN for the
+    # coordinate whose logit is NaN (and its row's log|det|), and its inverse
+    # fails the same assert (NaN >= 0 is false).  A genuinely negative fp32
+    # discriminant is ~5e-4 rare under NSF_CL's double softmax (slopes capped
+    # near 1/min_bin_width, interior derivatives >= 0.69), so it cannot be
+    # pinned robustly there; the raw case above pins it.
+    size = 32
+    gz = torch.Generator().manual_seed(78)
+    x = torch.randn(512, 2 * size, generator=gz) * 1.2
+
+    def poison(layer, row):
+        with torch.no_grad():
+            layer.psi.network[4].weight[row, 3] = float("nan")
+
+    torch.manual_seed(1234)
+    layer = rflows.NSF_CL(size=size, dim=2, K=8, B=3, hidden_dim=100, mask=[1])
+    poison(layer, 5 * 23 + 2)      # W logit 2 of upper coordinate 5
+    with torch.no_grad():
+        z, ld = layer.forward(x.clone())
+        ok = _asserts(lambda: layer.inverse(x.clone()))
+    assert ok, "reference NSF_CL.inverse did not assert"
+    _save("err_nsfcl_nan", dict(kind="nan_layer", type="NSF_CL",
+                            kwargs=dict(size=size, dim=2, K=8, B=3, hidden_dim=100, mask=[1]),
+                            seed=1234, nan_weight=[5 * 23 + 2, 3]),
+          dict(x=x, z=z, ld=ld, inv_asserts=np.array(ok)), layer)
+
+    torch.manual_seed(1234)
+    flows = [rflows.NSF_CL(size=size, dim=2, K=8, B=3, hidden_dim=100, mask=[i % 2])
+             for i in range(2)]
+    poison(flows[1], 17 * 23 + 9)  # H logit 1 of upper coordinate 17 of the last layer
+    prior = torch.distributions.MultivariateNormal(torch.zeros(2 * size), torch.eye(2 * size))
+    model = rmodels.NormalizingFlowModel(prior, flows)
+    def raised(fn):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 -- record which error the reference raises
+            return type(e).__name__
+        return ""
+
+    with torch.no_grad():
+        # layer by layer (the model's own forward stops at the prior's
+        # argument validation: ValueError on a NaN z, torch MultivariateNormal)
+        zl, ld0 = flows[0].forward(x.clone())
+        zm, ld1 = flows[1].forward(zl.clone())
+        fwd_err = raised(lambda: model(x.clone()))
+        eval_err = raised(lambda: model.evaluate(x.clone()))
+        inv_err = raised(lambda: model.inverse(x.clone()))
+    assert fwd_err == "ValueError" and eval_err == "ValueError" and inv_err == "AssertionError", \
+        (fwd_err, eval_err, inv_err)
+    _save("err_model_nan", dict(kind="nan_model", dim=2 * size, var=1.0, seed=1234,
+                            layers=[dict(type="NSF_CL", kwargs=dict(size=size, dim=2, K=8, B=3,
+                                                                    hidden_dim=100, mask=[i % 2]))
+                                    for i in range(2)],
+                            forward_raises=fwd_err, evaluate_raises=eval_err,
+                            inverse_raises=inv_err),
+          dict(x=x, z=zm, ld=ld0 + ld1), model)
+
+
+def flows1_cases():
+    """nf/flows_1.py's own NSF_AR (its last definition, flows_1.py:395-465),
+    which `from nf.flows_1 import NSF_AR` binds: periodic and plain inputs (no fp64
+    companion: its i = 0 input is an fp32 zeros column, flows_1.py:430)."""
+    g = torch.Generator().manual_seed(4343)
+    x4 = torch.randn(128, 4, generator=g) * 1.3
+    case_layer("nsfar1_d4_k4_periodic", rflows1.NSF_AR, dict(dim=4, K=4, B=3, hidden_dim=16), x4, f64=False,
+               type_name="NSF_AR_flows1")
+    x3 = torch.randn(128, 3, generator=g) * 1.3
+    case_layer("nsfar1_d3_k5_plain", rflows1.NSF_AR,
+               dict(dim=3, K=5, B=2.5, hidden_dim=12, periodic=False), x3, f64=False,
+               type_name="NSF_AR_flows1")
+
+
 def main():
     g = torch.Generator().manual_seed(42)
     case_rqs("rqs_k4", 512, 4, 1.0, 3.0, 11)
@@ -260,6 +391,12 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["extra"]:
         extra_cases()
+    elif sys.argv[1:] == ["negdisc"]:
+        negdisc_cases()
+    elif sys.argv[1:] == ["flows1"]:
+        flows1_cases()
     else:
         main()
         extra_cases()
+        negdisc_cases()
+        flows1_cases()

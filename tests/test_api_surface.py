@@ -9,6 +9,7 @@ import torch.nn.functional as F
 
 import golden_io as gio
 import nf.flows as nff
+import nf.flows_1 as nff1
 import nf.models as nfm
 import nf.utils as nfu
 
@@ -17,14 +18,15 @@ NL = {"tanh": torch.tanh, "leaky_relu": F.leaky_relu, "elu": F.elu}
 
 def build_layer(meta):
     kw = dict(meta["kwargs"])
-    cls = getattr(nff, meta["type"])
+    # nf/flows_1.py's own NSF_AR (flows_1.py:395-465) is a different layer
+    cls = nff1.NSF_AR if meta["type"] == "NSF_AR_flows1" else getattr(nff, meta["type"])
     if meta["type"] == "Planar":
         kw["nonlinearity"] = NL[meta.get("nonlinearity", "tanh")]
     return cls(**kw)
 
 
 LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar",
-                                                       "maf", "actnorm", "onebyone")]
+                                                       "nsfar1", "maf", "actnorm", "onebyone")]
 # fixtures whose values were set after construction (ActNorm starts at zero, flows_1.py:204-205)
 _REINIT = ("mu", "log_sigma")
 
@@ -89,6 +91,23 @@ def test_exports():
     exec("from nf.flows import *", ns)
     for n in ("RealNVP", "NSF_AR", "NSF_CL"):
         assert n in ns
+
+
+def test_flows_1_nsf_ar_is_its_own_layer():
+    """`from nf.flows_1 import NSF_AR` binds flows_1.py:395-465: periodic
+    keyword, dim nets and no init_param (nf.flows.NSF_AR has init_param and
+    dim - 1 nets); its reset_parameters fails like the reference's."""
+    a = nff1.NSF_AR(dim=3, K=4, B=3, hidden_dim=8)
+    b = nff1.NSF_AR(dim=3, K=4, B=3, hidden_dim=8, periodic=False)
+    c = nff.NSF_AR(dim=3, K=4, B=3, hidden_dim=8)
+    assert len(a.layers) == 3 and not hasattr(a, "init_param")
+    assert [l.network[0].in_features for l in a.layers] == [2, 2, 4]
+    assert [l.network[0].in_features for l in b.layers] == [1, 1, 2]
+    assert len(c.layers) == 2 and "init_param" in c.state_dict()
+    with pytest.raises(AttributeError):
+        a.reset_parameters()
+    with pytest.raises(TypeError):
+        nff.NSF_AR(dim=3, periodic=True)
 
 
 def test_no_cpu_fallback():

@@ -1,0 +1,63 @@
+"""GPU: bench.py's own N = 2 data path, end to end (BASELINE c4 / the north
+star's strong scaling).  torchrun starts two ranks of
+bench.py on the box's one device over gloo (the driver's 8-GPU run uses the
+same code over RCCL).  Each rank runs the full 8-layer c3 model on its shard
+and the step ends in the NLL all-reduce (applications/src/train.py:23-25);
+the reported NLL must equal the CPU oracle's -mean(log_prob) over the same
+rows (nf/models.py:37-40) within the north star's 1e-5 relative."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("scaling,rows", [("strong", 32768), ("weak", 12288)])
+def test_bench_world2_nll_vs_oracle(hip_device, scaling, rows):
+    sys.path.insert(0, REPO)
+    import bench
+    from normalizingflow_amd.dist import shard_range
+    from oracle import nf_oracle as orc
+
+    size_arg = ["--global-batch", str(rows)] if scaling == "strong" else ["--batch", str(rows)]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--scaling", scaling,
+           *size_arg, "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--parity-rows", "1024"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    total = rows if scaling == "strong" else 2 * rows
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["config"]["global_batch"] == total and line["config"]["backend"] == "gloo"
+    assert line["value"] > 0 and line["parity"]["pass"]
+
+    # the same rows: each rank draws its shard from a device generator seeded by its rank
+    xs = []
+    for rank in range(2):
+        n = (lambda lo_hi: lo_hi[1] - lo_hi[0])(shard_range(rows, rank, 2)) if scaling == "strong" else rows
+        g = torch.Generator(device=hip_device).manual_seed(rank)
+        xs.append(torch.randn(n, 64, generator=g, device=hip_device).cpu())
+    x = torch.cat(xs)
+    assert x.shape[0] == total
+    _, sd, _ = bench.build_model("c3", hip_device)
+    ref = orc.model_log_prob(bench.specs_for("c3"), {k: v.cpu() for k, v in sd.items()}, x)
+    nll_ref = float(-ref.double().mean())
+    assert abs(line["nll"] - nll_ref) <= 1e-5 * abs(nll_ref), (line["nll"], nll_ref)

@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 import golden_io as gio
 import nf.flows as nff
+import nf.flows_1 as nff1
 import nf.models as nfm
 import nf.utils as nfu
 from normalizingflow_amd import config
@@ -58,6 +59,8 @@ def build_layer(meta):
     kw = dict(meta["kwargs"])
     if meta["type"] == "Planar":
         kw["nonlinearity"] = NL[meta.get("nonlinearity", "tanh")]
+    if meta["type"] == "NSF_AR_flows1":  # nf/flows_1.py:395-465
+        return nff1.NSF_AR(**kw)
     return getattr(nff, meta["type"])(**kw)
 
 
@@ -88,7 +91,7 @@ def cpu_sd(module):
 
 # --------------------------------------------------------------------------- golden
 LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar",
-                                                               "maf", "actnorm", "onebyone")]
+                                                               "nsfar1", "maf", "actnorm", "onebyone")]
 
 
 @pytest.mark.parametrize("name", LAYERS)

@@ -31,7 +31,7 @@ def test_rqs_fixture(name):
     _close(y64, d["y_f64"], rtol=1e-12, atol=1e-12); _close(lad64, d["lad_f64"], rtol=1e-12, atol=1e-12)
 
 
-LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar",
+LAYERS = [n for n in gio.names() if n.split("_")[0] in ("nsfcl", "realnvp", "planar", "radial", "nsfar", "nsfar1",
                                                                "maf", "actnorm", "onebyone")]
 
 
@@ -85,3 +85,49 @@ def test_bin_width_check():
     w = torch.zeros(4, 2000)
     with pytest.raises(ValueError):
         orc.unconstrained_rq_spline(x, w, w, torch.zeros(4, 1999), tail_bound=3.0)
+
+
+# ---- the reference's data-dependent errors (tests/golden/make_golden.py negdisc_cases)
+def test_negative_discriminant_fixture():
+    """utils.py:121: the reference asserts on this batch; the oracle must too,
+    and on exactly the rows that assert one at a time."""
+    meta, d, _ = gio.load("err_rqs_negdisc")
+    tb = meta["tail_bound"]
+    args = (d["x"], d["uw"], d["uh"], d["ud"])
+    with pytest.raises(AssertionError):
+        orc.unconstrained_rq_spline(*args, inverse=True, tail_bound=tb)
+    bad = []
+    for i in range(d["x"].shape[0]):
+        try:
+            orc.unconstrained_rq_spline(*(a[i:i + 1] for a in args), inverse=True, tail_bound=tb)
+        except AssertionError:
+            bad.append(i)
+    assert bad == d["row_neg"].tolist()
+
+
+def test_nan_conditioner_layer_fixture():
+    """A NaN weight in psi's output layer: NaN at that coordinate in the
+    forward (flows.py:227-239) and AssertionError in the inverse."""
+    meta, d, sd = gio.load("err_nsfcl_nan")
+    spec = gio.layer_spec(meta)
+    z, ld = orc.apply_layer(spec, d["x"], sd)
+    _close(z, d["z"]); _close(ld, d["ld"])
+    with pytest.raises(AssertionError):
+        orc.apply_layer(spec, d["x"], sd, inverse=True)
+
+
+def test_nan_conditioner_model_fixture():
+    """Model level: forward / evaluate raise ValueError (the prior's argument
+    validation on a NaN z), inverse raises AssertionError."""
+    meta, d, sd = gio.load("err_model_nan")
+    specs = _model_specs(meta)
+    assert (meta["forward_raises"], meta["inverse_raises"]) == ("ValueError", "AssertionError")
+    with pytest.raises(ValueError):
+        orc.model_forward(specs, sd, d["x"], meta["var"])
+    with pytest.raises(AssertionError):
+        orc.model_inverse(specs, sd, d["x"])
+    z, ld = d["x"], torch.zeros(d["x"].shape[0])
+    for s in specs:
+        z, l = orc.apply_layer(s, z, sd)
+        ld = ld + l
+    _close(z, d["z"]); _close(ld, d["ld"], atol=1e-5)
