@@ -82,9 +82,11 @@ PARITY_ATOL = 1e-5   # ... with this absolute floor for values near 0 (tests/tes
 CLOCK_GHZ = 2.4      # MI355X_MICROARCH.md: max engine clock
 N_SIMD = 1024        # 256 CUs x 4 SIMDs
 # VALU issue cost per wave64 instruction on one SIMD-32 with several waves
-# resident (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
-# cycles; transcendentals at twice the issue cost of v_fma_f32; an MFMA holds
-# the SIMD's vector issue for 8 cycles)
+# resident: measured by tools/ubench_valu.hip (profiles/r2_ubench_valu.txt:
+# each added co-resident wave adds 2 cycles per v_fma_f32 / v_add_f32 and 4
+# per v_exp_f32 to every wave's per-instruction time, i.e. the SIMD retires
+# one VALU per 2 cycles and one transcendental per 4), and
+# MI355X_MICROARCH.md: an MFMA holds the SIMD's vector issue for 8 cycles
 VALU_CYC, TRANS_CYC, MFMA_HOLD_CYC = 2.0, 4.0, 8.0
 
 

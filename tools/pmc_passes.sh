@@ -20,7 +20,7 @@ i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $p --kernel-include-regex "$REGEX" --output-format csv \
-      -d "$OUT/pmc$i" -o pmc -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-timer "$@" \
+      -d "$OUT/pmc$i" -o pmc -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-timer --parity-rows 0 "$@" \
       > "$OUT/pmc$i.log" 2>&1; rc=$?
   echo "pass $i rc=$rc ($p)"
   case $rc in 0) ;; *) tail -5 "$OUT/pmc$i.log"; exit $rc;; esac
