@@ -109,12 +109,12 @@ __device__ uint32_t f16_part_pair(float v0, float v1, int part) {
     return (uint32_t)__builtin_bit_cast(uint16_t, r0) | ((uint32_t)__builtin_bit_cast(uint16_t, r1) << 16);
 }
 
-// word of an f16-split record (f16 blocks, f32 tail groups, bias block) with
+// word of an f16-split record (f16 blocks, tail blocks, bias block) with
 // nt tiles; row(t, i) and the weight row pointer come from the caller's lambda
 template <class RowF, class BiasF>
 __device__ uint32_t pack_record_word(int blk, int wl, const Layout& L, int nt, float sc, float bsc,
                                      RowF row_of, BiasF bias_of) {
-    const int nf = L.KBH * nt * 2, ntg = L.T1 ? (nt + 3) / 4 : 0;
+    const int nf = L.KBH * nt * 2, ntg = L.T1 ? (nt + 1) / 2 : 0;
     if (blk < nf) {
         const int part = blk & 1, idx = blk >> 1, kb = idx / nt, t = idx - kb * nt;
         const int lane = wl >> 2, j = 2 * (wl & 3);
@@ -128,16 +128,7 @@ __device__ uint32_t pack_record_word(int blk, int wl, const Layout& L, int nt, f
         }
         return f16_part_pair(v0, v1, part);
     }
-    if (blk < nf + ntg) {  // f32 tail: lane l, component e of group g
-        const int g = blk - nf, lane = wl >> 2, e = wl & 3, t = 4 * g + e;
-        const int k = 32 * L.KBH + (lane >> 4);
-        float v = 0.0f;
-        if (t < nt && k < L.H) {
-            const float* w = row_of(t, lane & 15);
-            if (w != nullptr) v = w[k] * sc;
-        }
-        return __float_as_uint(v);
-    }
+    if (blk < nf + ntg) return tail_word(blk - nf, wl, nt, 32 * L.KBH, L.H, sc, row_of);
     const int t = wl >> 4, i = wl & 15;  // bias block [tile][row]
     return __float_as_uint(t < nt ? bias_of(t, i) * bsc : 0.0f);
 }
@@ -292,7 +283,7 @@ bool shape_ok(int n_lo, int n_up, int H, int K) {
 }
 
 // Shapes of the wide kernel (nfk_fused_wide.h): H = 32 KBH for an instantiated
-// KBH, no f32 tail; layer-1 inputs within the KBH k-blocks; every lower
+// KBH, no tail step; layer-1 inputs within the KBH k-blocks; every lower
 // coordinate inside the x tiles (16 lower + 16 upper coordinates per chunk
 // pair); even K; LDS within the CU.
 bool wide_ok(int n_lo, int n_up, int H, int K) {

@@ -12,6 +12,7 @@ int nfk_set_error(const char* msg);  // nfk_kernels.hip
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 
 #ifndef NFK_WAVES
 #define NFK_WAVES 8
@@ -54,11 +55,14 @@ constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 
 //            x {hi, lo}: lane l of block (kb, t, p) holds part p of
 //            2^s W[row(t, l&15)][32kb + 8(l>>4) + j], j = 0..7, where hi = f16(v),
 //            lo = f16(v - hi) and 2^s puts max|W| in [2^14, 2^15)
-//   f32 tail (T1 only: H = 32 KBH + R, 0 < R <= 4, v_mfma_f32_16x16x4_f32):
-//            one block per 4 tiles: lane l, component e holds
-//            2^s W[row(4g+e, l&15)][32 KBH + (l>>4)]
+//   tail (T1 only: H = 32 KBH + R, 0 < R <= 4, one v_mfma_f32_16x16x16_f16
+//            per tile): one block per 2 tiles; lane l's 16 B hold tile 2g's
+//            then tile 2g + 1's fragment, 4 halves over the tail features
+//            32 KBH + 0..3 of row(t, l&15): k-group l>>4 = {hi, hi, lo, 0} of 2^s W, against
+//            the B groups {a_hi, a_lo, a_hi, -} (tail_word, act_operands): the
+//            same three split products as the k-blocks, in one f16 MFMA
 //   layer 1: KB1 = ceil(n_lo/32) f16 k-blocks (x is scaled per wave), bias unscaled
-//   layer 2: KBH f16 k-blocks (+ f32 tail), bias pre-scaled by 2^(s2+14)
+//   layer 2: KBH f16 k-blocks (+ tail blocks), bias pre-scaled by 2^(s2+14)
 //   per 16-coordinate chunk: W logits (K tiles), H logits (K tiles), D logits
 //            (K-1 tiles), same form; row i of tile t = parameter t of coordinate 16c+i
 // Hidden feature permutation: row i of hidden tile t < 2 KBH computes feature
@@ -66,8 +70,9 @@ constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 
 // so accumulator register r of tiles 2kb, 2kb+1 of lane l are exactly
 // elements j = r, 4 + r of the next product's B fragment for k-block kb
 // (k = 32kb + 8(l>>4) + j) -- activations never leave registers.  With a
-// tail, tile 2 KBH holds feature 32 KBH + q in register 0 of lane group q:
-// exactly the B operand (k = l>>4) of the f32 tail step.
+// tail, tile 2 KBH holds features 32 KBH + r in register r of every lane
+// group (rows duplicated): the B operand of the tail step needs all R in
+// each lane.
 // wide = 1 (nfk_fused_wide.h): the output layer in 8-coordinate chunks whose
 //   W/H/D records have ceil(K/2) tiles; row i of tile t = parameter
 //   2t + (i&1) of coordinate 8c + 2(i>>2) + ((i>>1)&1), so lane group q holds
@@ -116,8 +121,8 @@ struct Layout {
     int64_t o_h1, o_h2, o_w3, total;  // offsets / size in floats
 };
 
-// blocks of an f16-split record with nt tiles (+ f32 tail groups, + bias)
-inline int rec_blocks(int kbh, int t1, int nt) { return kbh * nt * 2 + (t1 ? (nt + 3) / 4 : 0) + 1; }
+// blocks of an f16-split record with nt tiles (+ tail blocks, + bias)
+inline int rec_blocks(int kbh, int t1, int nt) { return kbh * nt * 2 + (t1 ? (nt + 1) / 2 : 0) + 1; }
 
 inline Layout make_layout(int n_lo, int n_up, int H, int K, int wide = 0) {
     Layout L;
@@ -176,11 +181,11 @@ inline size_t lds_bytes(const Layout& L) {
            NFK_LDS_PAD;
 }
 
-// Split form (NfkSplit): slot of KBH NS 2 + T1 + 1 blocks (at least the
+// Split form (NfkSplit): slot of KBH NS 2 + T1 NS/2 + 1 blocks (at least the
 // layer-1 record); used when three workgroups then fit a CU.
 inline int split_slot_blocks(const Layout& L) {
     const int ns = L.KBH <= 3 ? NFK_SPLIT_NS : 2;
-    const int sb = L.KBH * ns * 2 + L.T1 + 1;
+    const int sb = L.KBH * ns * 2 + (L.T1 ? (ns + 1) / 2 : 0) + 1;
     return sb > L.blk_h1 ? sb : L.blk_h1;
 }
 // split-form LDS: the slot, four maps + the output->input column map, each
@@ -219,7 +224,33 @@ inline int chain_max_layers(const Layout& L) {
 // hidden feature computed by row i (0..15) of hidden tile t (>= H: padding)
 __host__ __device__ inline int hid_feature(int t, int i, int kbh) {
     if (t < 2 * kbh) return 32 * (t >> 1) + 8 * (i >> 2) + 4 * (t & 1) + (i & 3);
-    return (i & 3) == 0 ? 32 * kbh + (i >> 2) : (1 << 20);
+    return 32 * kbh + (i & 3);  // the tail tile: every lane group holds the tail features
+}
+
+// f16 pair (v0, v1) of split part p (0 = hi, 1 = lo) as one packed word
+__device__ __forceinline__ uint32_t nfk_f16_part_pair(float v0, float v1, int part) {
+    const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+    const _Float16 r0 = part ? (_Float16)(v0 - (float)h0) : h0;
+    const _Float16 r1 = part ? (_Float16)(v1 - (float)h1) : h1;
+    return (uint32_t)__builtin_bit_cast(uint16_t, r0) | ((uint32_t)__builtin_bit_cast(uint16_t, r1) << 16);
+}
+
+// Word wl (0..255) of tail block g of a record with nt tiles (the 16x16x16 f16
+// A fragments of tiles 2g and 2g + 1, interleaved per lane: words 4l, 4l + 1
+// tile 2g, 4l + 2, 4l + 3 tile 2g + 1): lane l of tile t holds halves j = 0..3 =
+// tail features kbase + j of weight row row_of(t, l & 15), as the hi part in
+// k-groups 0 and 1, the lo part in k-group 2, zero in k-group 3.
+template <class RowF>
+__device__ uint32_t tail_word(int g, int wl, int nt, int kbase, int H, float sc, RowF row_of) {
+    const int t = 2 * g + ((wl & 3) >> 1), lane = wl >> 2, j = 2 * (wl & 1), q = lane >> 4;
+    if (t >= nt || q == 3) return 0u;
+    const float* w = row_of(t, lane & 15);
+    float v0 = 0.0f, v1 = 0.0f;
+    if (w != nullptr) {
+        if (kbase + j < H) v0 = w[kbase + j] * sc;
+        if (kbase + j + 1 < H) v1 = w[kbase + j + 1] * sc;
+    }
+    return nfk_f16_part_pair(v0, v1, q == 2 ? 1 : 0);
 }
 
 // Spline constants of NSF_CL (flows.py:236: left = bottom = -B, right = top = B,
@@ -260,16 +291,13 @@ struct FusedArgs {
     float prior_inv_scale, prior_c2pi, prior_hld;
 };
 
-__device__ __forceinline__ f32x4 mfma32(float a, float b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
 __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float pick4(const float4& w, int e) {
-    return e == 0 ? w.x : e == 1 ? w.y : e == 2 ? w.z : w.w;
+// the tail step: K = 16 over the packed (hi, hi, lo, 0) x (a_hi, a_lo, a_hi, -) groups
+__device__ __forceinline__ f32x4 mfma16k16(h4 a, h4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ f32x4 as_f32x4(const float4& v) {
@@ -385,62 +413,72 @@ __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, 
     }
 }
 
-// acc[t] = bias + 2^s W[tile t] . act^T: the f32 tail step, then KBH k-blocks
-// of 32 in the fp16 split, three MFMAs per (tile, k-block), small terms first.
+// acc[t] = bias + 2^s W[tile t] . act^T: KBH k-blocks of 32 in the fp16
+// split, three MFMAs per (tile, k-block), small terms first, then the tail
+// step (T1: one f16 MFMA holding the three split products of the <= 4 tail
+// features, its fragments carried by the same prefetch ring).
 // Tiles go in pairs whose MFMAs alternate accumulators: a dependent MFMA
 // chain blocks the SIMD partner wave's VALU, two interleaved chains let it
 // overlap (tools/ubench_coexec2.hip, modes 5-6).  A fragments of the next
 // pair are read from the LDS slot while the current pair's MFMAs run.
 // Split form (sub-records, k_fused_nsf<..., SPLIT = true>): the slot holds
 // tiles [T0, T0 + NT) of a record, at a tile stride of NS per k-block, then
-// the tail group holding them and the record's whole bias block; acc has NA
+// the tail blocks holding them and the record's whole bias block; acc has NA
 // tiles and this call fills acc[T0 .. T0 + NT).  Whole records: NS = NA = NT.
 template <int KBH, bool T1, int NT, int NS = NT, int T0 = 0, int NA = NT>
-__device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH], float btail,
+__device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH], h4 btail,
                                        const float4* slot, int lane, f32x4 (&acc)[NA]) {
     constexpr int NPR = (NT + 1) / 2;  // tile pairs (the last may be a single tile)
-    constexpr int N = KBH * NPR;
-    constexpr int NTG = T1 ? (NS + 3) / 4 : 0;
+    constexpr int N = KBH * NPR;       // k-block steps; T1: then NPR tail steps
+    constexpr int NI = N + (T1 ? NPR : 0);
+    constexpr int NTG = T1 ? (NS + 1) / 2 : 0;
     const int q = lane >> 4;
     const float4* tail = slot + KBH * NS * 2 * 64;
     const float4* bias = tail + NTG * 64;
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[T0 + t] = as_f32x4(bias[(T0 + t) * 4 + q]);
-    if constexpr (T1) {
+    // fragments of step i into a ring slot: k-block step i = (kb, pr): tile
+    // t0 = 2 pr {hi, lo}, tile t0 + 1 {hi, lo}; tail step N + pr: one 16-B
+    // word per lane holding both tiles' tail fragments (tail block pr)
+    auto fetch = [&](int i, float4 (&r)[4]) {
+        if (i < N) {
+            const int kb = i / NPR, pr = i - kb * NPR;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int g = ((T0 + t) >> 2) - (T0 >> 2), e = (T0 + t) & 3;
-            const float4 w = tail[g * 64 + lane];
-            acc[T0 + t] = mfma32(pick4(w, e), btail, acc[T0 + t]);
+            for (int j = 0; j < 4; ++j)
+                if (2 * pr + (j >> 1) < NT) r[j] = slot[((kb * NS + 2 * pr) * 2 + j) * 64 + lane];
+        } else {
+            r[0] = tail[(i - N) * 64 + lane];
         }
-    }
-    // blocks of pair i = (kb, pr): tile t0 = 2 pr {hi, lo}, tile t0 + 1 {hi, lo}
-    auto blk = [](int i, int j) {  // j = 0..3
-        const int kb = i / NPR, pr = i - kb * NPR;
-        return (kb * NS + 2 * pr) * 2 + j;
     };
     float4 ring[2][4];
-    if constexpr (NFK_GEMM_PF) {
+    if constexpr (NFK_GEMM_PF) fetch(0, ring[0]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (2 * (0 % NPR) + (j >> 1) < NT) ring[0][j] = slot[blk(0, j) * 64 + lane];
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const int kb = i / NPR, pr = i - kb * NPR, t0 = T0 + 2 * pr;
+    for (int i = 0; i < NI; ++i) {
+        const int pr = i < N ? i % NPR : i - N, kb = i < N ? i / NPR : 0, t0 = T0 + 2 * pr;
         const bool two = t0 + 1 < T0 + NT;
-        if constexpr (!NFK_GEMM_PF) {  // no prefetch: the pair's fragments just before its MFMAs
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (2 * pr + (j >> 1) < NT) ring[i & 1][j] = slot[blk(i, j) * 64 + lane];
-        } else if (i + 1 < N) {
-            const int pn = (i + 1) % NPR;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (2 * pn + (j >> 1) < NT) ring[(i + 1) & 1][j] = slot[blk(i + 1, j) * 64 + lane];
-        }
+        if constexpr (!NFK_GEMM_PF)  // no prefetch: the step's fragments just before its MFMAs
+            fetch(i, ring[i & 1]);
+        else if (i + 1 < NI)
+            fetch(i + 1, ring[(i + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         const float4* r = ring[i & 1];
+        if (i >= N) {  // tail step (T1)
+            if (i == N && NT <= 2) {
+                // the tail MFMA (16x16x16) reads as its accumulator what a
+                // 16x16x32 MFMA one or no instruction earlier wrote: across the
+                // two opcodes the result is not forwarded (measured: rows 0, 1
+                // of each lane group stale), so wait it out; with three or more
+                // tiles two other MFMAs separate them
+                __builtin_amdgcn_sched_barrier(0);
+                if (NT == 1) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7");
+                else asm volatile("s_nop 7\n\ts_nop 7");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const float4 w = r[0];
+            acc[t0] = mfma16k16(__builtin_bit_cast(h4, make_float2(w.x, w.y)), btail, acc[t0]);
+            if (two) acc[t0 + 1] = mfma16k16(__builtin_bit_cast(h4, make_float2(w.z, w.w)), btail, acc[t0 + 1]);
+            continue;
+        }
         const h8 ahi0 = __builtin_bit_cast(h8, r[0]), alo0 = __builtin_bit_cast(h8, r[1]);
         if (two) {
             const h8 ahi1 = __builtin_bit_cast(h8, r[2]), alo1 = __builtin_bit_cast(h8, r[3]);
@@ -459,16 +497,29 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
 }
 
 // activations of a hidden layer -> B operands of the next product
+// (T1: the tail B operand, k-groups {a_hi, a_lo, a_hi, a_hi} over the tail
+// features held in registers 0..3 of the tail tile; A's group 3 is zero)
 template <int KBH, bool T1, int HT>
 __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[KBH], h8 (&bl)[KBH],
-                                             float& btail) {
+                                             h4& btail) {
 #pragma unroll
     for (int t = 0; t < 2 * KBH; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) h[t][r] = tanh_scaled(h[t][r], c2);
 #pragma unroll
     for (int kb = 0; kb < KBH; ++kb) split_act<HT>(h, kb, bh[kb], bl[kb]);
-    btail = T1 ? tanh_scaled(h[HT - 1][0], c2) : 0.0f;  // registers 1-3 of the tail tile are padding
+    if constexpr (T1) {
+        h4 hi, lo;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float v = tanh_scaled(h[HT - 1][r], c2);
+            hi[r] = (_Float16)v;
+            lo[r] = (_Float16)(v - (float)hi[r]);
+        }
+        btail = ((threadIdx.x >> 4) & 3) == 1 ? lo : hi;
+    } else {
+        btail = h4{0, 0, 0, 0};
+    }
 }
 
 // Knot phase epilogue: for the 4 coordinates of this lane, turn the K logits
@@ -621,16 +672,16 @@ struct NfkSplit {
     static constexpr int NW = (K + NS - 1) / NS;     // W (or H) logits sub-records
     static constexpr int ND = (K - 1 + NS - 1) / NS; // derivative logits sub-records
     static constexpr int SPC = 2 * NW + ND;          // sub-records per chunk
-    static constexpr int slot_blocks = KBH * NS * 2 + (T1 ? 1 : 0) + 1;
+    static constexpr int slot_blocks = KBH * NS * 2 + (T1 ? (NS + 1) / 2 : 0) + 1;
 };
 
 // Copy tiles [t0, t0 + NS) (fewer at the record's end) of the record at rec
 // (nt tiles) into the slot at tile stride NS: per k-block NS x {hi, lo}
-// blocks, then the tail group holding them, then the record's bias block.
+// blocks, then the tail blocks holding them, then the record's bias block.
 template <int KBH, bool T1, int NS>
 __device__ __forceinline__ void stage_tiles(const float* __restrict__ rec, int nt, int t0, float4* slot, int wid,
                                             int lane) {
-    constexpr int NF = KBH * NS * 2, NB = NF + (T1 ? 1 : 0) + 1;
+    constexpr int NTB = T1 ? (NS + 1) / 2 : 0, NF = KBH * NS * 2, NB = NF + NTB + 1;
     const int nts = (nt - t0) < NS ? (nt - t0) : NS;
     const uint32_t base = lds_addr(slot);
     for (int i = wid; i < NB; i += kNsfWaves) {
@@ -639,10 +690,10 @@ __device__ __forceinline__ void stage_tiles(const float* __restrict__ rec, int n
             const int kb = i / (2 * NS), r = i - kb * 2 * NS;
             if ((r >> 1) >= nts) continue;
             src = (kb * nt + t0 + (r >> 1)) * 2 + (r & 1);
-        } else if (T1 && i == NF) {
-            src = KBH * nt * 2 + (t0 >> 2);
+        } else if (i < NF + NTB) {
+            src = KBH * nt * 2 + (t0 >> 1) + (i - NF);
         } else {
-            src = KBH * nt * 2 + (T1 ? (nt + 3) / 4 : 0);
+            src = KBH * nt * 2 + (T1 ? (nt + 1) / 2 : 0);
         }
         dma16(rec + (int64_t)src * 256 + lane * 4, base + i * 1024);
     }
@@ -679,7 +730,7 @@ __device__ __forceinline__ void stage_split(const FusedArgs& a, const float* __r
 // GEMM over all parts J, J+1, ... of an NT-tile record: each part is followed
 // by step(last) (barrier, next copy; if not last, wait for it).
 template <int KBH, bool T1, int NT, int NS, int J, class Step>
-__device__ __forceinline__ void gemm_parts(const h8 (&bh)[KBH], const h8 (&bl)[KBH], float btail,
+__device__ __forceinline__ void gemm_parts(const h8 (&bh)[KBH], const h8 (&bl)[KBH], h4 btail,
                                            const float4* slot, int lane, f32x4 (&acc)[NT], Step&& step) {
     constexpr int T0 = J * NS;
     constexpr int N = (NT - T0) < NS ? (NT - T0) : NS;
@@ -761,7 +812,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const bool row_ok = sl < nrows;
     h8 bh[KBH], bl[KBH];  // B operands (activations) of the current product
-    float btail = 0.0f;
+    h4 btail = h4{0, 0, 0, 0};
     NfkTrace tr;
     (void)tr;
     NFK_MARK(tr);  // start
@@ -1270,7 +1321,7 @@ int launch_fused(const FusedArgs& a, size_t lds, bool inv, bool split, bool chai
     extern template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, \
                                                  bool chain, hipStream_t st);
 
-// hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f32 tail step of <= 4
+// hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f16 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132
 #define NFK_FUSED_KB(X) X(1, 0) X(1, 1) X(2, 0) X(2, 1) X(3, 0) X(3, 1) X(4, 0) X(4, 1)
 #define NFK_FUSED_K(X, KBH, T1) X(KBH, T1, 4) X(KBH, T1, 5) X(KBH, T1, 6) X(KBH, T1, 8) X(KBH, T1, 10)

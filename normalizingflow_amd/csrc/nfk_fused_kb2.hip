@@ -1,5 +1,5 @@
 // nfk_fused_kb2.hip -- fused NSF layer kernel instances with 2 fp16 hidden k-blocks of 32
-// (H = 64, or H = 65..68 with an f32 tail step).
+// (H = 64, or H = 65..68 with an f16 tail step).
 #include "nfk_fused_impl.h"
 
 namespace nfk_fused {

@@ -1,5 +1,5 @@
 // nfk_fused_kb3.hip -- fused NSF layer kernel instances with 3 fp16 hidden k-blocks of 32
-// (H = 96, or H = 97..100 with an f32 tail step).
+// (H = 96, or H = 97..100 with an f16 tail step).
 #include "nfk_fused_impl.h"
 
 namespace nfk_fused {

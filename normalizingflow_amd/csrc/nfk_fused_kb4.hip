@@ -1,5 +1,5 @@
 // nfk_fused_kb4.hip -- fused NSF layer kernel instances with 4 fp16 hidden k-blocks of 32
-// (H = 128, or H = 129..132 with an f32 tail step).
+// (H = 128, or H = 129..132 with an f16 tail step).
 #include "nfk_fused_impl.h"
 
 namespace nfk_fused {

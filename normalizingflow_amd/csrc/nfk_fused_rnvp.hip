@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_rnvp(RArgs a) {
 
         // ---- phase 0: layer 1 of s and t from the (per-wave scaled) input half
         h8 bsh[KBH], bsl[KBH], bth[KBH], btl[KBH];
-        float bst, btt;
+        h4 bst, btt;
         {
             float mx = 0.0f;
 #pragma unroll
@@ -310,12 +310,12 @@ __device__ inline uint32_t f16_pair(float v0, float v1, int part) {
     return (uint32_t)__builtin_bit_cast(uint16_t, r0) | ((uint32_t)__builtin_bit_cast(uint16_t, r1) << 16);
 }
 
-// word wl of block blk of a gemm_h-form record (f16 blocks, f32 tail, bias)
+// word wl of block blk of a gemm_h-form record (f16 blocks, tail blocks, bias)
 // with nt tiles; rows: weight row pointer (or null) per (tile, row)
 template <class RowF, class BiasF>
 __device__ uint32_t rec_word(int blk, int wl, const RLayout& L, int nt, float sc, float bsc, RowF row_of,
                              BiasF bias_of) {
-    const int nf = L.KBH * nt * 2, ntg = L.T1 ? (nt + 3) / 4 : 0;
+    const int nf = L.KBH * nt * 2, ntg = L.T1 ? (nt + 1) / 2 : 0;
     if (blk < nf) {
         const int part = blk & 1, idx = blk >> 1, kb = idx / nt, t = idx - kb * nt;
         const int lane = wl >> 2, j = 2 * (wl & 3), k0 = 32 * kb + 8 * (lane >> 4) + j;
@@ -328,15 +328,7 @@ __device__ uint32_t rec_word(int blk, int wl, const RLayout& L, int nt, float sc
         }
         return f16_pair(v0, v1, part);
     }
-    if (blk < nf + ntg) {
-        const int g = blk - nf, lane = wl >> 2, e = wl & 3, t = 4 * g + e, k = 32 * L.KBH + (lane >> 4);
-        float v = 0.0f;
-        if (t < nt && k < L.H) {
-            const float* w = row_of(t, lane & 15);
-            if (w != nullptr) v = w[k] * sc;
-        }
-        return __float_as_uint(v);
-    }
+    if (blk < nf + ntg) return tail_word(blk - nf, wl, nt, 32 * L.KBH, L.H, sc, row_of);
     const int t = wl >> 4, i = wl & 15;
     return __float_as_uint(t < nt ? bias_of(t, i) * bsc : 0.0f);
 }

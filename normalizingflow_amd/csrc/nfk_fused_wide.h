@@ -348,7 +348,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
     NFK_MARK(tr);  // prologue done
 
     // ---- layer 1 (S1 sub-steps) and layer 2 (S2 sub-steps)
-    float btail;
+    h4 btail;
     {
         f32x4 h[HT];
         wide_phase<KBH, K, INV, HT>(a, s, a.S1, a.KB1, bh, bl, h, bsc, slot0, slot1, wid, lane, tr);
