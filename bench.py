@@ -69,9 +69,10 @@ METRICS = {
 
 # conditioner arithmetic of the fused layer kernels per workload
 _SPLIT = "fp16 two-way split (hi+lo, 3 MFMA products, fp32 accumulate, power-of-two pre-scaling)"
+_TAIL = "; the 4 tail features of H=100 as one 16x16x16 f16 MFMA per tile holding the same 3 products"
 ARITH = {
-    "c3": _SPLIT + "; 4-feature k-tail on f32 MFMA (nfk_fused_impl.h)",
-    "c2": _SPLIT + "; 4-feature k-tail on f32 MFMA (nfk_fused_rnvp.hip)",
+    "c3": _SPLIT + _TAIL + " (nfk_fused_impl.h)",
+    "c2": _SPLIT + _TAIL + " (nfk_fused_rnvp.hip)",
     "c5": _SPLIT + " (nfk_fused_wide.h)",
 }
 # the line's dtype: what the path computes in (fp32 values and outputs; the
@@ -194,14 +195,43 @@ def valu_floor_ms(insts, per_launch_scale=1.0):
     return cyc / N_SIMD / (CLOCK_GHZ * 1e9) * 1e3
 
 
+MFMA_CYC = 16.0  # MI355X_MICROARCH.md: 16x16x32 f16/bf16 back-to-back on one SIMD (16x16x16 f16 the same)
+
+
+def mfma_per_wave_layer(workload):
+    """MFMA instructions one 16-sample wave issues per layer in the fused
+    kernels' formulation: per (output tile, 32-wide k-block) the 3 fp16-split
+    products, per tile one tail MFMA when H = 32 KBH + 1..4."""
+    desc, kind, kw, D, L = WORKLOADS[workload]
+    H = kw["hidden_dim"]
+    kbf, R = divmod(H, 32)
+    T1 = 1 if (0 < R <= 4 and kbf >= 1) else 0
+    KBH = kbf if (R == 0 or T1) else kbf + 1
+    HT = 2 * KBH + T1
+    per_tile = 3 * KBH + T1
+    if kind == "RealNVP":
+        n = kw["dim"] // 2
+        NO, KBI = n // 16, (n // 16 + 1) // 2
+        return 4 * (KBI * HT * 3 + HT * per_tile + NO * per_tile)
+    n_lo, n_up = kw["size"], kw["size"] * (kw["dim"] - 1)
+    K = kw["K"]
+    if n_lo + n_up <= 128:  # k_fused_nsf: 16-coordinate chunks of W, H (K tiles), D (K-1)
+        tiles = ((n_up + 15) // 16) * (3 * K - 1)
+    else:                   # k_fused_nsf_wide: 8-coordinate chunks of ceil(K/2), ceil(K/2), K/2 tiles
+        tiles = ((n_up + 7) // 8) * (2 * ((K + 1) // 2) + K // 2)
+    return ((n_lo + 31) // 32) * HT * 3 + HT * per_tile + tiles * per_tile
+
+
 def _floors(flops_f16, flops_f32, B, per, insts, name, workload, n_steps):
     """(bound, t_floor_ms, floors) of a fused kernel launch: the MFMA floor of
-    its formulation (every fp16-split product as 3 MFMAs at the dense fp16
-    rate, the k-tail on f32 MFMA) and, when its PMC instruction counts are
-    committed, the VALU-issue floor; the binding floor is the larger."""
-    t_mfma = (flops_f32 / (PEAK_FP32_TFLOPS * 1e12) + 3.0 * flops_f16 / (PEAK_FP16_TFLOPS * 1e12)) \
-        * B * per * 1e3
-    floors = {"mfma_ms": round(t_mfma, 4)}
+    its formulation (mfma_per_wave_layer instructions per 16 samples and layer
+    at MFMA_CYC each on the 1024 SIMDs) and, when its PMC instruction counts
+    are committed, the VALU-issue floor; the binding floor is the larger."""
+    n_mfma = mfma_per_wave_layer(workload)
+    t_mfma = n_mfma * MFMA_CYC * (B / 16.0) * per / N_SIMD / (CLOCK_GHZ * 1e9) * 1e3
+    floors = {"mfma_ms": round(t_mfma, 4),
+              "mfma_basis": "%d MFMA per 16 samples and layer x %g cyc on 1024 SIMDs at %.1f GHz"
+                            % (n_mfma, MFMA_CYC, CLOCK_GHZ)}
     t_valu = None
     if insts:
         scale = (B / insts["batch"]) * (per / insts.get("layers", 1))
@@ -227,12 +257,12 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
     desc, kind, kw, D, L = WORKLOADS[workload]
     B = per_gpu_batch
     insts = load_insts(name, workload)
-    if name in ("nfk_fused_nsf", "nfk_fused_nsf_chain", "nfk_fused_realnvp"):
+    if name in ("nfk_fused_nsf", "nfk_fused_nsf_chain", "nfk_fused_realnvp", "nfk_fused_realnvp_chain"):
         H = kw["hidden_dim"]
         kbf, R = divmod(H, 32)
         tail = R if (0 < R <= 4 and kbf >= 1) else 0
-        if name == "nfk_fused_realnvp":
-            per = 1
+        if name in ("nfk_fused_realnvp", "nfk_fused_realnvp_chain"):
+            per = L * n_steps / n_launch if name == "nfk_fused_realnvp_chain" else 1
             n = kw["dim"] // 2
             f32 = 4 * 2.0 * tail * (H + n)                       # k-tails of layers 2-3, 4 nets
             f16 = 4 * 2.0 * (n * H + H * H + H * n) - f32         # 131,200/sample
@@ -254,9 +284,8 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
                 "floor_ms": round(t_floor, 4), "floors": floors,
                 "per_launch": "%d samples x %g layers x %.0f flop (fp32-equivalent)"
                               % (B, per, flops / B / per),
-                "peak_basis": "fp32-equivalent flop per launch / the binding floor; MFMA floor: "
-                              "%.0f flop/sample/layer as 3 fp16 products (%.1f TF dense) + %.0f on "
-                              "f32 MFMA (%.1f TF)" % (f16, PEAK_FP16_TFLOPS, f32, PEAK_FP32_TFLOPS),
+                "peak_basis": "fp32-equivalent flop per launch / the binding floor (the larger of "
+                              "the MFMA floor and the VALU-issue floor, see floors)",
                 "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
     if name == "nfk_rqs_coupling":
         n_up = kw["size"] * (kw["dim"] - 1)

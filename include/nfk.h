@@ -259,6 +259,34 @@ int nfk_fused_realnvp(const float* x, int64_t ldx, const float* wpack, int32_t h
                       float* z, int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
                       int32_t inverse, nfk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Chained RealNVP layers: nlayers consecutive RealNVP layers of one shape in
+ * ONE launch (NormalizingFlowModel's layer loop, models.py:13-20 / 22-29 /
+ * 37-40, over RealNVP.forward / inverse, flows.py:52-76).  Each layer's x is
+ * the previous layer's z (the lower/upper halves keep their positions), so x
+ * rows stay in LDS from the first layer to the last; z and log|det| are
+ * bitwise those of nlayers nfk_fused_realnvp launches in the same order.
+ *   wpacks: DEVICE array of nlayers pack pointers (nfk_fused_realnvp_pack:
+ *           where nfk_fused_realnvp_chain_max() != 0 the pack also holds the
+ *           chain's weight stream), in execution order (reversed layer order
+ *           when inverse != 0, as the caller runs them).
+ *   z: [batch, 2*half_dim] or NULL when log_prob is given.
+ *   log_prob: nullable; the isotropic-Normal prior epilogue (the reference's
+ *           "Normal" prior, applications/src/setup.py:25-30): log_prob[b] =
+ *           log N(z_b; 0, prior_scale^2 I) + log|det|_b (prior_half_log_det =
+ *           Sigma log of the scale_tril diagonal), and a NaN in z ORs
+ *           NFK_ST_NAN_Z into status[0] (nullable).
+ *   x, z rows 16-byte aligned (ldx, ldz multiples of 4).
+ * nfk_fused_realnvp_chain_max(): most layers per launch (0: the chain form
+ * does not apply to this shape; use nfk_fused_realnvp per layer).
+ * ------------------------------------------------------------------------- */
+int nfk_fused_realnvp_chain_max(int32_t half_dim, int32_t hidden);
+int nfk_fused_realnvp_chain(const float* x, int64_t ldx, const float* const* wpacks, int32_t nlayers,
+                            int32_t half_dim, int32_t hidden, float* z, int64_t ldz, float* logdet,
+                            int32_t logdet_mode, int64_t batch, int32_t inverse, int32_t* status,
+                            float* log_prob, float prior_scale, float prior_half_log_det,
+                            nfk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

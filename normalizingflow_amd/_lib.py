@@ -84,6 +84,13 @@ SIGNATURES = {
         P, I64, P, I32, I32,            # x, ldx, wpack, half_dim, hidden
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
         I64, I32, P]),                  # batch, inverse, stream
+    "nfk_fused_realnvp_chain_max": (ctypes.c_int, [I32, I32]),
+    "nfk_fused_realnvp_chain": (ctypes.c_int, [
+        P, I64, P, I32,                 # x, ldx, wpacks, nlayers
+        I32, I32,                       # half_dim, hidden
+        P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
+        I64, I32, P,                    # batch, inverse, status
+        P, F32, F32, P]),               # log_prob, prior_scale, prior_half_log_det, stream
 }
 
 _lock = threading.Lock()

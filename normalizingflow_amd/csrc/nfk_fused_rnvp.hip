@@ -25,7 +25,9 @@
 //   4 pr + 3: layer 3 of s and t (two sub-records) + the affine update
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -426,6 +428,352 @@ bool rshape_ok(int n, int H) {
     return kb;
 }
 
+// ---------------------------------------------------------------- chain form
+// k_rnvp_chain: every layer of a run of RealNVP layers in ONE launch.  Each
+// wave keeps its 16 x rows in an LDS tile from the first layer to the last
+// (lower half at columns [0, XI), upper at [XI, 2 XI); the layers read and
+// overwrite it in place) and writes z -- or only log p, with the isotropic
+// Normal prior as the epilogue -- at the end.
+// Work split as the split-form NSF kernel (nfk_fused_impl.h): 4-wave
+// workgroups, one wave per SIMD, three workgroups per CU.  The conditioner
+// weights stream through TWO LDS slots as a sequence of equal sub-records
+// (the pack's chain stream, built by k_rnvp_stream): per net, the layer-1
+// record, then layer 2 and layer 3 in sub-records of kRNS output tiles.  At
+// the barrier that ends the GEMM of sub-record k every wave has read slot
+// k & 1 and (vmcnt(0) before it) has landed its part of sub-record k + 1 in
+// the other slot, so the copy of k + 2 goes into slot k & 1 and overlaps the
+// GEMM of k + 1: one barrier per sub-record, no copy latency exposed (the
+// RealNVP epilogues are too short to cover a copy, unlike the spline's).
+// Per half-coupling the s net runs first (its output tiles kept in
+// registers), then the t net on the same input operands, then the affine
+// update of the target half (flows.py:56-63, inverse 68-75).  The
+// arithmetic and its order are those of k_fused_rnvp, so z and log|det| are
+// bitwise those of one k_fused_rnvp launch per layer.
+constexpr int kRNS = 2;  // output tiles per layer-2 / layer-3 sub-record
+
+struct RChainDims {
+    int HT, KBI, XI, RS, NP2, NP3, NSUB, NTB, B1, BP, SB;
+    size_t lds;
+};
+
+__host__ __device__ constexpr RChainDims rchain_dims(int KBH, int T1, int NO) {
+    RChainDims d{};
+    d.HT = 2 * KBH + (T1 ? 1 : 0);
+    d.KBI = (NO + 1) / 2;
+    d.XI = 32 * d.KBI;
+    d.RS = 2 * d.XI + 4;  // tile row stride (floats): rows 4 banks apart, 16-B reads conflict-free
+    d.NP2 = (d.HT + kRNS - 1) / kRNS;
+    d.NP3 = (NO + kRNS - 1) / kRNS;
+    d.NSUB = 1 + d.NP2 + d.NP3;  // sub-records per net
+    d.NTB = T1 ? (kRNS + 1) / 2 : 0;
+    d.B1 = d.KBI * d.HT * 2 + 1;          // layer-1 record (input_gemm form)
+    d.BP = KBH * kRNS * 2 + d.NTB + 1;    // a layer-2/3 sub-record (stage_tiles form)
+    d.SB = (((d.B1 > d.BP ? d.B1 : d.BP) + 3) / 4) * 4;  // slot blocks: a multiple of the 4 waves
+    d.lds = (size_t)2 * d.SB * 1024 + (size_t)4 * 16 * d.RS * sizeof(float);
+    return d;
+}
+
+// floats of one layer's chain stream: 2 pairs x 2 nets x NSUB sub-records of SB blocks
+__host__ __device__ inline int64_t rchain_stream_floats(const RLayout& L) {
+    const RChainDims d = rchain_dims(L.KBH, L.T1, L.NO);
+    return (int64_t)4 * d.NSUB * d.SB * 256;
+}
+
+// the chain form applies where three workgroups share a CU (LDS counted in
+// the 1280-B allocation granule of nfk_fused_impl.h)
+inline bool rchain_ok(const RLayout& L) {
+    const RChainDims d = rchain_dims(L.KBH, L.T1, L.NO);
+    return 3 * lds_alloc(d.lds) <= (size_t)kLdsBytes;
+}
+
+// Block b of a kRNS-tile sub-record (tiles [t0, t0 + kRNS) of a record with
+// nt tiles) -> block of the record, -1 for none (stage_tiles' layout).
+__device__ inline int rchain_tile_src(int b, int kbh, int t1, int nt, int t0) {
+    const int nf = kbh * kRNS * 2, ntb = t1 ? (kRNS + 1) / 2 : 0;
+    const int nts = (nt - t0) < kRNS ? (nt - t0) : kRNS;
+    if (b < nf) {
+        const int kb = b / (2 * kRNS), r = b - kb * 2 * kRNS;
+        if ((r >> 1) >= nts) return -1;
+        return (kb * nt + t0 + (r >> 1)) * 2 + (r & 1);
+    }
+    if (b < nf + ntb) return kbh * nt * 2 + (t0 >> 1) + (b - nf);
+    if (b == nf + ntb) return kbh * nt * 2 + (t1 ? (nt + 1) / 2 : 0);
+    return -1;
+}
+
+// The chain stream of a pack (after k_rnvp_pack wrote its records): sub-record
+// u = (2 pr + net) NSUB + j, j = 0: the net's layer-1 record; 1..NP2: its
+// layer-2 tiles [(j-1) kRNS, ..); then its layer-3 tiles; zero padding to SB.
+__global__ __launch_bounds__(256) void k_rnvp_stream(float* pack, RLayout L, int64_t o_stream) {
+    const RChainDims d = rchain_dims(L.KBH, L.T1, L.NO);
+    const int64_t total = rchain_stream_floats(L);
+    int off[4];
+    off[0] = 0;
+    for (int i = 1; i < 4; ++i) off[i] = off[i - 1] + L.rec[i - 1];
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const int wl = (int)(g & 255);
+        const int64_t blk = g >> 8;
+        const int u = (int)(blk / d.SB), b = (int)(blk - (int64_t)u * d.SB);
+        const int pr = u / (2 * d.NSUB), rem = u - pr * 2 * d.NSUB, net = rem / d.NSUB, j = rem - net * d.NSUB;
+        const int base = pr * L.pair_blocks;
+        int src = -1;
+        if (j == 0) {
+            if (b < d.B1) src = base + off[0] + net * L.blk_l1 + b;
+        } else if (j <= d.NP2) {
+            const int r = rchain_tile_src(b, L.KBH, L.T1, d.HT, (j - 1) * kRNS);
+            if (r >= 0) src = base + off[1 + net] + r;
+        } else {
+            const int r = rchain_tile_src(b, L.KBH, L.T1, L.NO, (j - 1 - d.NP2) * kRNS);
+            if (r >= 0) src = base + off[3] + net * L.blk_l3 + r;
+        }
+        pack[o_stream + g] = src >= 0 ? pack[256 + (int64_t)src * 256 + wl] : 0.0f;
+    }
+}
+
+struct RChainArgs {
+    const float* x;
+    const float* const* packs;  // device array: the layers' packs, in execution order
+    float* z;
+    float* logdet;
+    float* log_prob;  // optional prior epilogue: log N(z; 0, s^2 I) + log|det| (z may be null)
+    int32_t* status;  // NFK_ST_NAN_Z of the prior epilogue (nullable)
+    int64_t ldx, ldz, batch;
+    int32_t n, mode, nlayers, o_stream;
+    float prior_inv_scale, prior_c2pi, prior_hld;
+};
+
+// layer-2 / layer-3 GEMM over its kRNS-tile sub-records J, J + 1, ... in
+// alternating slots (part J in slot (P + J) & 1), each followed by
+// step(that slot)
+template <int KBH, bool T1, int NT, int J, int P, class Step>
+__device__ __forceinline__ void rchain_parts(const h8 (&bh)[KBH], const h8 (&bl)[KBH], h4 bt, float4* s0,
+                                             float4* s1, int lane, f32x4 (&acc)[NT], Step&& step) {
+    constexpr int T0 = J * kRNS;
+    constexpr int N = (NT - T0) < kRNS ? (NT - T0) : kRNS;
+    float4* const sl = ((P + J) & 1) ? s1 : s0;
+    gemm_h<KBH, T1, N, kRNS, T0, NT>(bh, bl, bt, sl, lane, acc);
+    step(sl);
+    if constexpr (T0 + kRNS < NT) rchain_parts<KBH, T1, NT, J + 1, P>(bh, bl, bt, s0, s1, lane, acc, step);
+}
+
+template <int KBH, bool T1, int NO, bool INV>
+__global__ __launch_bounds__(64 * kNsfWaves, 3) void k_rnvp_chain(RChainArgs a) {
+    constexpr RChainDims d = rchain_dims(KBH, T1 ? 1 : 0, NO);
+    constexpr int HT = d.HT, KBI = d.KBI, XI = d.XI, RS = d.RS, NSUB = d.NSUB, SB = d.SB;
+    constexpr int NPL = 4 * NSUB;  // sub-records per layer (even: the slot parity repeats per layer)
+    // the arguments through the kernarg-segment pointer, re-derived opaquely
+    // per layer (as k_fused_nsf's chain form: values loaded from them are not
+    // kept live across the layer loop)
+    using ArgsK = const __attribute__((address_space(4))) RChainArgs;
+    ArgsK* A = (ArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)a;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4, sl = lane & 15;
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    float4* const slot0 = lds4;
+    float4* const slot1 = lds4 + SB * 64;
+    float* const tile = reinterpret_cast<float*>(lds4 + 2 * SB * 64) + wid * 16 * RS;
+    const int64_t b0 = ((int64_t)blockIdx.x * kNsfWaves + wid) * 16;
+    const int64_t rem = A->batch - b0;
+    const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
+    const int n = A->n, NL = A->nlayers;
+
+    // ---- sub-record staging: (nl, nj) is the next sub-record to copy, in
+    // execution order; its pack position swaps the two pairs when inverting
+    int nl = 0, nj = 0;
+    const float* nbase = A->packs[0] + A->o_stream;
+    auto stage_next = [&](float4* slot) {
+        if (nl >= NL) return;
+        const int pos = INV ? (nj < 2 * NSUB ? nj + 2 * NSUB : nj - 2 * NSUB) : nj;
+        const float* src = nbase + (int64_t)pos * SB * 256;
+        const uint32_t base = lds_addr(slot);
+#pragma unroll
+        for (int i = 0; i < SB / 4; ++i)
+            dma16(src + (int64_t)(wid + 4 * i) * 256 + lane * 4, base + (wid + 4 * i) * 1024);
+        if (++nj == NPL) {
+            nj = 0;
+            if (++nl < NL) nbase = A->packs[nl] + A->o_stream;
+        }
+    };
+    // end of the GEMM of sub-record k (slot k & 1 = freed): this wave's reads
+    // of it and its copy of k + 1 done, barrier, then the copy of k + 2 into it
+    auto step = [&](float4* freed) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stage_next(freed);
+    };
+
+    // ---- prologue: the wave's x rows into its tile (plain loads, padding
+    // columns zero), then the first two sub-records, one wait
+    {
+        const float* x = A->x;
+        const int64_t ldx = A->ldx;
+        constexpr int R4 = 2 * XI / 4;  // float4 per tile row
+        for (int i = lane; i < 16 * R4; i += 64) {
+            const int r = i / R4, c = 4 * (i - r * R4);
+            const int hf = c >= XI ? 1 : 0, cc = c - hf * XI;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (r < nrows && cc < n) v = *reinterpret_cast<const float4*>(x + (b0 + r) * ldx + hf * n + cc);
+            *reinterpret_cast<float4*>(tile + r * RS + c) = v;
+        }
+    }
+    stage_next(slot0);
+    stage_next(slot1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    const bool row_ok = sl < nrows;
+    float ld_acc = (q == 0 && row_ok && A->mode == 2) ? A->logdet[b0 + sl] : 0.0f;
+    float* const trow = tile + sl * RS;
+    for (int l = 0; l < NL; ++l) {
+        asm volatile("" : "+s"(A));
+        const float* hdr = A->packs[l];
+        float ldsum = 0.0f;
+#pragma unroll
+        for (int hk = 0; hk < 2; ++hk) {
+            const int pr = INV ? 1 - hk : hk;     // net pair of this half: 0 = (s1, t1), 1 = (s2, t2)
+            const int in_off = pr == 0 ? 0 : XI;  // pair 0 reads the lower half, updates the upper
+            const int tg_off = pr == 0 ? XI : 0;
+            const float* un = hdr + 16 + pr * 6;  // unscale factors of (net, layer) in the pair
+            // layer-1 operands of the input half, per-wave power-of-two scaled (as k_fused_rnvp)
+            h8 xh[KBI], xl[KBI];
+            int ex = 0;
+            {
+                float mx = 0.0f;
+#pragma unroll
+                for (int kb = 0; kb < KBI; ++kb) {
+                    const float4 u = *reinterpret_cast<const float4*>(trow + in_off + 32 * kb + 4 * q);
+                    const float4 v = *reinterpret_cast<const float4*>(trow + in_off + 32 * kb + 16 + 4 * q);
+                    mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))),
+                                         fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+                if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
+                const float sx = ldexpf(1.0f, 14 - ex);
+#pragma unroll
+                for (int kb = 0; kb < KBI; ++kb) {
+                    const float4 u = *reinterpret_cast<const float4*>(trow + in_off + 32 * kb + 4 * q);
+                    const float4 v = *reinterpret_cast<const float4*>(trow + in_off + 32 * kb + 16 + 4 * q);
+                    const float x8[8] = {u.x * sx, u.y * sx, u.z * sx, u.w * sx,
+                                         v.x * sx, v.y * sx, v.z * sx, v.w * sx};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const _Float16 hh = (_Float16)x8[j];
+                        xh[kb][j] = hh;
+                        xl[kb][j] = (_Float16)(x8[j] - (float)hh);
+                    }
+                }
+            }
+            // one net (c = 0: s, 1: t): layer 1 (sub-record 0), layer 2 (NP2
+            // sub-records), layer 3 (NP3) into out, unscaled.  A half starts at
+            // an even sub-record, so net c's sub-record j sits in slot (c NSUB + j) & 1.
+            auto run_net = [&](auto netc, f32x4 (&out)[NO]) {
+                constexpr int C = decltype(netc)::value;
+                constexpr int P0 = (C * NSUB) & 1, P2 = (C * NSUB + 1) & 1, P3 = (C * NSUB + 1 + d.NP2) & 1;
+                const float u1 = ldexpf(un[3 * C], ex - 14);
+                h8 bh[KBH], bl[KBH];
+                h4 bt;
+                {
+                    f32x4 h1[HT];
+                    input_gemm<KBI, HT>(xh, xl, P0 ? slot1 : slot0, 1.0f / u1, lane, h1);
+                    step(P0 ? slot1 : slot0);
+                    act_operands<KBH, T1, HT>(h1, -2.0f * kL2E * u1, bh, bl, bt);
+                }
+                {
+                    f32x4 h2[HT];
+                    rchain_parts<KBH, T1, HT, 0, P2>(bh, bl, bt, slot0, slot1, lane, h2, step);
+                    act_operands<KBH, T1, HT>(h2, -2.0f * kL2E * un[3 * C + 1], bh, bl, bt);
+                }
+                rchain_parts<KBH, T1, NO, 0, P3>(bh, bl, bt, slot0, slot1, lane, out, step);
+            };
+            f32x4 so[NO], to[NO];
+            run_net(std::integral_constant<int, 0>{}, so);
+            run_net(std::integral_constant<int, 1>{}, to);
+            // affine update of the target half (flows.py:56-63; inverse 68-75)
+            const float u3s = un[2], u3t = un[5];
+#pragma unroll
+            for (int t = 0; t < NO; ++t) {
+                float* p = trow + tg_off + 16 * t + 4 * q;
+                const float4 xv = *reinterpret_cast<const float4*>(p);
+                const float xr[4] = {xv.x, xv.y, xv.z, xv.w};
+                float o[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float sv = so[t][r] * u3s, tv = to[t][r] * u3t;
+                    if (INV) {
+                        o[r] = (xr[r] - tv) * expf(-sv);
+                        ldsum += -sv;
+                    } else {
+                        o[r] = tv + xr[r] * expf(sv);
+                        ldsum += sv;
+                    }
+                }
+                *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+            }
+        }
+        // the layer's log|det| added to the running sum, in the order of one
+        // k_fused_rnvp launch per layer
+        float v = ldsum;
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        ld_acc = ld_acc + v;
+    }
+
+    // ---- tail: z rows (lower | upper), log|det|, or the prior epilogue
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (A->z != nullptr) {
+        float* z = A->z;
+        const int64_t ldz = A->ldz;
+        const int N4 = n / 2;  // float4 per z row (2 n floats)
+        for (int i = lane; i < 16 * N4; i += 64) {
+            const int r = i / N4, c = 4 * (i - r * N4);
+            const int hf = c >= n ? 1 : 0;
+            if (r < nrows)
+                *reinterpret_cast<float4*>(z + (b0 + r) * ldz + c) =
+                    *reinterpret_cast<const float4*>(tile + r * RS + hf * XI + c - hf * n);
+        }
+    }
+    if (q == 0 && row_ok && A->mode != 0) A->logdet[b0 + sl] = ld_acc;
+    if (A->log_prob != nullptr) {
+        // log N(z; 0, s^2 I) + log|det| from the tile row: the four lanes of sample
+        // sl sum output columns 4 (q + 4 i) .. + 3 as k_normal_lp4 (y = z / s)
+        const float il = A->prior_inv_scale;
+        float m = 0.0f;
+        for (int g = q; g < (n >> 1); g += 4) {
+            const int o = 4 * g, c = o < n ? o : XI + o - n;
+            const float4 zv = *reinterpret_cast<const float4*>(trow + c);
+            const float y0 = zv.x * il, y1 = zv.y * il, y2 = zv.z * il, y3 = zv.w * il;
+            m += (y0 * y0 + y1 * y1) + (y2 * y2 + y3 * y3);
+        }
+        m += __shfl_xor(m, 16, 64);
+        m += __shfl_xor(m, 32, 64);
+        const float lp = -0.5f * (A->prior_c2pi + m) - A->prior_hld;
+        if (q == 0 && row_ok) A->log_prob[b0 + sl] = lp + ld_acc;
+        // a NaN in z: the prior's argument validation raises (NFK_ST_NAN_Z)
+        if (__any(row_ok && m != m) && lane == 0 && A->status != nullptr) atomicOr(A->status, NFK_ST_NAN_Z);
+    }
+}
+
+template <int KBH, int T1, int NO>
+int launch_chain(const RChainArgs& a, bool inv, hipStream_t st) {
+    const int64_t blocks = (a.batch + kNsfWaves * 16 - 1) / (kNsfWaves * 16);
+    if (blocks == 0) return 0;
+    const size_t lds = rchain_dims(KBH, T1, NO).lds;
+    if (inv)
+        hipLaunchKernelGGL((k_rnvp_chain<KBH, T1 != 0, NO, true>), dim3((unsigned)blocks), dim3(64 * kNsfWaves),
+                           lds, st, a);
+    else
+        hipLaunchKernelGGL((k_rnvp_chain<KBH, T1 != 0, NO, false>), dim3((unsigned)blocks), dim3(64 * kNsfWaves),
+                           lds, st, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
 template <int KBH, int T1, int NO>
 int launch(const RArgs& a, size_t lds, bool inv, hipStream_t st) {
     const int64_t blocks = (a.batch + kWaves * 16 - 1) / (kWaves * 16);
@@ -448,8 +796,15 @@ extern "C" int nfk_fused_realnvp_supported(int32_t half_dim, int32_t hidden) {
     return rshape_ok(half_dim, hidden) ? 1 : 0;
 }
 
+// floats of a pack: the per-layer kernel's records, then (where the chain form
+// applies) the chain stream
+static int64_t rpack_floats(int32_t half_dim, int32_t hidden) {
+    const RLayout L = make_rlayout(half_dim, hidden);
+    return L.total + (rchain_ok(L) ? rchain_stream_floats(L) : 0);
+}
+
 extern "C" int64_t nfk_fused_realnvp_pack_elems(int32_t half_dim, int32_t hidden) {
-    return rshape_ok(half_dim, hidden) ? make_rlayout(half_dim, hidden).total : 0;
+    return rshape_ok(half_dim, hidden) ? rpack_floats(half_dim, hidden) : 0;
 }
 
 extern "C" int nfk_fused_realnvp_pack(const float* const* nets, int32_t half_dim, int32_t hidden, float* wpack,
@@ -470,6 +825,11 @@ extern "C" int nfk_fused_realnvp_pack(const float* const* nets, int32_t half_dim
     int64_t g = (a.L.total + 255) / 256;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_rnvp_pack, dim3((unsigned)g), dim3(256), 0, st, a);
+    if (rchain_ok(a.L)) {  // the chain stream, re-cut from the records just written
+        int64_t gs = (rchain_stream_floats(a.L) + 255) / 256;
+        if (gs > 8192) gs = 8192;
+        hipLaunchKernelGGL(k_rnvp_stream, dim3((unsigned)gs), dim3(256), 0, st, wpack, a.L, a.L.total);
+    }
     e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -513,4 +873,53 @@ extern "C" int nfk_fused_realnvp(const float* x, int64_t ldx, const float* wpack
 #undef RDISPATCH_KB
 #undef RDISPATCH
     return nfk_set_error("nfk_fused_realnvp: no kernel instance");
+}
+
+extern "C" int nfk_fused_realnvp_chain_max(int32_t half_dim, int32_t hidden) {
+    if (!rshape_ok(half_dim, hidden) || !rchain_ok(make_rlayout(half_dim, hidden))) return 0;
+    return 1 << 16;  // no per-layer state in LDS: any run length
+}
+
+extern "C" int nfk_fused_realnvp_chain(const float* x, int64_t ldx, const float* const* wpacks, int32_t nlayers,
+                                       int32_t half_dim, int32_t hidden, float* z, int64_t ldz, float* logdet,
+                                       int32_t logdet_mode, int64_t batch, int32_t inverse, int32_t* status,
+                                       float* log_prob, float prior_scale, float prior_half_log_det,
+                                       nfk_stream_t stream) {
+    if (nfk_fused_realnvp_chain_max(half_dim, hidden) == 0)
+        return nfk_set_error("nfk_fused_realnvp_chain: shape not supported");
+    if (nlayers < 1 || nlayers > (1 << 16)) return nfk_set_error("nfk_fused_realnvp_chain: bad layer count");
+    if (batch < 0) return nfk_set_error("nfk_fused_realnvp_chain: bad batch");
+    if (batch == 0) return 0;
+    if (!x || !wpacks || (!z && !log_prob)) return nfk_set_error("nfk_fused_realnvp_chain: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_realnvp_chain: null logdet");
+    if (log_prob && !(prior_scale > 0.0f)) return nfk_set_error("nfk_fused_realnvp_chain: bad prior scale");
+    if (((uintptr_t)x % 16) != 0 || ((uintptr_t)z % 16) != 0 || ldx % 4 != 0 || (z && ldz % 4 != 0))
+        return nfk_set_error("nfk_fused_realnvp_chain: x and z rows must be 16-byte aligned");
+    const RLayout L = make_rlayout(half_dim, hidden);
+    RChainArgs a;
+    a.x = x;
+    a.packs = wpacks;
+    a.z = z;
+    a.logdet = logdet;
+    a.log_prob = log_prob;
+    a.status = status;
+    a.ldx = ldx;
+    a.ldz = ldz;
+    a.batch = batch;
+    a.n = half_dim;
+    a.mode = logdet_mode;
+    a.nlayers = nlayers;
+    a.o_stream = (int32_t)L.total;
+    a.prior_inv_scale = log_prob ? 1.0f / prior_scale : 0.0f;
+    a.prior_c2pi = (float)(2 * half_dim * std::log(2.0 * M_PI));
+    a.prior_hld = prior_half_log_det;
+    hipStream_t st = (hipStream_t)stream;
+    const bool inv = inverse != 0;
+#define RDISPATCH(h, t, no) \
+    if (L.KBH == h && L.T1 == t && L.NO == no) return launch_chain<h, t, no>(a, inv, st);
+#define RDISPATCH_KB(h, t) RDISPATCH(h, t, 1) RDISPATCH(h, t, 2) RDISPATCH(h, t, 3) RDISPATCH(h, t, 4)
+    NFK_FUSED_KB(RDISPATCH_KB)
+#undef RDISPATCH_KB
+#undef RDISPATCH
+    return nfk_set_error("nfk_fused_realnvp_chain: no kernel instance");
 }

@@ -318,6 +318,15 @@ class RealNVP(_HipFlow):
         self._pack_cache = (key, pack, hidden)
         return pack
 
+    def _chain_shape(self, device):
+        """("rnvp", half_dim, hidden) when this layer runs as the fused kernel and
+        the chain form applies (so it may join an nfk_fused_realnvp_chain launch
+        with layers of the same shape), else None."""
+        if self.dim % 2 or self._fused_pack(device) is None:
+            return None
+        h, hidden = self.dim // 2, self._pack_cache[2]
+        return ("rnvp", h, hidden) if K_.fused_realnvp_chain_max(h, hidden) > 0 else None
+
     def _run(self, x, inverse, logdet, mode, status):
         h = self.dim // 2
         if x.shape[1] != self.dim or self.dim - h != h:

@@ -372,6 +372,35 @@ def fused_realnvp_pack(nets, half_dim, hidden):
     return pack
 
 
+_RCHAIN_MAX = {}
+
+
+def fused_realnvp_chain_max(half_dim, hidden):
+    """Most RealNVP layers of this shape one nfk_fused_realnvp_chain launch holds (0: none)."""
+    key = (half_dim, hidden)
+    n = _RCHAIN_MAX.get(key)
+    if n is None:
+        n = _RCHAIN_MAX[key] = int(_lib.load().nfk_fused_realnvp_chain_max(half_dim, hidden))
+    return n
+
+
+def fused_realnvp_chain(x, wpacks, nlayers, half_dim, hidden, z, *, logdet, logdet_mode, inverse=False,
+                        status=None, log_prob=None, prior_scale=1.0, prior_hld=0.0):
+    """nlayers fused RealNVP layers in one launch (include/nfk.h nfk_fused_realnvp_chain).
+    wpacks: int64 device tensor of the layers' pack pointers in execution order;
+    log_prob (optional [batch]): the isotropic-normal prior epilogue, z may be None."""
+    dev = _require_hip(x, wpacks, z, logdet, status, log_prob)
+    B = x.shape[0]
+    if wpacks.dtype != torch.int64 or wpacks.numel() != nlayers:
+        raise ValueError("wpacks must hold %d int64 pack pointers" % nlayers)
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z") if z is not None else (None, 0)
+    _timed("nfk_fused_realnvp_chain", dev, "nfk_fused_realnvp_chain", xp, ldx, wpacks.data_ptr(), nlayers,
+           half_dim, hidden, zp, ldz, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0,
+           _vec(status, 1, "status", torch.int32), _vec(log_prob, B, "log_prob"), float(prior_scale),
+           float(prior_hld), _stream(dev))
+
+
 def fused_realnvp(x, wpack, half_dim, hidden, z, *, logdet, logdet_mode, inverse=False):
     dev = _require_hip(x, wpack, z, logdet)
     B = x.shape[0]

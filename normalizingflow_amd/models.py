@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from . import config
 from . import kernels as K_
-from .flows import NSF_CL, _HipFlow, _check_input, _invalidate_after_load, _needs_grad, check_status
+from .flows import NSF_CL, RealNVP, _HipFlow, _check_input, _invalidate_after_load, _needs_grad, check_status
 
 __all__ = ["NormalizingFlowModel", "NormalizingFlow"]
 
@@ -163,9 +163,9 @@ class NormalizingFlowModel(nn.Module):
         flows = self.flows[::-1] if inverse else self.flows
         with torch.set_grad_enabled(grad):
             for item in self._groups(flows, x.device, grad):
-                if isinstance(item, tuple):  # a run of fused NSF_CL layers: one launch
+                if isinstance(item, tuple):  # a run of fused NSF_CL or RealNVP layers: one launch
                     run, shape = item
-                    k = len(run)
+                    k = sum(f._n_status for f in run)
                     x = self._run_chain(run, shape, x, inverse, logdet, status[off:off + k])
                     off += k
                     continue
@@ -194,16 +194,27 @@ class NormalizingFlowModel(nn.Module):
         return status[n_st:n_st + 1]
 
     # ------------------------------------------------------- chained launches
+    @staticmethod
+    def _is_rnvp(shape):
+        return shape[0] == "rnvp"
+
     def _groups(self, flows, device, grad):
-        """The layer sequence with every run of consecutive NSF_CL layers that
-        share one fused-kernel shape replaced by (run, shape) tuples of at most
-        nfk_fused_nsf_chain_max layers (inference only; runs of one stay single)."""
+        """The layer sequence with every run of consecutive NSF_CL layers (or of
+        RealNVP layers) that share one fused-kernel shape replaced by (run,
+        shape) tuples of at most nfk_fused_nsf_chain_max /
+        nfk_fused_realnvp_chain_max layers (inference only; runs of one stay
+        single).  RealNVP shapes are ("rnvp", half_dim, hidden)."""
         if grad or not (config.USE_FUSED and config.USE_CHAIN):
             return list(flows)
         out, run, shape = [], [], None
 
         def flush():
-            nmax = K_.fused_nsf_chain_max(*shape[:4]) if shape is not None else 0
+            if shape is None:
+                nmax = 0
+            elif self._is_rnvp(shape):
+                nmax = K_.fused_realnvp_chain_max(shape[1], shape[2])
+            else:
+                nmax = K_.fused_nsf_chain_max(*shape[:4])
             i = 0
             while i < len(run):
                 piece = run[i:i + max(nmax, 1)]
@@ -211,7 +222,7 @@ class NormalizingFlowModel(nn.Module):
                 i += len(piece)
 
         for flow in flows:
-            sh = flow._chain_shape(device) if isinstance(flow, NSF_CL) else None
+            sh = flow._chain_shape(device) if isinstance(flow, (NSF_CL, RealNVP)) else None
             if sh is not None and sh == shape:
                 run.append(flow)
                 continue
@@ -232,8 +243,8 @@ class NormalizingFlowModel(nn.Module):
         ent = self._chain_cache.get(key)
         ptrs = tuple(p.data_ptr() for p in packs)
         if ent is None or ent[0] != ptrs:
-            ent = (ptrs, torch.tensor(ptrs, dtype=torch.int64, device=x.device),
-                   _compose_maps(run, D, x.device))
+            maps = None if isinstance(run[0], RealNVP) else _compose_maps(run, D, x.device)
+            ent = (ptrs, torch.tensor(ptrs, dtype=torch.int64, device=x.device), maps)
             self._chain_cache[key] = ent
         return ent[1], ent[2]
 
@@ -248,11 +259,21 @@ class NormalizingFlowModel(nn.Module):
         if plan is None:
             return None
         run, shape, iso, wp, cm = plan
+        out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+        if self._is_rnvp(shape):
+            _, h, hidden = shape
+            if not self._chain_layout_ok(x, 2 * h):
+                return None
+            status = torch.zeros(1, dtype=torch.int32, device=x.device)  # the prior's NaN-z word
+            K_.fused_realnvp_chain(x, wp, len(run), h, hidden, None, logdet=None, logdet_mode=K_.MODE_NONE,
+                                   inverse=False, status=status, log_prob=out, prior_scale=iso[0],
+                                   prior_hld=iso[1])
+            check_status(status, 0, prior=self.prior)
+            return out
         n_lo, n_up, hidden, K, B = shape
         if not self._chain_layout_ok(x, n_lo + n_up):
             return None
         status = torch.zeros(len(run), dtype=torch.int32, device=x.device)
-        out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
         K_.fused_nsf_chain(x, wp, cm, len(run), n_lo, n_up, hidden, None, logdet=None,
                            logdet_mode=K_.MODE_NONE, K=K, tail_bound=B, inverse=False, status=status,
                            log_prob=out, prior_scale=iso[0], prior_hld=iso[1])
@@ -278,14 +299,29 @@ class NormalizingFlowModel(nn.Module):
             groups = self._groups(self.flows, x.device, False)
             if iso is not None and len(groups) == 1 and isinstance(groups[0], tuple):
                 run, shape = groups[0]
-                wp, cm = self._chain_args(run, shape[0] + shape[1], False, x)
+                wp, cm = self._chain_args(run, self._shape_dim(shape), False, x)
                 plan = (run, shape, iso, wp, cm)
             self._lp_plan_cache = (key, plan)
-        if plan is not None and self.prior.loc.shape[0] != plan[1][0] + plan[1][1]:
+        if plan is not None and self.prior.loc.shape[0] != self._shape_dim(plan[1]):
             return None  # the prior's dimension does not match: the generic path raises like torch
         return plan
 
+    @classmethod
+    def _shape_dim(cls, shape):
+        return 2 * shape[1] if cls._is_rnvp(shape) else shape[0] + shape[1]
+
     def _run_chain(self, run, shape, x, inverse, logdet, status):
+        if self._is_rnvp(shape):
+            _, h, hidden = shape
+            if not self._chain_layout_ok(x, 2 * h):
+                for flow in run:  # not the chain's layout: one launch per layer
+                    x = flow._run(x, inverse, logdet, K_.MODE_ACC, None)
+                return x
+            wp, _ = self._chain_args(run, 2 * h, inverse, x)
+            z = torch.empty_like(x, memory_format=torch.contiguous_format)
+            K_.fused_realnvp_chain(x, wp, len(run), h, hidden, z, logdet=logdet, logdet_mode=K_.MODE_ACC,
+                                   inverse=inverse)
+            return z
         n_lo, n_up, hidden, K, B = shape
         D = n_lo + n_up
         if not self._chain_layout_ok(x, D):
