@@ -137,6 +137,19 @@ int nfk_affine_coupling(const float* x_in, int64_t ld_in, const float* s, const 
                         int32_t logdet_mode, int64_t batch, int32_t n, int32_t inverse,
                         nfk_stream_t stream);
 
+/* Backward of nfk_affine_coupling (the VJP of flows.py:56/61 and 68/74 for
+ * RealNVP's training path):
+ *   forward  out = t + in e, e = exp(s):    g_in (+)= g e, g_t = g,    g_s = g in e + g_ld
+ *   inverse  out = (in - t) e, e = exp(-s): g_in (+)= g e, g_t = -g e, g_s = -g out - g_ld
+ * g = g_out (NULL: 0), g_ld = g_logdet[row] (NULL: 0); g_in written
+ * (accumulate = 0) or added to (1); g_t may be NULL forward (it equals g_out).
+ * g_s and g_t share the row stride ld_gst. */
+int nfk_affine_coupling_bwd(const float* x_in, int64_t ld_in, const float* s, const float* t,
+                            int64_t ld_st, const float* g_out, int64_t ld_g, const float* g_logdet,
+                            float* g_in, int64_t ld_gin, int32_t accumulate, float* g_s, float* g_t,
+                            int64_t ld_gst, int64_t batch, int32_t n, int32_t inverse,
+                            nfk_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Planar flow forward (nf/flows_1.py:42-60), parameters w,u [dim], b [1].
  * nonlinearity: 0 tanh (u re-parameterised to u_hat), 1 leaky_relu, 2 elu

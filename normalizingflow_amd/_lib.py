@@ -84,6 +84,11 @@ SIGNATURES = {
         P, I64, P, I32, I32,            # x, ldx, wpack, half_dim, hidden
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
         I64, I32, P]),                  # batch, inverse, stream
+    "nfk_affine_coupling_bwd": (ctypes.c_int, [
+        P, I64, P, P, I64,              # x_in, ld_in, s, t, ld_st
+        P, I64, P,                      # g_out, ld_g, g_logdet
+        P, I64, I32, P, P, I64,         # g_in, ld_gin, accumulate, g_s, g_t, ld_gst
+        I64, I32, I32, P]),             # batch, n, inverse, stream
     "nfk_fused_realnvp_chain_max": (ctypes.c_int, [I32, I32]),
     "nfk_fused_realnvp_chain": (ctypes.c_int, [
         P, I64, P, I32,                 # x, ldx, wpacks, nlayers

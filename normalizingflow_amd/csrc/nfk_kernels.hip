@@ -623,6 +623,72 @@ extern "C" int nfk_affine_coupling(const float* x_in, int64_t ld_in, const float
     return launch_status("nfk_affine_coupling");
 }
 
+// Backward of the affine half-coupling (the VJP of k_affine): per element,
+//   forward  out = t + in e,  e = exp(s):   g_in = g e,  g_t = g,    g_s = g in e + g_ld
+//   inverse  out = (in - t) e, e = exp(-s): g_in = g e,  g_t = -g e, g_s = -g out - g_ld
+// with g = g_out (0 where null) and g_ld the row's log|det| gradient (0 where
+// null).  g_in is written (acc = 0) or accumulated (acc = 1); g_t may be null
+// in the forward direction (it is g_out itself).
+template <int W, bool INV>
+__global__ __launch_bounds__(256) void k_affine_bwd(const float* __restrict__ xin, int64_t ld_in,
+                                                    const float* __restrict__ s,
+                                                    const float* __restrict__ t, int64_t ld_st,
+                                                    const float* __restrict__ gout, int64_t ld_g,
+                                                    const float* __restrict__ gld, float* gin,
+                                                    int64_t ld_gin, int acc, float* gs, float* gt,
+                                                    int64_t ld_gst, int64_t batch, int n) {
+    NFK_ROW_PROLOGUE(W)
+    for (int64_t r0 = wave * RPW; r0 < batch; r0 += nwave * RPW) {
+        const int64_t b = r0 + sub;
+        if (b >= batch) continue;
+        const float gl = gld ? gld[b] : 0.0f;
+        for (int c = c0; c < n; c += W) {
+            const float sv = s[b * ld_st + c], xv = xin[b * ld_in + c];
+            const float g = gout ? gout[b * ld_g + c] : 0.0f;
+            float vi, vs, vt;
+            if (INV) {
+                const float e = expf(-sv), o = (xv - t[b * ld_st + c]) * e;
+                vi = g * e;
+                vt = -g * e;
+                vs = -g * o - gl;
+            } else {
+                const float e = expf(sv);
+                vi = g * e;
+                vt = g;
+                vs = g * xv * e + gl;
+            }
+            float* pi = gin + b * ld_gin + c;
+            *pi = acc ? *pi + vi : vi;
+            gs[b * ld_gst + c] = vs;
+            if (gt) gt[b * ld_gst + c] = vt;
+        }
+    }
+}
+
+extern "C" int nfk_affine_coupling_bwd(const float* x_in, int64_t ld_in, const float* s, const float* t,
+                                       int64_t ld_st, const float* g_out, int64_t ld_g, const float* g_logdet,
+                                       float* g_in, int64_t ld_gin, int32_t accumulate, float* g_s, float* g_t,
+                                       int64_t ld_gst, int64_t batch, int32_t n, int32_t inverse,
+                                       nfk_stream_t stream) {
+    if (batch < 0 || n <= 0) return nfk_set_error("nfk_affine_coupling_bwd: bad sizes");
+    if (batch == 0) return 0;
+    if (!x_in || !s || !g_in || !g_s || (inverse && (!t || !g_t)))
+        return nfk_set_error("nfk_affine_coupling_bwd: null pointer");
+    const int w = lanes_for(n);
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned g = grid_for_rows(batch, w);
+#define CALL(W)                                                                                      \
+    if (inverse)                                                                                     \
+        hipLaunchKernelGGL((k_affine_bwd<W, true>), dim3(g), dim3(256), 0, st, x_in, ld_in, s, t, ld_st,  \
+                           g_out, ld_g, g_logdet, g_in, ld_gin, accumulate, g_s, g_t, ld_gst, batch, n); \
+    else                                                                                             \
+        hipLaunchKernelGGL((k_affine_bwd<W, false>), dim3(g), dim3(256), 0, st, x_in, ld_in, s, t, ld_st, \
+                           g_out, ld_g, g_logdet, g_in, ld_gin, accumulate, g_s, g_t, ld_gst, batch, n);
+    NFK_W_DISPATCH(w, CALL)
+#undef CALL
+    return launch_status("nfk_affine_coupling_bwd");
+}
+
 // ---------------------------------------------------------------------------
 // planar flow (flows_1.py:42-60)
 // ---------------------------------------------------------------------------

@@ -1,0 +1,93 @@
+"""Recompute-backward of the stock FCNN conditioner (nf/flows.py:20-35:
+Linear -> Tanh -> Linear -> Tanh -> Linear) for the training path.
+
+The layer kernels save only their input; the backward recomputes the three
+activations and forms the vector-Jacobian products by hand instead of through
+autograd, so each product is a GEMM of the shape that suits the device:
+
+* input and hidden gradients (g @ W, M = batch): one GEMM each;
+* weight gradients g^T h reduce over the batch (against [h | 1], so the same
+  GEMM's last column is the bias gradient) (K = 2^20 rows against 100 x 100
+  or 736 x 100 outputs).  A single GEMM of that shape has a few dozen output
+  tiles for 256 CUs, so the batch is split into S slices and the S partial
+  products (one batched GEMM) summed: split-K by hand (wgrad).
+
+Same values as autograd through nn.Linear / nn.Tanh up to fp32 summation
+order (tests/test_gpu_grad.py checks the layer gradients against the oracle's
+autograd)."""
+from __future__ import annotations
+
+import torch
+
+_WG_ROWS = 8192   # rows per split-K slice of the weight-gradient GEMMs
+_WG_SLICES = 64   # at most this many slices
+
+
+def linears(p, pre):
+    """(W1, b1, W2, b2, W3, b3) of FCNN ``pre`` from the name -> tensor map."""
+    return tuple(p[pre + "network.%d.%s" % (i, k)] for i in (0, 2, 4) for k in ("weight", "bias"))
+
+
+def _with_ones(B, H, like):
+    """[B, H + 1] with a ones last column: the hidden activations are written
+    into [:, :H], so one GEMM against it yields a weight gradient and, in its
+    last column, the bias gradient (the column sum of the output gradient)."""
+    a = torch.empty(B, H + 1, dtype=like.dtype, device=like.device)
+    a[:, H].fill_(1.0)
+    return a
+
+
+def forward_saved(p, pre, x):
+    """psi(x) and the activations its backward needs: (x, [h1 | 1], [h2 | 1])."""
+    W1, b1, W2, b2, W3, b3 = linears(p, pre)
+    B, H = x.shape[0], W1.shape[0]
+    h1a = _with_ones(B, H, x)
+    torch.tanh(torch.addmm(b1, x, W1.t()), out=h1a[:, :H])
+    h2a = _with_ones(B, H, x)
+    torch.tanh(torch.addmm(b2, h1a[:, :H], W2.t()), out=h2a[:, :H])
+    return torch.addmm(b3, h2a[:, :H], W3.t()), (x, h1a, h2a)
+
+
+def wgrad(g, h):
+    """g^T h for g [B, M], h [B, N]: split over the batch (see module doc)."""
+    B = g.shape[0]
+    S = min(_WG_SLICES, B // _WG_ROWS)
+    if S <= 1:
+        return g.t() @ h
+    R = B // S
+    out = torch.bmm(g[:S * R].view(S, R, -1).transpose(1, 2), h[:S * R].view(S, R, -1)).sum(0)
+    if S * R < B:
+        out += g[S * R:].t() @ h[S * R:]
+    return out
+
+
+def vjp(p, pre, cache, g, need_x, need):
+    """(dL/dx or None, {name: grad}) of psi at the cached activations for the
+    output gradient g; ``need``: the parameter names whose gradient is wanted."""
+    x, h1a, h2a = cache
+    H = h1a.shape[1] - 1
+    h1, h2 = h1a[:, :H], h2a[:, :H]
+    W1, b1, W2, b2, W3, b3 = linears(p, pre)
+    names = [pre + "network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias")]
+    grads = {}
+
+    def put(i, g_out, act_a):
+        """weight and bias gradient of Linear i from ONE GEMM against [act | 1]"""
+        nw, nb = names[2 * i], names[2 * i + 1]
+        if nw in need or nb in need:
+            wb = wgrad(g_out, act_a)
+            if nw in need:
+                grads[nw] = wb[:, :-1].contiguous()
+            if nb in need:
+                grads[nb] = wb[:, -1].contiguous()
+
+    put(2, g, h2a)
+    ga2 = torch.ops.aten.tanh_backward(g @ W3, h2)
+    put(1, ga2, h1a)
+    ga1 = torch.ops.aten.tanh_backward(ga2 @ W2, h1)
+    if names[0] in need:
+        grads[names[0]] = wgrad(ga1, x)
+    if names[1] in need:
+        grads[names[1]] = ga1.sum(0)
+    gx = ga1 @ W1 if need_x else None
+    return gx, grads

@@ -39,6 +39,7 @@ import torch.nn.functional as F
 import torch.nn.init as init
 
 from . import config
+from . import fcnn_grad
 from . import kernels as K_
 from . import split_gemm
 from . import torch_math
@@ -354,6 +355,69 @@ class RealNVP(_HipFlow):
             K_.affine_coupling(up, s1, t1, zup, logdet=logdet, logdet_mode=m2, inverse=True)
         return z
 
+    _NETS = ("s1", "t1", "s2", "t2")
+
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward by hand for four stock FCNN conditioners (else None: the
+        generic autograd recompute): the conditioners recomputed and
+        differentiated by fcnn_grad (GEMMs, split-K weight gradients), each
+        affine half-coupling by nfk_affine_coupling_bwd (flows.py:52-76)."""
+        want_names = {"%s.network.%d.%s" % (n, i, k) for n in self._NETS for i in (0, 2, 4)
+                      for k in ("weight", "bias")}
+        if not all(_is_stock_fcnn(getattr(self, n)) for n in self._NETS) or set(names) != want_names \
+                or x.shape[1] != self.dim or self.dim % 2:
+            return None
+        h = self.dim // 2
+        p = {n: t.detach() for n, t in zip(names, params)}
+        want = {n for n, r in zip(names, need[1:]) if r}
+        x = x.detach()
+        B = x.shape[0]
+        gz = torch.zeros_like(x) if gz is None else gz.contiguous()
+        gldc = None if gld is None else gld.contiguous()
+        grads = {}
+        gx = torch.empty_like(x)
+
+        # forward:  up' = t1(lo) + up e^{s1(lo)};  lo' = t2(up') + lo e^{s2(up')}
+        # inverse:  lo' = (lo - t2(up)) e^{-s2(up)};  up' = (up - t1(lo')) e^{-s1(lo')}
+        lo, up = x[:, :h], x[:, h:]
+        order = (("s1", "t1", lo, up), ("s2", "t2", None, lo)) if not inverse else \
+                (("s2", "t2", up, lo), ("s1", "t1", None, up))
+        # recompute: the first half's conditioner input is an input half, the
+        # second one's is the first half's output
+        sn, tn, src, tgt = order[0]
+        s_a, c_sa = fcnn_grad.forward_saved(p, sn + ".", src)
+        t_a, c_ta = fcnn_grad.forward_saved(p, tn + ".", src)
+        out_a = t_a + tgt * torch.exp(s_a) if not inverse else (tgt - t_a) * torch.exp(-s_a)
+        sn2, tn2, _, tgt2 = order[1]
+        s_b, c_sb = fcnn_grad.forward_saved(p, sn2 + ".", out_a)
+        t_b, c_tb = fcnn_grad.forward_saved(p, tn2 + ".", out_a)
+        # the second half-coupling's output half of z is its target (lo forward, up inverse)
+        g_a_out = gz[:, h:] if not inverse else gz[:, :h]  # gradient reaching out_a from z
+        g_b_out = gz[:, :h] if not inverse else gz[:, h:]
+        gx_b = gx[:, :h] if not inverse else gx[:, h:]      # gradient slot of tgt2 (x half)
+        gx_a = gx[:, h:] if not inverse else gx[:, :h]      # gradient slot of tgt (x half)
+        g_s = torch.empty(B, h, dtype=x.dtype, device=x.device)
+        g_t = torch.empty_like(g_s) if inverse else None
+        K_.affine_coupling_bwd(tgt2, s_b, t_b, g_b_out, gldc, gx_b, g_s, g_t, inverse=inverse)
+        g_tb = g_t if inverse else g_b_out
+        g_in_b_s, gr = fcnn_grad.vjp(p, sn2 + ".", c_sb, g_s, True, want)
+        grads.update(gr)
+        g_in_b_t, gr = fcnn_grad.vjp(p, tn2 + ".", c_tb, g_tb, True, want)
+        grads.update(gr)
+        g_outa = g_a_out + g_in_b_s + g_in_b_t
+        g_s2 = torch.empty_like(g_s)
+        g_t2 = torch.empty_like(g_s) if inverse else None
+        K_.affine_coupling_bwd(tgt, s_a, t_a, g_outa, gldc, gx_a, g_s2, g_t2, inverse=inverse)
+        g_ta = g_t2 if inverse else g_outa
+        g_src_s, gr = fcnn_grad.vjp(p, sn + ".", c_sa, g_s2, need[0], want)
+        grads.update(gr)
+        g_src_t, gr = fcnn_grad.vjp(p, tn + ".", c_ta, g_ta, need[0], want)
+        grads.update(gr)
+        if need[0]:
+            g_src = gx[:, :h] if not inverse else gx[:, h:]  # src is lo forward, up inverse = gx_b's half
+            g_src += g_src_s + g_src_t
+        return [gx if need[0] else None] + [grads.get(n) for n in names]
+
     def forward(self, x):
         return self._call(x, False)
 
@@ -463,17 +527,27 @@ class NSF_CL(_HipFlow):
         return z
 
     def _vjp(self, x, names, params, gz, gld, inverse, need):
-        """Backward: the conditioner is recomputed and differentiated by torch
-        (hipBLASLt GEMMs: fp16-split products, split_gemm, for the stock FCNN),
-        the spline by nfk_rqs_coupling_bwd."""
+        """Backward: the conditioner is recomputed and, for the stock FCNN,
+        differentiated by hand (fcnn_grad: hipBLASLt GEMMs, the weight
+        gradients split over the batch), any other one by torch autograd; the
+        spline by nfk_rqs_coupling_bwd."""
         maps = self._maps(x.device)
-        with torch.enable_grad():
-            lower = x.detach().index_select(1, maps.lo_in_long).requires_grad_(need[0])
-            pd = {n: t.detach().requires_grad_(r) for n, t, r in zip(names, params, need[1:])}
-            if config.SPLIT_GEMM and _is_stock_fcnn(self.psi):
-                raw = split_gemm.fcnn(pd, "psi.", lower)  # fp16-split GEMMs (fp32-accurate)
-            else:
-                raw = torch_math.conditioner(self, pd, "psi", lower)
+        # stock FCNN: recompute and differentiate by hand (fcnn_grad: split-K
+        # weight gradients); any other conditioner through autograd
+        manual = _is_stock_fcnn(self.psi) and not config.SPLIT_GEMM and set(names) == set(
+            "psi.network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias"))
+        if manual:
+            lower = x.detach().index_select(1, maps.lo_in_long)
+            pmap = {n: t.detach() for n, t in zip(names, params)}
+            raw, cache = fcnn_grad.forward_saved(pmap, "psi.", lower)
+        else:
+            with torch.enable_grad():
+                lower = x.detach().index_select(1, maps.lo_in_long).requires_grad_(need[0])
+                pd = {n: t.detach().requires_grad_(r) for n, t, r in zip(names, params, need[1:])}
+                if config.SPLIT_GEMM and _is_stock_fcnn(self.psi):
+                    raw = split_gemm.fcnn(pd, "psi.", lower)  # fp16-split GEMMs (fp32-accurate)
+                else:
+                    raw = torch_math.conditioner(self, pd, "psi", lower)
         rawc = raw.detach().contiguous()
         gp = torch.empty_like(rawc)
         gx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
@@ -483,6 +557,12 @@ class NSF_CL(_HipFlow):
                             None if gld is None else gld.contiguous(), gp, gx, lo_in=maps.lo_in,
                             lo_out=maps.lo_out, K=self.K, left=-b, right=b, bottom=-b, top=b,
                             tails=True, param_mode=0, inverse=inverse)
+        if manual:
+            want = {n for n, r in zip(names, need[1:]) if r}
+            g_lower, grads = fcnn_grad.vjp(pmap, "psi.", cache, gp, need[0], want)
+            if g_lower is not None:
+                gx.index_add_(1, maps.lo_in_long, g_lower)
+            return [gx if need[0] else None] + [grads.get(n) for n in names]
         inputs = [t for t in [lower] + list(pd.values()) if t.requires_grad]
         got = list(torch.autograd.grad(raw, inputs, gp, allow_unused=True)) if inputs else []
         g_lower = got.pop(0) if need[0] else None

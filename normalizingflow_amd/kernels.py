@@ -231,6 +231,36 @@ def affine_coupling(x_in, s, t, x_out, *, logdet=None, logdet_mode=MODE_NONE, in
               logdet_mode, B, n, 1 if inverse else 0, _stream(dev))
 
 
+def affine_coupling_bwd(x_in, s, t, g_out, g_logdet, g_in, g_s, g_t=None, *, accumulate=False, inverse=False):
+    """VJP of affine_coupling (include/nfk.h nfk_affine_coupling_bwd); g_s / g_t
+    are written (contiguous [B, n]), g_in written or accumulated."""
+    dev = _require_hip(x_in, s, t, g_out, g_logdet, g_in, g_s, g_t)
+    B, n = x_in.shape
+    for name, v in (("s", s), ("t", t), ("g_out", g_out), ("g_in", g_in), ("g_s", g_s), ("g_t", g_t)):
+        if v is not None and tuple(v.shape) != (B, n):
+            raise ValueError("affine_coupling_bwd: %s has shape %s, want %s" % (name, tuple(v.shape), (B, n)))
+    if inverse and (t is None or g_t is None):
+        raise ValueError("affine_coupling_bwd: the inverse needs t and g_t")
+    xp, ldi = _mat(x_in, "x_in")
+    sp, lds = _mat(s, "s")
+    tp = None
+    if t is not None:
+        tp, ldt = _mat(t, "t")
+        if ldt != lds and B > 1:
+            raise ValueError("affine_coupling_bwd: s and t need one row stride")
+    gp, ldg = _mat(g_out, "g_out") if g_out is not None else (None, 0)
+    ip, ldgi = _mat(g_in, "g_in")
+    gsp, ldgs = _mat(g_s, "g_s")
+    gtp = None
+    if g_t is not None:
+        gtp, ldgt = _mat(g_t, "g_t")
+        if ldgt != ldgs and B > 1:
+            raise ValueError("affine_coupling_bwd: g_s and g_t need one row stride")
+    _timed("nfk_affine_coupling_bwd", dev, "nfk_affine_coupling_bwd", xp, ldi, sp, tp, lds, gp, ldg,
+           _vec(g_logdet, B, "g_logdet"), ip, ldgi, 1 if accumulate else 0, gsp, gtp, ldgs, B, n,
+           1 if inverse else 0, _stream(dev))
+
+
 PLANAR_NL = {"tanh": 0, "leaky_relu": 1, "elu": 2}
 
 

@@ -61,11 +61,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle train step")
-    ap.add_argument("--no-split-gemm", action="store_true",
-                    help="fp32 conditioner GEMMs in the NSF_CL backward (config.SPLIT_GEMM off)")
+    ap.add_argument("--split-gemm", action="store_true",
+                    help="fp16-split conditioner GEMMs in the NSF_CL backward (config.SPLIT_GEMM on; "
+                         "default off: hand-written fp32 backward, fcnn_grad)")
     args = ap.parse_args()
     from normalizingflow_amd import config
-    config.SPLIT_GEMM = not args.no_split_gemm
+    config.SPLIT_GEMM = args.split_gemm
     dev = torch.device("cuda", 0)
     model, sd, _ = bench.build_model(args.workload, dev)
     x = torch.randn(args.batch, bench.WORKLOADS[args.workload][3], device=dev)
