@@ -255,6 +255,35 @@ int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* const* wpacks,
                         float prior_half_log_det, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Training backward of one fused NSF_CL layer (the VJP of flows.py:227-253,
+ * utils.py:58-152 at the layer input x): the conditioner recomputed on the
+ * matrix cores as nfk_fused_nsf computes it, and the spline VJP of every
+ * element on the logits in registers.  Writes
+ *   gparams [batch, n_up, 3K-1]: dL/d(conditioner output), the input of the
+ *            conditioner's own backward (GEMMs outside);
+ *   gx [batch, D]: upper coordinates dL/dx through the spline, lower ones the
+ *            identity part (gz of their output column; the conditioner's part
+ *            is added by the caller);
+ *   h1, h2 [batch, ldh]: the two tanh activations in columns [0, hidden) and
+ *            1.0 at column hidden (ldh >= hidden + 1, a multiple of 4; rows
+ *            16-byte aligned), for the weight-gradient GEMMs.
+ * gz (dL/dz, [batch, D]) and glogdet (dL/dlog|det|, [batch]) are nullable.
+ * vpack: nfk_fused_nsf_vjp_pack (the pack's records in 8-coordinate chunks and
+ * their sub-record stream).  Supported: nfk_fused_nsf_vjp_pack_elems() > 0
+ * (n_lo <= 32, D <= 128 and a multiple of 4; (KBH, tail, K) instantiated).
+ * ------------------------------------------------------------------------- */
+int64_t nfk_fused_nsf_vjp_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K);
+int nfk_fused_nsf_vjp_pack(const float* w0, const float* b0, const float* w2, const float* b2,
+                           const float* w4, const float* b4, int32_t n_lo, int32_t n_up,
+                           int32_t hidden, int32_t K, float* vpack, nfk_stream_t stream);
+int nfk_fused_nsf_vjp(const float* x, int64_t ldx, const float* vpack, const int32_t* up_in,
+                      const int32_t* up_out, int32_t n_up, const int32_t* lo_in,
+                      const int32_t* lo_out, int32_t n_lo, int32_t hidden, const float* gz,
+                      int64_t ldgz, const float* glogdet, float* gparams, float* gx, int64_t ldgx,
+                      float* h1, float* h2, int64_t ldh, int64_t batch, int32_t K,
+                      double tail_bound, int32_t inverse, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Fused RealNVP layer: both affine half-couplings with their four FCNN
  * conditioners (s1, t1, s2, t2) in one launch; replaces RealNVP.forward /
  * inverse (flows.py:44-76).  x, z: [batch, 2*half_dim] row-major.

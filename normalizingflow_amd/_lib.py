@@ -77,6 +77,15 @@ SIGNATURES = {
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
         I64, I32, F64, I32, P,          # batch, K, tail_bound, inverse, status
         P, F32, F32, P]),               # log_prob, prior_scale, prior_half_log_det, stream
+    "nfk_fused_nsf_vjp_pack_elems": (ctypes.c_int64, [I32, I32, I32, I32]),
+    "nfk_fused_nsf_vjp_pack": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P, P]),
+    "nfk_fused_nsf_vjp": (ctypes.c_int, [
+        P, I64, P, P, P, I32,           # x, ldx, vpack, up_in, up_out, n_up
+        P, P, I32, I32,                 # lo_in, lo_out, n_lo, hidden
+        P, I64, P,                      # gz, ldgz, glogdet
+        P, P, I64,                      # gparams, gx, ldgx
+        P, P, I64,                      # h1, h2, ldh
+        I64, I32, F64, I32, P]),        # batch, K, tail_bound, inverse, stream
     "nfk_fused_realnvp_supported": (ctypes.c_int, [I32, I32]),
     "nfk_fused_realnvp_pack_elems": (ctypes.c_int64, [I32, I32]),
     "nfk_fused_realnvp_pack": (ctypes.c_int, [P, I32, I32, P, P]),

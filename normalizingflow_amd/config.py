@@ -16,6 +16,9 @@ USE_FUSED      run NSF_CL layers whose conditioner is the stock FCNN through the
 USE_CHAIN      in inference, run consecutive fused NSF_CL layers of one shape as
                one nfk_fused_nsf_chain launch (x resident in LDS across the
                layers); results are bitwise those of the per-layer launches.
+USE_FUSED_VJP  training: NSF_CL's backward through nfk_fused_nsf_vjp (conditioner
+               recompute on the matrix cores + spline VJP in one kernel) where
+               the shape is supported; off: recompute GEMMs + nfk_rqs_coupling_bwd.
 SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
                fp16-split products on the fp16 matrix cores (split_gemm.py,
                fp32-accurate) instead of fp32 GEMMs.  Off: torch.mm with
@@ -25,4 +28,5 @@ SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
 STRICT_CHECKS = True
 USE_FUSED = True
 USE_CHAIN = True
+USE_FUSED_VJP = True
 SPLIT_GEMM = False

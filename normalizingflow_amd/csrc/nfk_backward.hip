@@ -32,12 +32,15 @@
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
+#include "nfk_spline_bwd.h"
 
 int nfk_set_error(const char* msg);
 NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, double top,
                               int tails, double min_w, double min_h, double min_d);
 
 namespace {
+
+using namespace nfk_bwd;
 
 int launch_status(const char* what) {
     hipError_t e = hipGetLastError();
@@ -48,212 +51,6 @@ int launch_status(const char* what) {
         return (int)e;
     }
     return 0;
-}
-
-// d softplus(v) / dv as torch's softplus_backward (beta 1, threshold 20)
-__device__ __forceinline__ float softplus_grad(float v) {
-    if (v > 20.0f) return 1.0f;
-    const float e = expf(v);
-    return e / (e + 1.0f);
-}
-
-// softmax backward in place: g <- s * (g - sum(g * s))
-template <int K>
-__device__ __forceinline__ void softmax_bwd(const float (&s)[K], float (&g)[K]) {
-    float dot = 0.0f;
-#pragma unroll
-    for (int i = 0; i < K; ++i) dot += g[i] * s[i];
-#pragma unroll
-    for (int i = 0; i < K; ++i) g[i] = s[i] * (g[i] - dot);
-}
-
-// softmax forward, reference summation order (shared with the forward kernels)
-template <int K>
-__device__ __forceinline__ void softmax_fwd(const float (&u)[K], float (&s)[K]) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) s[i] = u[i];
-    nfk_softmax<K>(s);
-}
-
-// One side (widths or heights): logits -> (s0 if PRE) -> s1 -> edges.
-template <int K, bool PRE>
-struct KnotSide {
-    float s0[K];  // first softmax (PRE only)
-    float s1[K];  // second softmax
-    float edge[K + 1];
-
-    __device__ __forceinline__ void build(const float (&u)[K], float scale2b, float lo, float hi,
-                                          float span, float min_b, float fb) {
-        if (PRE) {
-            softmax_fwd<K>(u, s0);
-#pragma unroll
-            for (int i = 0; i < K; ++i) s1[i] = scale2b * s0[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; ++i) s1[i] = u[i];
-        }
-        nfk_softmax<K>(s1);
-        double acc = 0.0;
-        edge[0] = lo;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            acc += (double)(min_b + fb * s1[i]);
-            edge[i + 1] = span * (float)acc + lo;
-        }
-        edge[K] = hi;
-    }
-
-    // gradient w.r.t. the logits from the adjoints of (edge_k, size_k = edge_k+1 - edge_k)
-    __device__ __forceinline__ void backward(int k, float g_pos, float g_size, float span, float fb,
-                                             float scale2b, float (&g)[K]) const {
-        // adjoint of edge_k and edge_k+1 (the pinned ends 0 and K carry none)
-        const float ga = (k >= 1) ? (g_pos - g_size) : 0.0f;
-        const float gb = (k + 1 <= K - 1) ? g_size : 0.0f;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            float v = 0.0f;
-            if (j < k) v += ga;
-            if (j <= k) v += gb;
-            g[j] = span * fb * v;  // d edge_e / d s1_j = span * fb for j < e
-        }
-        softmax_bwd<K>(s1, g);
-        if (PRE) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) g[j] *= scale2b;
-            softmax_bwd<K>(s0, g);
-        }
-    }
-};
-
-template <int K>
-__device__ __forceinline__ float sel(const float (&a)[K], int k) { return nfk_sel<K>(a, k); }
-
-// Backward of one spline element.  wr/hr/dr in: logits; out: their gradients.
-template <int K, bool INV, bool PRE, bool DFULL>
-__device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float (&hr)[K],
-                                                 float (&dr)[NfkDN<K, DFULL>::n],
-                                                 const NfkSplineConst& c, float gout, float gl) {
-    constexpr int DN = NfkDN<K, DFULL>::n;
-    const bool inside = !c.tails || ((x >= c.lo) && (x <= c.hi));
-    if (!inside) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) wr[i] = hr[i] = 0.0f;
-#pragma unroll
-        for (int i = 0; i < DN; ++i) dr[i] = 0.0f;
-        return gout;
-    }
-    KnotSide<K, PRE> W, H;
-    W.build(wr, c.scale2b, c.lo, c.hi, c.span, c.min_w, c.fw);
-    H.build(hr, c.scale2b, c.ylo, c.yhi, c.yspan, c.min_h, c.fh);
-    const int k = nfk_bin<K>(INV ? H.edge : W.edge, x, c.knot_eps);
-    float cw_k = W.edge[0], w_k = W.edge[1] - W.edge[0], ch_k = H.edge[0], h_k = H.edge[1] - H.edge[0];
-#pragma unroll
-    for (int j = 1; j < K; ++j) {
-        if (k == j) {
-            cw_k = W.edge[j];
-            w_k = W.edge[j + 1] - W.edge[j];
-            ch_k = H.edge[j];
-            h_k = H.edge[j + 1] - H.edge[j];
-        }
-    }
-    // derivative logits used by bin k: v0 -> d_k, v1 -> d_k1 (pre-RQS-softplus
-    // values), with their source index (-1: the constant boundary pad)
-    int i0 = -1, i1 = -1;
-    float v0 = c.dpad, v1 = c.dpad, r0 = 0.0f, r1 = 0.0f;  // r: NSF_CL raw logit (PRE)
-    if (DFULL) {
-        i0 = k;
-        i1 = k + 1;
-#pragma unroll
-        for (int j = 0; j < DN; ++j) {
-            if (j == i0) v0 = dr[j];
-            if (j == i1) v1 = dr[j];
-        }
-    } else {
-        i0 = k - 1;  // padded index k holds logit k-1
-        i1 = (k + 1 <= K - 1) ? k : -1;
-#pragma unroll
-        for (int j = 0; j < DN; ++j) {
-            if (j == i0) r0 = dr[j];
-            if (j == i1) r1 = dr[j];
-        }
-        if (i0 >= 0) v0 = PRE ? nfk_softplus(r0) : r0;
-        if (i1 >= 0) v1 = PRE ? nfk_softplus(r1) : r1;
-    }
-    const float d0 = c.min_d + nfk_softplus(v0);
-    const float d1 = c.min_d + nfk_softplus(v1);
-    const float delta = h_k / w_k;
-    const float gap = (d0 + d1) - 2.0f * delta;
-
-    float th;
-    if (INV) {
-        const float y = x - ch_k;
-        const float qa = y * gap + h_k * (delta - d0);
-        const float qb = h_k * d0 - y * gap;
-        const float qc = (-delta) * y;
-        const float disc = qb * qb - (4.0f * qa) * qc;
-        th = (2.0f * qc) / (-qb - sqrtf(fmaxf(disc, 0.0f)));
-    } else {
-        th = (x - cw_k) / w_k;
-    }
-    const float s = th * (1.0f - th);
-    const float omt = 1.0f - th;
-    const float Dn = delta + gap * s;
-    const float N = h_k * (delta * th * th + d0 * s);
-    const float R = N / Dn;
-    const float M = delta * delta * (d1 * th * th + 2.0f * delta * s + d0 * omt * omt);
-    const float iDn = 1.0f / Dn, iM = 1.0f / M;
-    const float one_m2t = 1.0f - 2.0f * th;
-    // partials of Dn, N, M over the base variables
-    const float Dn_t = gap * one_m2t, Dn_dl = 1.0f - 2.0f * s, Dn_d0 = s, Dn_d1 = s;
-    const float N_t = h_k * (2.0f * delta * th + d0 * one_m2t), N_dl = h_k * th * th;
-    const float N_h = delta * th * th + d0 * s, N_d0 = h_k * s;
-    const float M_t = delta * delta * (2.0f * d1 * th + 2.0f * delta * one_m2t - 2.0f * d0 * omt);
-    const float M_dl = 2.0f * delta * (d1 * th * th + 2.0f * delta * s + d0 * omt * omt) +
-                       2.0f * delta * delta * s;
-    const float M_d0 = delta * delta * omt * omt, M_d1 = delta * delta * th * th;
-    // f and lad partials over (theta, delta, h explicit, d0, d1)
-    const float f_t = (N_t - R * Dn_t) * iDn, f_dl = (N_dl - R * Dn_dl) * iDn;
-    const float f_h = N_h * iDn, f_d0 = (N_d0 - R * Dn_d0) * iDn, f_d1 = (-R * Dn_d1) * iDn;
-    const float l_t = M_t * iM - 2.0f * Dn_t * iDn, l_dl = M_dl * iM - 2.0f * Dn_dl * iDn;
-    const float l_d0 = M_d0 * iM - 2.0f * Dn_d0 * iDn, l_d1 = M_d1 * iM - 2.0f * Dn_d1 * iDn;
-    const float iw = 1.0f / w_k;
-
-    float a, b, gx;  // g_bin = a * f_bin + b * lad_bin
-    if (INV) {
-        const float fprime = f_t * iw;
-        const float gbar = gout - gl * (l_t * iw);
-        gx = gbar / fprime;
-        a = -gx;
-        b = -gl;
-    } else {
-        a = gout;
-        b = gl;
-        gx = a * f_t * iw + b * l_t * iw;
-    }
-    const float G_t = a * f_t + b * l_t, G_dl = a * f_dl + b * l_dl;
-    const float g_cw = -G_t * iw;
-    const float g_w = -(G_t * th + G_dl * delta) * iw;
-    const float g_ch = a;
-    const float g_h = a * f_h + G_dl * iw;
-    const float g_d0 = a * f_d0 + b * l_d0;
-    const float g_d1 = a * f_d1 + b * l_d1;
-
-    W.backward(k, g_cw, g_w, c.span, c.fw, c.scale2b, wr);
-    H.backward(k, g_ch, g_h, c.yspan, c.fh, c.scale2b, hr);
-    // derivative logits: d = min_d + softplus(v); v = softplus(r) under PRE
-    float gv0 = g_d0 * softplus_grad(v0), gv1 = g_d1 * softplus_grad(v1);
-    if (PRE && !DFULL) {
-        gv0 *= softplus_grad(r0);
-        gv1 *= softplus_grad(r1);
-    }
-#pragma unroll
-    for (int j = 0; j < DN; ++j) {
-        float g = 0.0f;
-        if (j == i0) g += gv0;
-        if (j == i1) g += gv1;
-        dr[j] = g;
-    }
-    return gx;
 }
 
 struct RqsBwdArgs {

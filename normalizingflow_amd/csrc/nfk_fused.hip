@@ -370,6 +370,73 @@ extern "C" int nfk_debug_fused_form(int form) {
     return prev;
 }
 
+// ---- the VJP pack (nfk_fused_vjp.hip): records in the 8-coordinate layout,
+// then the stream of SB-block sub-records re-cut from them (vjp_dims)
+namespace {
+__global__ __launch_bounds__(256) void k_vjp_stream(float* pack, Layout L) {
+    const VjpDims d = vjp_dims(L.KBH, L.T1, L.K);
+    const int64_t total = (int64_t)vjp_nsub(d, L.NCH) * d.SB * 256;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const int wl = (int)(g & 255);
+        const int64_t blk = g >> 8;
+        const int u = (int)(blk / d.SB), b = (int)(blk - (int64_t)u * d.SB);
+        int64_t src = -1;  // record block (from the start of the records, o_h1)
+        if (u == 0) {
+            if (b < L.blk_h1) src = b;
+        } else if (u <= d.NP2) {
+            const int r = subrec_tile_src(b, L.KBH, L.T1, kVNS, d.HT, (u - 1) * kVNS);
+            if (r >= 0) src = L.blk_h1 + r;
+        } else {
+            const int v = u - 1 - d.NP2, ch = v / d.SPC, w = v - ch * d.SPC;
+            int64_t rec = L.blk_h1 + L.blk_h2 + (int64_t)ch * L.blk_chunk;
+            int nt = d.KW, t0;
+            if (w < d.NPW) {
+                t0 = w * kVNS;
+            } else if (w < 2 * d.NPW) {
+                rec += L.blk_w;
+                t0 = (w - d.NPW) * kVNS;
+            } else {
+                rec += 2 * L.blk_w;
+                nt = d.KD;
+                t0 = (w - 2 * d.NPW) * kVNS;
+            }
+            const int r = subrec_tile_src(b, L.KBH, L.T1, kVNS, nt, t0);
+            if (r >= 0) src = rec + r;
+        }
+        pack[L.total + g] = src >= 0 ? pack[L.o_h1 + src * 256 + wl] : 0.0f;
+    }
+}
+}  // namespace
+
+extern "C" int64_t nfk_fused_nsf_vjp_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
+    if (!vjp_ok(n_lo, n_up, hidden, K)) return 0;
+    const Layout L = make_layout(n_lo, n_up, hidden, K, 1);
+    return L.total + (int64_t)vjp_nsub(vjp_dims(L.KBH, L.T1, K), L.NCH) * vjp_dims(L.KBH, L.T1, K).SB * 256;
+}
+
+extern "C" int nfk_fused_nsf_vjp_pack(const float* w0, const float* b0, const float* w2, const float* b2,
+                                      const float* w4, const float* b4, int32_t n_lo, int32_t n_up,
+                                      int32_t hidden, int32_t K, float* vpack, nfk_stream_t stream) {
+    if (!vjp_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_vjp_pack: shape not supported");
+    if (!w0 || !b0 || !w2 || !b2 || !w4 || !b4 || !vpack)
+        return nfk_set_error("nfk_fused_nsf_vjp_pack: null pointer");
+    PackArgs a{w0, b0, w2, b2, w4, b4, vpack, make_layout(n_lo, n_up, hidden, K, 1)};
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(vpack, 0, 3 * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_pack_max, dim3(64), dim3(256), 0, st, a);
+    int64_t g = (a.L.total + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, st, a);
+    const int64_t n = nfk_fused_nsf_vjp_pack_elems(n_lo, n_up, hidden, K) - a.L.total;
+    int64_t gs = (n + 255) / 256;
+    if (gs > 8192) gs = 8192;
+    hipLaunchKernelGGL(k_vjp_stream, dim3((unsigned)gs), dim3(256), 0, st, vpack, a.L);
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
 extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
     return pack_ok(n_lo, n_up, hidden, K) ? 1 : 0;
 }

@@ -496,6 +496,32 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
     }
 }
 
+// layer 1 from a whole layer-1 record (KBI f16 k-blocks x HT tiles, then the
+// bias block): acc = b 2^(s1+sx) + 2^s1 W1 . (2^sx in)^T (fp16 split), the
+// operands xh/xl of k-block kb holding inputs 32 kb + 8 q + j (in the
+// record's input order)
+template <int KBI, int HT>
+__device__ __forceinline__ void input_gemm(const h8 (&xh)[KBI], const h8 (&xl)[KBI], const float4* rec,
+                                           float bsc, int lane, f32x4 (&acc)[HT]) {
+    const int q = lane >> 4;
+    const float4* bias = rec + KBI * HT * 2 * 64;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+        const float4 bv = bias[t * 4 + q];
+        acc[t] = f32x4{bv.x * bsc, bv.y * bsc, bv.z * bsc, bv.w * bsc};
+    }
+#pragma unroll
+    for (int kb = 0; kb < KBI; ++kb)
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+            const h8 ahi = __builtin_bit_cast(h8, rec[((kb * HT + t) * 2) * 64 + lane]);
+            const h8 alo = __builtin_bit_cast(h8, rec[((kb * HT + t) * 2 + 1) * 64 + lane]);
+            acc[t] = mfma16(alo, xh[kb], acc[t]);
+            acc[t] = mfma16(ahi, xl[kb], acc[t]);
+            acc[t] = mfma16(ahi, xh[kb], acc[t]);
+        }
+}
+
 // activations of a hidden layer -> B operands of the next product
 // (T1: the tail B operand, k-groups {a_hi, a_lo, a_hi, a_hi} over the tail
 // features held in registers 0..3 of the tail tile; A's group 3 is zero)
@@ -513,6 +539,7 @@ __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float v = tanh_scaled(h[HT - 1][r], c2);
+            h[HT - 1][r] = v;  // (kept like the other tiles' activations: store_act reads them)
             hi[r] = (_Float16)v;
             lo[r] = (_Float16)(v - (float)hi[r]);
         }
@@ -697,6 +724,22 @@ __device__ __forceinline__ void stage_tiles(const float* __restrict__ rec, int n
         }
         dma16(rec + (int64_t)src * 256 + lane * 4, base + i * 1024);
     }
+}
+
+// Block b of an NS-tile sub-record (tiles [t0, t0 + NS) of a record with nt
+// tiles, at tile stride NS per k-block, then its tail blocks and the record's
+// bias block: stage_tiles' slot layout) -> block of the record; -1 for none.
+__host__ __device__ inline int subrec_tile_src(int b, int kbh, int t1, int ns, int nt, int t0) {
+    const int nf = kbh * ns * 2, ntb = t1 ? (ns + 1) / 2 : 0;
+    const int nts = (nt - t0) < ns ? (nt - t0) : ns;
+    if (b < nf) {
+        const int kb = b / (2 * ns), r = b - kb * 2 * ns;
+        if ((r >> 1) >= nts) return -1;
+        return (kb * nt + t0 + (r >> 1)) * 2 + (r & 1);
+    }
+    if (b < nf + ntb) return kbh * nt * 2 + (t0 >> 1) + (b - nf);
+    if (b == nf + ntb) return kbh * nt * 2 + (t1 ? (nt + 1) / 2 : 0);
+    return -1;
 }
 
 // Stage sub-record s of the split sequence: layer 1 (whole), NH2 layer-2
@@ -1320,6 +1363,46 @@ int launch_fused(const FusedArgs& a, size_t lds, bool inv, bool split, bool chai
 #define NFK_FUSED_EXTERN(KBH, T1, K) \
     extern template int launch_fused<KBH, T1, K>(const FusedArgs& a, size_t lds, bool inv, bool split, \
                                                  bool chain, hipStream_t st);
+
+// ---- recompute + VJP form (nfk_fused_vjp.hip): the layer's records in the
+// 8-coordinate (wide = 1) layout re-cut into sub-records of kVNS output tiles
+// (layer 1 whole), each padded to SB blocks, double-buffered in two LDS slots.
+// Stream order: layer 1, NP2 layer-2 parts, then per 8-coordinate chunk the
+// W (NPW parts), H (NPW) and D (NPD) records.
+constexpr int kVNS = 2;
+struct VjpDims {
+    int HT, NP2, KW, KD, NPW, NPD, SPC, B1, BP, SB;
+};
+__host__ __device__ constexpr VjpDims vjp_dims(int KBH, int T1, int K) {
+    VjpDims d{};
+    d.HT = 2 * KBH + (T1 ? 1 : 0);
+    d.NP2 = (d.HT + kVNS - 1) / kVNS;
+    d.KW = (K + 1) / 2;
+    d.KD = K / 2;
+    d.NPW = (d.KW + kVNS - 1) / kVNS;
+    d.NPD = (d.KD + kVNS - 1) / kVNS;
+    d.SPC = 2 * d.NPW + d.NPD;
+    d.B1 = d.HT * 2 + 1;  // the layer-1 record with one input k-block (n_lo <= 32)
+    d.BP = KBH * kVNS * 2 + (T1 ? (kVNS + 1) / 2 : 0) + 1;
+    d.SB = (((d.B1 > d.BP ? d.B1 : d.BP) + 3) / 4) * 4;
+    return d;
+}
+__host__ __device__ inline int vjp_nsub(const VjpDims& d, int nch) { return 1 + d.NP2 + nch * d.SPC; }
+inline size_t vjp_lds_bytes(const VjpDims& d, int D) {
+    return (size_t)2 * d.SB * 1024 + (size_t)((2 * D + 3) / 4) * 16 + (size_t)kNsfWaves * 16 * (D + 1) * sizeof(float);
+}
+// instantiated (KBH, T1, K) of the VJP kernel
+#define NFK_VJP_SHAPES(X) X(1, 1, 4) X(1, 1, 8) X(2, 0, 4) X(2, 0, 8) X(3, 0, 4) X(3, 0, 8) X(3, 1, 4) X(3, 1, 8)
+inline bool vjp_ok(int n_lo, int n_up, int H, int K) {
+    if (n_lo < 1 || n_lo > 32 || n_up < 1 || n_lo + n_up > 128 || (n_lo + n_up) % 4 != 0) return false;
+    const Layout L = make_layout(n_lo, n_up, H, K, 1);
+    bool inst = false;
+#define NFK_VJP_CHK(h, t, k) inst |= (L.KBH == h && L.T1 == t && K == k);
+    NFK_VJP_SHAPES(NFK_VJP_CHK)
+#undef NFK_VJP_CHK
+    // two workgroups per CU at least (LDS counted in the allocation granule)
+    return inst && 2 * lds_alloc(vjp_lds_bytes(vjp_dims(L.KBH, L.T1, K), n_lo + n_up)) <= (size_t)kLdsBytes;
+}
 
 // hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f16 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132

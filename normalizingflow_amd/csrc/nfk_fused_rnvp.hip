@@ -112,29 +112,6 @@ __device__ __forceinline__ void rblock_end(int b, const RArgs& a, bool inv, floa
     if (b + 2 < 8) stage_rphase(a, b + 2, inv, slot0, slot1, wid, lane);
 }
 
-// layer 1 of one net: acc = b 2^(s1+sx) + 2^s1 W1 . (2^sx in)^T (fp16 split)
-template <int KBI, int HT>
-__device__ __forceinline__ void input_gemm(const h8 (&xh)[KBI], const h8 (&xl)[KBI], const float4* rec,
-                                           float bsc, int lane, f32x4 (&acc)[HT]) {
-    const int q = lane >> 4;
-    const float4* bias = rec + KBI * HT * 2 * 64;
-#pragma unroll
-    for (int t = 0; t < HT; ++t) {
-        const float4 bv = bias[t * 4 + q];
-        acc[t] = f32x4{bv.x * bsc, bv.y * bsc, bv.z * bsc, bv.w * bsc};
-    }
-#pragma unroll
-    for (int kb = 0; kb < KBI; ++kb)
-#pragma unroll
-        for (int t = 0; t < HT; ++t) {
-            const h8 ahi = __builtin_bit_cast(h8, rec[((kb * HT + t) * 2) * 64 + lane]);
-            const h8 alo = __builtin_bit_cast(h8, rec[((kb * HT + t) * 2 + 1) * 64 + lane]);
-            acc[t] = mfma16(alo, xh[kb], acc[t]);
-            acc[t] = mfma16(ahi, xl[kb], acc[t]);
-            acc[t] = mfma16(ahi, xh[kb], acc[t]);
-        }
-}
-
 template <int KBH, bool T1, int NO, bool INV>
 __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_rnvp(RArgs a) {
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0);
@@ -486,21 +463,6 @@ inline bool rchain_ok(const RLayout& L) {
     return 3 * lds_alloc(d.lds) <= (size_t)kLdsBytes;
 }
 
-// Block b of a kRNS-tile sub-record (tiles [t0, t0 + kRNS) of a record with
-// nt tiles) -> block of the record, -1 for none (stage_tiles' layout).
-__device__ inline int rchain_tile_src(int b, int kbh, int t1, int nt, int t0) {
-    const int nf = kbh * kRNS * 2, ntb = t1 ? (kRNS + 1) / 2 : 0;
-    const int nts = (nt - t0) < kRNS ? (nt - t0) : kRNS;
-    if (b < nf) {
-        const int kb = b / (2 * kRNS), r = b - kb * 2 * kRNS;
-        if ((r >> 1) >= nts) return -1;
-        return (kb * nt + t0 + (r >> 1)) * 2 + (r & 1);
-    }
-    if (b < nf + ntb) return kbh * nt * 2 + (t0 >> 1) + (b - nf);
-    if (b == nf + ntb) return kbh * nt * 2 + (t1 ? (nt + 1) / 2 : 0);
-    return -1;
-}
-
 // The chain stream of a pack (after k_rnvp_pack wrote its records): sub-record
 // u = (2 pr + net) NSUB + j, j = 0: the net's layer-1 record; 1..NP2: its
 // layer-2 tiles [(j-1) kRNS, ..); then its layer-3 tiles; zero padding to SB.
@@ -521,10 +483,10 @@ __global__ __launch_bounds__(256) void k_rnvp_stream(float* pack, RLayout L, int
         if (j == 0) {
             if (b < d.B1) src = base + off[0] + net * L.blk_l1 + b;
         } else if (j <= d.NP2) {
-            const int r = rchain_tile_src(b, L.KBH, L.T1, d.HT, (j - 1) * kRNS);
+            const int r = subrec_tile_src(b, L.KBH, L.T1, kRNS, d.HT, (j - 1) * kRNS);
             if (r >= 0) src = base + off[1 + net] + r;
         } else {
-            const int r = rchain_tile_src(b, L.KBH, L.T1, L.NO, (j - 1 - d.NP2) * kRNS);
+            const int r = subrec_tile_src(b, L.KBH, L.T1, kRNS, L.NO, (j - 1 - d.NP2) * kRNS);
             if (r >= 0) src = base + off[3] + net * L.blk_l3 + r;
         }
         pack[o_stream + g] = src >= 0 ? pack[256 + (int64_t)src * 256 + wl] : 0.0f;

@@ -230,7 +230,7 @@ class _HipFlow(nn.Module):
         (optimizer steps, ``with torch.no_grad(): p.add_(...)``,
         ``load_state_dict``) bumps.  Writes through ``p.data`` do not bump it:
         call this (or NormalizingFlowModel.invalidate_caches) after them."""
-        for name in ("_pack_cache", "_winv_key"):
+        for name in ("_pack_cache", "_winv_key", "_vjp_cache"):
             if name in self.__dict__:
                 self.__dict__[name] = None
 
@@ -496,6 +496,27 @@ class NSF_CL(_HipFlow):
         self._pack_cache = (key, pack, hidden)
         return pack
 
+    def _vjp_pack(self, device):
+        """The fused backward's pack (nfk_fused_nsf_vjp_pack), rebuilt when any
+        weight changes; None when that kernel does not apply."""
+        if not (config.USE_FUSED and config.USE_FUSED_VJP) or not _is_stock_fcnn(self.psi):
+            return None
+        lins = [self.psi.network[i] for i in (0, 2, 4)]
+        n_lo, n_up = len(self.mask) * self.size, len(self.unmasked) * self.size
+        hidden = lins[0].out_features
+        if not K_.fused_nsf_vjp_supported(n_lo, n_up, hidden, self.K):
+            return None
+        params = [t for l in lins for t in (l.weight, l.bias)]
+        if any(p.device != device or p.dtype != torch.float32 for p in params):
+            return None
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        cache = self.__dict__.get("_vjp_cache")
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        pack = K_.fused_nsf_vjp_pack(*params, n_lo, n_up, hidden, self.K)
+        self.__dict__["_vjp_cache"] = (key, pack, hidden)
+        return pack
+
     def _chain_shape(self, device):
         """(n_lo, n_up, hidden, K, B) when this layer runs as the fused kernel
         (so it may join an nfk_fused_nsf_chain launch with layers of the same
@@ -536,6 +557,28 @@ class NSF_CL(_HipFlow):
         # weight gradients); any other conditioner through autograd
         manual = _is_stock_fcnn(self.psi) and not config.SPLIT_GEMM and set(names) == set(
             "psi.network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias"))
+        vpack = self._vjp_pack(x.device) if manual else None
+        if vpack is not None:
+            # fused: the conditioner recomputed on the matrix cores and the
+            # spline VJP in one kernel (nfk_fused_nsf_vjp); it hands over
+            # dL/dparams and the activations [h | 1] for the GEMMs below
+            x = x.detach().contiguous()
+            B, H = x.shape[0], self.__dict__["_vjp_cache"][2]
+            ldh = (H + 4) // 4 * 4
+            hbuf = torch.empty(2, B, ldh, dtype=x.dtype, device=x.device)
+            gp = torch.empty(B, len(maps.lists[2]) * (3 * self.K - 1), dtype=x.dtype, device=x.device)
+            gx = torch.empty_like(x)
+            K_.fused_nsf_vjp(x, vpack, maps.up_in, maps.up_out, maps.lo_in, maps.lo_out, H,
+                             None if gz is None else gz.contiguous(), None if gld is None else gld.contiguous(),
+                             gp, gx, hbuf[0], hbuf[1], K=self.K, tail_bound=float(self.B), inverse=inverse)
+            pmap = {n: t.detach() for n, t in zip(names, params)}
+            lower = x.index_select(1, maps.lo_in_long)
+            want = {n for n, r in zip(names, need[1:]) if r}
+            g_lower, grads = fcnn_grad.vjp(pmap, "psi.", (lower, hbuf[0][:, :H + 1], hbuf[1][:, :H + 1]),
+                                           gp, need[0], want)
+            if g_lower is not None:
+                gx.index_add_(1, maps.lo_in_long, g_lower)
+            return [gx if need[0] else None] + [grads.get(n) for n in names]
         if manual:
             lower = x.detach().index_select(1, maps.lo_in_long)
             pmap = {n: t.detach() for n, t in zip(names, params)}

@@ -353,6 +353,51 @@ def fused_nsf(x, wpack, up_in, up_out, lo_in, lo_out, hidden, z, *, logdet, logd
               1 if inverse else 0, _vec(status, 1, "status", torch.int32), _stream(dev))
 
 
+_VJP_ELEMS = {}
+
+
+def fused_nsf_vjp_supported(n_lo, n_up, hidden, K):
+    key = (n_lo, n_up, hidden, K)
+    n = _VJP_ELEMS.get(key)
+    if n is None:
+        n = _VJP_ELEMS[key] = int(_lib.load().nfk_fused_nsf_vjp_pack_elems(n_lo, n_up, hidden, K))
+    return n > 0
+
+
+def fused_nsf_vjp_pack(w0, b0, w2, b2, w4, b4, n_lo, n_up, hidden, K):
+    dev = _require_hip(w0, b0, w2, b2, w4, b4)
+    n = int(_lib.load().nfk_fused_nsf_vjp_pack_elems(n_lo, n_up, hidden, K))
+    if n <= 0:
+        raise ValueError("nfk_fused_nsf_vjp: shape not supported")
+    ws = [t.detach().contiguous() for t in (w0, b0, w2, b2, w4, b4)]
+    pack = torch.empty(n, dtype=F32, device=dev)
+    _lib.call("nfk_fused_nsf_vjp_pack", *[t.data_ptr() for t in ws], n_lo, n_up, hidden, K, pack.data_ptr(),
+              _stream(dev))
+    return pack
+
+
+def fused_nsf_vjp(x, vpack, up_in, up_out, lo_in, lo_out, hidden, gz, gld, gparams, gx, h1, h2, *, K,
+                  tail_bound, inverse=False):
+    """Recompute + spline VJP of one fused NSF_CL layer (include/nfk.h nfk_fused_nsf_vjp).
+    h1, h2: [B, ldh] with ldh >= hidden + 1 (a multiple of 4); gparams [B, n_up*(3K-1)]."""
+    dev = _require_hip(x, vpack, up_in, gz, gld, gparams, gx, h1, h2)
+    B = x.shape[0]
+    n_up, n_lo = up_in.numel(), lo_in.numel()
+    xp, ldx = _mat(x, "x")
+    gzp, ldgz = _mat(gz, "gz") if gz is not None else (None, 0)
+    gxp, ldgx = _mat(gx, "gx")
+    if gparams.shape != (B, n_up * (3 * K - 1)) or not gparams.is_contiguous():
+        raise ValueError("gparams must be a contiguous [%d, %d] tensor" % (B, n_up * (3 * K - 1)))
+    h1p, ldh = _mat(h1, "h1")
+    h2p, ldh2 = _mat(h2, "h2")
+    if ldh2 != ldh or h1.shape[1] < hidden + 1:
+        raise ValueError("h1 and h2 need one row stride and hidden + 1 columns")
+    _timed("nfk_fused_nsf_vjp", dev, "nfk_fused_nsf_vjp", xp, ldx, vpack.data_ptr(), up_in.data_ptr(),
+           up_out.data_ptr(), n_up, lo_in.data_ptr(), lo_out.data_ptr(), n_lo, hidden, gzp, ldgz,
+           _vec(gld, B, "gld"), gparams.data_ptr(), gxp, ldgx, h1p, h2p, ldh, B, K, float(tail_bound),
+           1 if inverse else 0, _stream(dev))
+
+
 _CHAIN_MAX = {}
 
 
