@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) void k_pack_frames(PackArgs a, int s1, int ns,
         }
         const int kb0 = gg * j, nk = (nkb - kb0) < gg ? (nkb - kb0) : gg;
         uint32_t v = 0;
-        if (blk == 64)
+        if (blk == kWideFB)
             v = pack_word(a, rec + (int64_t)nkb * nt * 2 * 256 + wl, ps);
         else if (blk < nk * nt * 2)
             v = pack_word(a, rec + ((int64_t)kb0 * nt * 2 + blk) * 256 + wl, ps);
@@ -290,7 +290,7 @@ bool wide_ok(int n_lo, int n_up, int H, int K) {
     if (n_lo < 1 || n_up < 1 || H < 1 || K < 2 || (K & 1)) return false;
     const Layout L = make_layout(n_lo, n_up, H, K, 1);
     if (L.T1 != 0 || L.KB1 > L.KBH || n_lo > 16 * ((L.NCH + 1) / 2)) return false;
-    if (wide_lds_bytes(n_lo, n_up) > (size_t)kLdsBytes) return false;
+    if (kWideWGs * lds_alloc(wide_lds_bytes(n_lo, n_up)) > (size_t)kLdsBytes) return false;
     bool kb = false, kk = false;
 #define CHK_KB(h) kb |= (L.KBH == h);
     NFK_WIDE_KB(CHK_KB)

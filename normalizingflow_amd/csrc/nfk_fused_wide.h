@@ -39,11 +39,34 @@
 
 namespace nfk_fused {
 
-constexpr int kWideSlotBlocks = 65;  // 64 f16 blocks + the record's bias block
-constexpr int kWideTile = 16 * 32;   // floats of a wave's chunk-pair tile
+// Frame size and workgroup shape.  Default: one 8-wave workgroup per CU,
+// 65-block frames.  NFK_WIDE_FB=32 NFK_WIDE_NW=4 builds two 4-wave workgroups
+// per CU with 33-block frames (measured 4-5 % slower at c5: twice the
+// sub-steps, and the two workgroups do not desynchronise usefully).
+#ifndef NFK_WIDE_FB
+#define NFK_WIDE_FB 64
+#endif
+#ifndef NFK_WIDE_NW
+#define NFK_WIDE_NW 8
+#endif
+#ifndef NFK_WIDE_PK
+#define NFK_WIDE_PK 1
+#endif
+#ifndef NFK_WIDE_PIN
+#define NFK_WIDE_PIN 1
+#endif
+constexpr int kWideFB = NFK_WIDE_FB;             // f16 blocks of a frame
+constexpr int kWideSlotBlocks = kWideFB + 1;     // + the record's bias block
+constexpr int kWideWaves = NFK_WIDE_NW;          // waves per workgroup
+constexpr int kWideWGs = 8 / kWideWaves;         // workgroups per CU
+constexpr int kWideTile = 16 * 32;               // floats of a wave's chunk-pair tile
+static_assert(kWideFB == 32 || kWideFB == 64, "frame of 32 or 64 blocks");
+static_assert(kWideWaves == 4 || kWideWaves == 8, "4- or 8-wave workgroups");
 
 // k-blocks per sub-record of a record with nt tiles
-__host__ __device__ constexpr int wide_g(int nt, int kbh) { return (32 / nt) < kbh ? (32 / nt) : kbh; }
+__host__ __device__ constexpr int wide_g(int nt, int kbh) {
+    return (kWideFB / 2 / nt) < kbh ? (kWideFB / 2 / nt) : kbh;
+}
 
 struct WideArgs {
     const float* x;
@@ -61,7 +84,7 @@ struct WideArgs {
 
 inline size_t wide_lds_bytes(int n_lo, int n_up) {
     return 2 * (size_t)kWideSlotBlocks * 1024 + (size_t)((2 * (n_lo + n_up) + 3) / 4) * 16 +
-           (size_t)kWaves * kWideTile * sizeof(float);
+           (size_t)kWideWaves * kWideTile * sizeof(float);
 }
 
 // sub-steps of one layer: layer 1, layer 2, then per 8-coordinate chunk the
@@ -73,8 +96,8 @@ inline int wide_substeps(int kb1, int kbh, int K, int nch, int* s1) {
 }
 
 // Copy the frame of sub-step s (if any) into slot s & 1.  The pack holds one
-// 65-block frame per sub-step in forward order (W, H, D records per chunk);
-// the inverse searches the heights, so it takes each chunk's H frames first.
+// frame per sub-step in forward order (W, H, D records per chunk); the
+// inverse searches the heights, so it takes each chunk's H frames first.
 template <int KBH, int K, bool INV>
 __device__ __forceinline__ void wide_stage(const WideArgs& a, int s, float4* slot0, float4* slot1, int wid,
                                            int lane) {
@@ -92,7 +115,8 @@ __device__ __forceinline__ void wide_stage(const WideArgs& a, int s, float4* slo
     if (s >= 2) return;  // diagnostic: no copies after the prologue
 #endif
     float4* slot = (s & 1) ? slot1 : slot0;
-    stage_record(a.pack + 256 + (int64_t)f * (kWideSlotBlocks * 256), kWideSlotBlocks, slot, wid, lane);
+    stage_record<kWideWaves>(a.pack + 256 + (int64_t)f * (kWideSlotBlocks * 256), kWideSlotBlocks, slot, wid,
+                             lane);
 }
 
 // GEMM over sub-record J (k-blocks G J .. G J + G - 1, those below nkb) of a
@@ -106,7 +130,7 @@ __device__ __forceinline__ void gemm_sub(const h8 (&bh)[KBH], const h8 (&bl)[KBH
     static_assert(G * (J + 1) <= KBH, "sub-record beyond the k-blocks");
     const int q = lane >> 4;
     if constexpr (J == 0) {
-        const float4* bias = slot + 64 * 64;
+        const float4* bias = slot + kWideFB * 64;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const float4 b = bias[t * 4 + q];
@@ -160,7 +184,7 @@ __device__ __forceinline__ void wide_phase(const WideArgs& a, int& s, int nsub, 
                                            const h8 (&bl)[KBH], f32x4 (&acc)[NT], float bscale, float4* slot0,
                                            float4* slot1, int wid, int lane, NfkTrace& tr) {
     constexpr int NS = KBH / wide_g(NT, KBH);
-    static_assert(NS <= 4, "at most 4 sub-records per phase");
+    static_assert(NS <= 8, "at most 8 sub-records per phase");
     auto one = [&](auto Jc) {
         constexpr int J = decltype(Jc)::value;
         if (J < nsub) {
@@ -178,6 +202,10 @@ __device__ __forceinline__ void wide_phase(const WideArgs& a, int& s, int nsub, 
     if constexpr (NS > 1) one(std::integral_constant<int, 1>{});
     if constexpr (NS > 2) one(std::integral_constant<int, 2>{});
     if constexpr (NS > 3) one(std::integral_constant<int, 3>{});
+    if constexpr (NS > 4) one(std::integral_constant<int, 4>{});
+    if constexpr (NS > 5) one(std::integral_constant<int, 5>{});
+    if constexpr (NS > 6) one(std::integral_constant<int, 6>{});
+    if constexpr (NS > 7) one(std::integral_constant<int, 7>{});
 }
 
 // Knot epilogue of the wide form: coordinate h (0, 1) of this lane group has
@@ -197,13 +225,33 @@ __device__ __forceinline__ void knot_phase_w(const f32x4 (&acc)[K / 2], const fl
     }
     return;
 #endif
+#if NFK_WIDE_PK
+    // both coordinates' prefixes as packed pairs (bitwise those of the scalar
+    // form, nfk_spline.h), then the selects one coordinate at a time
+    int pre2[2][K];
+    nfk_f2 s22;
+    {
+        float u0[K], u1[K];
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            u0[p] = acc[p >> 1][p & 1];
+            u1[p] = acc[p >> 1][2 + (p & 1)];
+        }
+        s22 = nfk_prefix_nsf_lean2<K>(u0, u1, l2e, c.m2b, c.fb30, c.mb30, pre2[0], pre2[1]);
+    }
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+#if NFK_WIDE_PK
+        const int(&pre)[K] = pre2[h];
+        const float s2 = h ? s22.y : s22.x;
+#else
         float u[K];
         int pre[K];
 #pragma unroll
         for (int p = 0; p < K; ++p) u[p] = acc[p >> 1][2 * h + (p & 1)];
         const float s2 = nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
+#endif
         const float lo = __builtin_fmaf(s2, 0.0f, c.lo);  // NaN iff the logits were (knot_phase)
         int p0 = 0, p1 = pre[1 < K ? 1 : 0], k = 0;
         const int xi = __float2int_rd(__builtin_fmaf(xv[h], c.inv30, -c.lo * c.inv30));
@@ -220,8 +268,21 @@ __device__ __forceinline__ void knot_phase_w(const f32x4 (&acc)[K / 2], const fl
         const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, lo);
         ek[h] = e;
         sk[h] = e1 - e;
-        if constexpr (K > 8) __builtin_amdgcn_sched_barrier(0);  // one coordinate's temporaries at a time
+        if constexpr (K > 8 && !NFK_WIDE_PK) __builtin_amdgcn_sched_barrier(0);  // one coordinate at a time
     }
+}
+
+// Pin a knot epilogue's results at its place in the schedule: without it
+// the compiler sinks the searched-knot and other-knot epilogues below the
+// derivative record's GEMMs (only register dependences order them), so the
+// logits of three records stay live at once (256 VGPRs and scratch spills
+// whose reloads wait on the frame copies in flight) and every epilogue of a
+// chunk runs back to back.
+__device__ __forceinline__ void wide_pin(int (&kb)[2], float (&e)[2], float (&s)[2]) {
+#if NFK_WIDE_PIN
+#pragma unroll
+    for (int h = 0; h < 2; ++h) asm volatile("" : "+v"(kb[h]), "+v"(e[h]), "+v"(s[h]));
+#endif
 }
 
 // Column of a chunk-pair tile: even t = lower coordinate 16 g + t/2, odd t = upper.
@@ -267,7 +328,7 @@ __device__ __forceinline__ void wide_store(const WideArgs& a, const int32_t* m_l
 }
 
 template <int KBH, int K, bool INV>
-__global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
+__global__ __launch_bounds__(64 * kWideWaves, kWideWGs) void k_fused_nsf_wide(WideArgs a) {
     constexpr int HT = 2 * KBH;
     constexpr int NTC = K / 2;  // tiles of a chunk's W, H or D record
     constexpr int S2 = KBH / wide_g(HT, KBH);
@@ -285,7 +346,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
     int32_t* m_lo_out = m_lo_in + a.n_lo;
     float* tile = reinterpret_cast<float*>(lds4 + 2 * kWideSlotBlocks * 64 + (2 * (a.n_lo + a.n_up) + 3) / 4) +
                   wid * kWideTile;
-    const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wid) * 16;
+    const int64_t b0 = ((int64_t)blockIdx.x * kWideWaves + wid) * 16;
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const bool row_ok = sl < nrows;
@@ -295,11 +356,11 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
     NFK_MARK(tr);  // start
 
     // ---- prologue: index maps (plain loads, no copy in flight yet)
-    for (int i = threadIdx.x; i < a.n_up; i += 64 * kWaves) {
+    for (int i = threadIdx.x; i < a.n_up; i += 64 * kWideWaves) {
         m_up_in[i] = a.up_in[i];
         m_up_out[i] = a.up_out[i];
     }
-    for (int i = threadIdx.x; i < a.n_lo; i += 64 * kWaves) {
+    for (int i = threadIdx.x; i < a.n_lo; i += 64 * kWideWaves) {
         m_lo_in[i] = a.lo_in[i];
         m_lo_out[i] = a.lo_out[i];
     }
@@ -382,6 +443,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
                 if (jj[h] >= a.n_up) xv[h] = 0.0f;
             }
             knot_phase_w<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k);
+            wide_pin(kb, INV ? ch_k : cw_k, INV ? h_k : w_k);
             NFK_MARK(tr);  // epilogue A
         }
         // ---- the other knots, selected at the bin
@@ -389,6 +451,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
             f32x4 acc[NTC];
             wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, acc, 1.0f, slot0, slot1, wid, lane, tr);
             knot_phase_w<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k);
+            wide_pin(kb, INV ? cw_k : ch_k, INV ? w_k : h_k);
             NFK_MARK(tr);  // epilogue B
         }
         // ---- derivatives of the bin, evaluate, log|det|
@@ -500,13 +563,13 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_nsf_wide(WideArgs a) {
 
 template <int KBH, int K>
 int launch_fused_wide(const WideArgs& a, size_t lds, bool inv, hipStream_t st) {
-    const int64_t per_block = (int64_t)kWaves * 16;
+    const int64_t per_block = (int64_t)kWideWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
     if (inv)
-        hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, true>), dim3((unsigned)blocks), dim3(64 * kWaves), lds, st, a);
+        hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, true>), dim3((unsigned)blocks), dim3(64 * kWideWaves), lds, st, a);
     else
-        hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, false>), dim3((unsigned)blocks), dim3(64 * kWaves), lds, st, a);
+        hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, false>), dim3((unsigned)blocks), dim3(64 * kWideWaves), lds, st, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
