@@ -329,6 +329,54 @@ int nfk_fused_realnvp_chain(const float* x, int64_t ldx, const float* const* wpa
                             float* log_prob, float prior_scale, float prior_half_log_det,
                             nfk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Training backward of the remaining flow classes (nfk_flows_bwd.hip): the
+ * vector-Jacobian products autograd takes through flows_1.py's Planar
+ * (:42-60), Radial (:85-97), ActNorm (:207-215), MAF (:171-195) and NSF_AR's
+ * trig features (flows.py:172-173).  Batch sums (parameter gradients) are
+ * deterministic (fixed-order fp64 column reductions, no atomics).
+ *   workspace: device scratch of nfk_flows_bwd_workspace_bytes(batch, dim)
+ *              bytes, 256-byte aligned (MAF: dim = 2).
+ * Upstream gradients gz (dL/dz) and glogdet (dL/dlog|det|: [batch] per
+ * sample, or a [1] scalar where the layer's log|det| is a scalar) are nullable.
+ *
+ * nfk_planar_bwd: gx [batch, dim]; gw, gu [dim], gb [1] (through the tanh
+ *   re-parameterisation of u, flows_1.py:48-53).
+ * nfk_actnorm_bwd: gx, gmu, gls (log|det| = +-sum(log_sigma): gld_scalar).
+ * nfk_radial_bwd_scalars / _apply: two calls like the forward, because
+ *   r = ||x - x0||_F is batch-global: scal[4] = [dL/dsumsq, dL/dlog_alpha,
+ *   dL/dbeta, beta_hat h]; a sharded batch all-reduces (sums) scal[0] between
+ *   the calls (the backward of the forward's all-reduce of sumsq); _apply
+ *   writes gx and g_x0 [dim] (same workspace).
+ * nfk_maf_bwd: columns [c0, c1) of nfk_maf with gout = dL/dout: gx at each
+ *   column's input position (written), gparams (dL/d conditioner output, the
+ *   layout of params), ginit [2] (= the batch sum, written when c0 == 0).
+ *   The conditioners' own backward is the caller's (it adds into gx / gout).
+ * nfk_trig_features_bwd: gx[:, :n] += dL/dx through nfk_trig_features.
+ * ------------------------------------------------------------------------- */
+int64_t nfk_flows_bwd_workspace_bytes(int64_t batch, int32_t dim);
+int nfk_planar_bwd(const float* x, int64_t ldx, const float* w, const float* u, const float* b,
+                   const float* gz, int64_t ldgz, const float* glogdet, float* gx, int64_t ldgx,
+                   float* gw, float* gu, float* gb, void* workspace, int64_t batch, int32_t dim,
+                   int32_t nonlinearity, nfk_stream_t stream);
+int nfk_actnorm_bwd(const float* x, int64_t ldx, const float* mu, const float* log_sigma, int32_t dim,
+                    const float* gz, int64_t ldgz, const float* gld_scalar, float* gx, int64_t ldgx,
+                    float* gmu, float* gls, void* workspace, int64_t batch, int32_t inverse,
+                    nfk_stream_t stream);
+int nfk_radial_bwd_scalars(const float* x, int64_t ldx, const float* x0, const float* log_alpha,
+                           const float* beta, const double* sumsq, const float* gz, int64_t ldgz,
+                           const float* gld_scalar, float* scal, void* workspace, int64_t batch,
+                           int32_t dim, nfk_stream_t stream);
+int nfk_radial_bwd_apply(const float* x, int64_t ldx, const float* x0, const float* gz, int64_t ldgz,
+                         const float* scal, float* gx, int64_t ldgx, float* gx0, void* workspace,
+                         int64_t batch, int32_t dim, nfk_stream_t stream);
+int nfk_maf_bwd(const float* x, int64_t ldx, const float* init_param, const float* params, int64_t ldp,
+                const float* gout, int64_t ldgo, const float* glogdet, int32_t c0, int32_t c1,
+                int32_t dim, float* gx, int64_t ldgx, float* gparams, int64_t ldgp, float* ginit,
+                void* workspace, int64_t batch, int32_t inverse, nfk_stream_t stream);
+int nfk_trig_features_bwd(const float* x, int64_t ldx, const float* gfeat, int64_t ldgf, float* gx,
+                          int64_t ldgx, int64_t batch, int32_t n, double B, nfk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -93,6 +93,27 @@ SIGNATURES = {
         P, I64, P, I32, I32,            # x, ldx, wpack, half_dim, hidden
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
         I64, I32, P]),                  # batch, inverse, stream
+    "nfk_flows_bwd_workspace_bytes": (ctypes.c_int64, [I64, I32]),
+    "nfk_planar_bwd": (ctypes.c_int, [
+        P, I64, P, P, P,                # x, ldx, w, u, b
+        P, I64, P, P, I64,              # gz, ldgz, glogdet, gx, ldgx
+        P, P, P, P, I64, I32, I32, P]),  # gw, gu, gb, workspace, batch, dim, nonlinearity, stream
+    "nfk_actnorm_bwd": (ctypes.c_int, [
+        P, I64, P, P, I32,              # x, ldx, mu, log_sigma, dim
+        P, I64, P, P, I64,              # gz, ldgz, gld_scalar, gx, ldgx
+        P, P, P, I64, I32, P]),         # gmu, gls, workspace, batch, inverse, stream
+    "nfk_radial_bwd_scalars": (ctypes.c_int, [
+        P, I64, P, P, P, P,             # x, ldx, x0, log_alpha, beta, sumsq
+        P, I64, P, P, P, I64, I32, P]),  # gz, ldgz, gld_scalar, scal, workspace, batch, dim, stream
+    "nfk_radial_bwd_apply": (ctypes.c_int, [
+        P, I64, P, P, I64, P,           # x, ldx, x0, gz, ldgz, scal
+        P, I64, P, P, I64, I32, P]),    # gx, ldgx, gx0, workspace, batch, dim, stream
+    "nfk_maf_bwd": (ctypes.c_int, [
+        P, I64, P, P, I64,              # x, ldx, init_param, params, ldp
+        P, I64, P, I32, I32, I32,       # gout, ldgo, glogdet, c0, c1, dim
+        P, I64, P, I64, P, P,           # gx, ldgx, gparams, ldgp, ginit, workspace
+        I64, I32, P]),                  # batch, inverse, stream
+    "nfk_trig_features_bwd": (ctypes.c_int, [P, I64, P, I64, P, I64, I64, I32, F64, P]),
     "nfk_affine_coupling_bwd": (ctypes.c_int, [
         P, I64, P, P, I64,              # x_in, ld_in, s, t, ld_st
         P, I64, P,                      # g_out, ld_g, g_logdet

@@ -283,6 +283,15 @@ def _is_stock_fcnn(net):
             and all(isinstance(n[i], nn.Tanh) for i in (1, 3)))
 
 
+def _vjp_out(names, need, gx, grads):
+    """_LayerFn.backward's result list: dL/dx (if wanted), then per parameter."""
+    return [gx if need[0] else None] + [grads.get(n) if r else None for n, r in zip(names, need[1:])]
+
+
+def _dense(g, like):
+    return torch.zeros_like(like) if g is None else g.contiguous()
+
+
 class RealNVP(_HipFlow):
     """Affine coupling, two halves per layer (flows.py:38-76).
 
@@ -685,6 +694,43 @@ class NSF_AR(_HipFlow):
                             status=None if status is None else status[i:i + 1])
         return z
 
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward by hand for stock FCNN conditioners (else None: autograd
+        recompute).  Column i: the spline VJP (nfk_rqs_coupling_bwd), then the
+        conditioner's (fcnn_grad) and the trig features' (nfk_trig_features_bwd)
+        into the gradient of the coordinates it read -- x[:, :i] forward, the
+        output z[:, :i] inverse (flows.py:174-209), so the inverse runs the
+        columns last to first, each one's output gradient complete."""
+        if not all(_is_stock_fcnn(n) for n in self.layers) or x.shape[1] != self.dim:
+            return None
+        p = {n: t.detach() for n, t in zip(names, params)}
+        want = {n for n, r in zip(names, need[1:]) if r}
+        x = x.detach()
+        B, b = x.shape[0], float(self.B)
+        cond = self._eval(x, True, None)[0] if inverse else x
+        gout = _dense(gz, x).clone() if inverse else _dense(gz, x)
+        gldc = None if gld is None else gld.contiguous()
+        gx = torch.empty_like(x)
+        grads = {}
+        order = range(self.dim - 1, -1, -1) if inverse else range(self.dim)
+        for i in order:
+            if i == 0:
+                prm = p["init_param"].to(torch.float32).expand(B, -1).contiguous()
+            else:
+                prm, cache = fcnn_grad.forward_saved(p, "layers.%d." % (i - 1), self.trig_transform(cond[:, :i]))
+            gprm = torch.empty_like(prm)
+            col = self._col(i, x.device)
+            K_.rqs_coupling_bwd(x, prm, col, col, gout, gldc, gprm, gx, K=self.K, left=-b, right=b,
+                                bottom=-b, top=b, tails=True, param_mode=0, inverse=inverse)
+            if i == 0:
+                if "init_param" in want:
+                    grads["init_param"] = gprm.sum(0)
+                continue
+            gfeat, gr = fcnn_grad.vjp(p, "layers.%d." % (i - 1), cache, gprm, True, want)
+            grads.update(gr)
+            K_.trig_features_bwd(cond[:, :i], gfeat, gout if inverse else gx, b)
+        return _vjp_out(names, need, gx, grads)
+
     def forward(self, x):
         return self._call(x, False)
 
@@ -720,6 +766,19 @@ class Planar(_HipFlow):
         K_.planar(x, self.w.detach(), self.u.detach(), self.b.detach(), z, logdet=logdet,
                   logdet_mode=mode, nonlinearity=_NL_CODE[self.h])
         return z
+
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward (nfk_planar_bwd): gx and the w, u, b gradients in one call."""
+        if inverse or self.h not in _NL_CODE:
+            return None
+        p = {n: t.detach().contiguous() for n, t in zip(names, params)}
+        x = x.detach()
+        gx = torch.empty_like(x)
+        grads = {"w": torch.empty_like(p["w"]), "u": torch.empty_like(p["u"]), "b": torch.empty_like(p["b"])}
+        K_.planar_bwd(x, p["w"], p["u"], p["b"], None if gz is None else gz.contiguous(),
+                      None if gld is None else gld.contiguous(), gx, grads["w"], grads["u"], grads["b"],
+                      nonlinearity=_NL_CODE[self.h])
+        return _vjp_out(names, need, gx, grads)
 
     def forward(self, x):
         return self._call(x, False)
@@ -780,6 +839,33 @@ class Radial(_HipFlow):
             z = self._run(x, inverse, None, K_.MODE_NONE, None, ld_scalar=ld)
         return z, ld
 
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward (nfk_radial_bwd_scalars / _apply).  r is batch-global, so
+        with a process group the recomputed sumsq is all-reduced as in the
+        forward, and so is dL/dsumsq between the two calls (the backward of
+        that all-reduce): every shard then sees the gradient of the global r."""
+        if inverse:
+            return None
+        p = {n: t.detach().contiguous() for n, t in zip(names, params)}
+        x = x.detach()
+        B, D = x.shape
+        ws, sumsq = self._buffers_for(x.device)
+        K_.radial_sumsq(x, p["x0"], ws, sumsq)
+        if self.process_group is not None:
+            torch.distributed.all_reduce(sumsq, group=self.process_group)
+        wsb = K_.flows_bwd_workspace(B, D, x.device)
+        scal = torch.empty(4, dtype=torch.float32, device=x.device)
+        gzc = None if gz is None else gz.contiguous()
+        K_.radial_bwd_scalars(x, p["x0"], p["log_alpha"], p["beta"], sumsq, gzc,
+                              None if gld is None else gld.reshape(1).contiguous(), scal, wsb)
+        if self.process_group is not None:
+            torch.distributed.all_reduce(scal[0:1], group=self.process_group)
+        gx = torch.empty_like(x)
+        gx0 = torch.empty_like(p["x0"])
+        K_.radial_bwd_apply(x, p["x0"], gzc, scal, gx, gx0, wsb)
+        grads = {"x0": gx0, "log_alpha": scal[1:2].clone(), "beta": scal[2:3].clone()}
+        return _vjp_out(names, need, gx, grads)
+
     def forward(self, x):
         return self._call(x, False)
 
@@ -825,6 +911,47 @@ class MAF(_HipFlow):
             K_.maf(x, ip, prm, out, i, i + 1, logdet=logdet, logdet_mode=m2, inverse=True)
         return out
 
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward by hand for stock FCNN conditioners (else None: autograd
+        recompute): nfk_maf_bwd for the affine steps, fcnn_grad for the
+        conditioners, whose input gradient goes to x[:, :i] (forward) or to
+        the output columns they read (inverse, run last column first)."""
+        if not all(_is_stock_fcnn(n) for n in self.layers) or x.shape[1] != self.dim:
+            return None
+        p = {n: t.detach() for n, t in zip(names, params)}
+        want = {n for n, r in zip(names, need[1:]) if r}
+        x = x.detach()
+        ip = p["initial_param"].to(torch.float32).contiguous()
+        gldc = None if gld is None else gld.contiguous()
+        gx = torch.empty_like(x)
+        ginit = torch.empty(2, dtype=torch.float32, device=x.device)
+        grads = {}
+        cond = self._eval(x, True, None)[0] if inverse else x
+        saved = [fcnn_grad.forward_saved(p, "layers.%d." % (i - 1), cond[:, :i].contiguous())
+                 for i in range(1, self.dim)]
+        if not inverse:
+            prm = torch.cat([o for o, _ in saved], dim=1) if saved else None
+            gprm = None if prm is None else torch.empty_like(prm)
+            K_.maf_bwd(x, ip, prm, _dense(gz, x), gldc, 0, self.dim, gx, gprm, ginit)
+            for i in range(1, self.dim):
+                g_in, gr = fcnn_grad.vjp(p, "layers.%d." % (i - 1), saved[i - 1][1],
+                                         gprm[:, 2 * (i - 1):2 * i].contiguous(), True, want)
+                grads.update(gr)
+                gx[:, :i] += g_in
+        else:
+            gout = _dense(gz, x).clone()
+            for i in range(self.dim - 1, -1, -1):
+                prm = saved[i - 1][0].contiguous() if i > 0 else None
+                gprm = None if prm is None else torch.empty_like(prm)
+                K_.maf_bwd(x, ip, prm, gout, gldc, i, i + 1, gx, gprm, ginit if i == 0 else None,
+                           inverse=True)
+                if i > 0:
+                    g_in, gr = fcnn_grad.vjp(p, "layers.%d." % (i - 1), saved[i - 1][1], gprm, True, want)
+                    grads.update(gr)
+                    gout[:, :i] += g_in
+        grads["initial_param"] = ginit
+        return _vjp_out(names, need, gx, grads)
+
     def forward(self, x):
         return self._call(x, False)
 
@@ -858,6 +985,16 @@ class ActNorm(_HipFlow):
         with torch.no_grad():
             z = self._launch(x, inverse, None, K_.MODE_NONE, ld)
         return z, ld
+
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward (nfk_actnorm_bwd); log|det| is the scalar +-sum(log_sigma)."""
+        p = {n: t.detach().contiguous() for n, t in zip(names, params)}
+        x = x.detach()
+        gx = torch.empty_like(x)
+        grads = {"mu": torch.empty_like(p["mu"]), "log_sigma": torch.empty_like(p["log_sigma"])}
+        K_.actnorm_bwd(x, p["mu"], p["log_sigma"], _dense(gz, x), None if gld is None else gld.reshape(1).contiguous(),
+                       gx, grads["mu"], grads["log_sigma"], inverse=inverse)
+        return _vjp_out(names, need, gx, grads)
 
     def forward(self, x):
         return self._call(x, False)

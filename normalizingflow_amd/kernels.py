@@ -299,6 +299,90 @@ def radial_apply(x, x0, log_alpha, beta, sumsq, z, ld_scalar, *, logdet=None,
               _stream(dev))
 
 
+# ---- training backward of the remaining flow classes (nfk_flows_bwd.hip)
+def flows_bwd_workspace(batch, dim, device):
+    """Scratch of nfk_flows_bwd_workspace_bytes (uint8, 256-byte aligned by the allocator)."""
+    n = int(_lib.load().nfk_flows_bwd_workspace_bytes(int(batch), int(max(dim, 2))))
+    return torch.empty(n, dtype=torch.uint8, device=device)
+
+
+def planar_bwd(x, w, u, b, gz, glogdet, gx, gw, gu, gb, *, nonlinearity=0):
+    """VJP of planar (nfk_planar_bwd): gx [B, D] and the parameter gradients."""
+    dev = _require_hip(x, w, u, b, gz, glogdet, gx, gw, gu, gb)
+    B, D = x.shape
+    xp, ldx = _mat(x, "x")
+    gp, ldg = _mat(gz, "gz") if gz is not None else (None, 0)
+    gxp, ldgx = _mat(gx, "gx")
+    ws = flows_bwd_workspace(B, D, x.device)
+    _timed("nfk_planar_bwd", dev, "nfk_planar_bwd", xp, ldx, _vec(w, D, "w"), _vec(u, D, "u"), _vec(b, 1, "b"),
+           gp, ldg, _vec(glogdet, B, "glogdet"), gxp, ldgx, _vec(gw, D, "gw"), _vec(gu, D, "gu"),
+           _vec(gb, 1, "gb"), ws.data_ptr(), B, D, int(nonlinearity), _stream(dev))
+
+
+def actnorm_bwd(x, mu, log_sigma, gz, gld, gx, gmu, gls, *, inverse=False):
+    """VJP of actnorm (nfk_actnorm_bwd); gld: the scalar log|det|'s gradient ([1] or None)."""
+    dev = _require_hip(x, mu, log_sigma, gz, gld, gx, gmu, gls)
+    B, D = x.shape
+    xp, ldx = _mat(x, "x")
+    gp, ldg = _mat(gz, "gz")
+    gxp, ldgx = _mat(gx, "gx")
+    ws = flows_bwd_workspace(B, D, x.device)
+    _timed("nfk_actnorm_bwd", dev, "nfk_actnorm_bwd", xp, ldx, _vec(mu, D, "mu"), _vec(log_sigma, D, "log_sigma"),
+           D, gp, ldg, _vec(gld, 1, "gld"), gxp, ldgx, _vec(gmu, D, "gmu"), _vec(gls, D, "gls"), ws.data_ptr(),
+           B, 1 if inverse else 0, _stream(dev))
+
+
+def radial_bwd_scalars(x, x0, log_alpha, beta, sumsq, gz, gld, scal, workspace):
+    """First half of Radial's VJP (nfk_radial_bwd_scalars): scal = [dL/dsumsq,
+    dL/dlog_alpha, dL/dbeta, beta_hat h]; all-reduce scal[0] across shards
+    before radial_bwd_apply."""
+    dev = _require_hip(x, x0, log_alpha, beta, sumsq, gz, gld, scal, workspace)
+    B, D = x.shape
+    xp, ldx = _mat(x, "x")
+    gp, ldg = _mat(gz, "gz") if gz is not None else (None, 0)
+    _timed("nfk_radial_bwd_scalars", dev, "nfk_radial_bwd_scalars", xp, ldx, _vec(x0, D, "x0"),
+           _vec(log_alpha, 1, "log_alpha"), _vec(beta, 1, "beta"), _vec(sumsq, 1, "sumsq", torch.float64),
+           gp, ldg, _vec(gld, 1, "gld"), _vec(scal, 4, "scal"), workspace.data_ptr(), B, D, _stream(dev))
+
+
+def radial_bwd_apply(x, x0, gz, scal, gx, gx0, workspace):
+    dev = _require_hip(x, x0, gz, scal, gx, gx0, workspace)
+    B, D = x.shape
+    xp, ldx = _mat(x, "x")
+    gp, ldg = _mat(gz, "gz") if gz is not None else (None, 0)
+    gxp, ldgx = _mat(gx, "gx")
+    _timed("nfk_radial_bwd_apply", dev, "nfk_radial_bwd_apply", xp, ldx, _vec(x0, D, "x0"), gp, ldg,
+           _vec(scal, 4, "scal"), gxp, ldgx, _vec(gx0, D, "gx0"), workspace.data_ptr(), B, D, _stream(dev))
+
+
+def maf_bwd(x, init_param, params, gout, glogdet, c0, c1, gx, gparams, ginit, *, inverse=False):
+    """VJP of maf over columns [c0, c1) (nfk_maf_bwd)."""
+    dev = _require_hip(x, init_param, params, gout, glogdet, gx, gparams, ginit)
+    B, dim = x.shape
+    xp, ldx = _mat(x, "x")
+    pp, ldp = _mat(params, "params") if params is not None else (None, 0)
+    gpp, ldgp = _mat(gparams, "gparams") if gparams is not None else (None, 0)
+    gop, ldgo = _mat(gout, "gout") if gout is not None else (None, 0)
+    gxp, ldgx = _mat(gx, "gx")
+    ws = flows_bwd_workspace(B, 2, x.device)
+    _timed("nfk_maf_bwd", dev, "nfk_maf_bwd", xp, ldx, _vec(init_param, 2, "init_param"), pp, ldp, gop, ldgo,
+           _vec(glogdet, B, "glogdet"), int(c0), int(c1), dim, gxp, ldgx, gpp, ldgp, _vec(ginit, 2, "ginit"),
+           ws.data_ptr(), B, 1 if inverse else 0, _stream(dev))
+
+
+def trig_features_bwd(x, gfeat, gx, B):
+    """gx[:, :n] += dL/dx through trig_features (nfk_trig_features_bwd)."""
+    dev = _require_hip(x, gfeat, gx)
+    n_rows, n = x.shape
+    xp, ldx = _mat(x, "x")
+    fp, ldf = _mat(gfeat, "gfeat")
+    gp, ldg = _mat(gx, "gx")
+    if gfeat.shape != (n_rows, 2 * n) or gx.shape[0] != n_rows or gx.shape[1] < n:
+        raise ValueError("trig_features_bwd: gfeat must be [B, 2n] and gx [B, >=n]")
+    _timed("nfk_trig_features_bwd", dev, "nfk_trig_features_bwd", xp, ldx, fp, ldf, gp, ldg, n_rows, n, float(B),
+           _stream(dev))
+
+
 def iso_normal_consts(var, dim):
     """(scale, half_log_det) of MultivariateNormal(0, var*I) as torch evaluates
     them: scale = fp32 Cholesky diagonal, half_log_det = fp32 sum of its logs."""

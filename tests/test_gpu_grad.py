@@ -82,6 +82,7 @@ LAYERS = {
     "nsfar": (lambda: nff.NSF_AR(dim=4, K=5, B=3, hidden_dim=16), 4, True),
     "planar_tanh": (lambda: nff.Planar(6), 6, False),
     "planar_elu": (lambda: nff.Planar(6, nonlinearity=F.elu), 6, False),
+    "planar_leaky": (lambda: nff.Planar(6, nonlinearity=F.leaky_relu), 6, False),
     "radial": (lambda: _radial(6), 6, False),
     "maf": (lambda: nff.MAF(6, hidden_dim=8), 6, True),
     "actnorm": (lambda: _actnorm(6), 6, True),
@@ -129,6 +130,71 @@ def test_layer_grads_vs_oracle(name, inverse, hip_device):
             assert p.grad is None or not bool(p.grad.any()), k
         else:
             rel_close(p.grad, ref, what=k)
+
+
+# the hand-written backward of each layer class and the kernels it must launch
+NATIVE_BWD = {
+    "planar_tanh": {"nfk_planar_bwd"},
+    "planar_leaky": {"nfk_planar_bwd"},
+    "radial": {"nfk_radial_bwd_scalars", "nfk_radial_bwd_apply"},
+    "actnorm": {"nfk_actnorm_bwd"},
+    "maf": {"nfk_maf_bwd"},
+    "nsfar": {"nfk_rqs_coupling_bwd", "nfk_trig_features_bwd"},
+    "realnvp_unfused": {"nfk_affine_coupling_bwd"},
+    "nsfcl_fused": {"nfk_fused_nsf_vjp"},
+}
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("name", list(NATIVE_BWD))
+def test_backward_runs_native_kernels(name, inverse, hip_device):
+    """Each layer's backward is its hand-written VJP on the HIP kernels, not
+    the autograd recompute of torch_math (nothing of it may be called)."""
+    from normalizingflow_amd import kernels as K_, torch_math
+    layer, x, gz, gld = _layer_case(name, inverse)
+    layer = layer.to(hip_device)
+    xg = x.to(hip_device).requires_grad_(True)
+    z, ld = layer.inverse(xg) if inverse else layer(xg)
+    loss = (z * gz.to(hip_device)).sum() + (ld * gld.to(hip_device)).sum()
+    prev, prev_fwd = K_.TIMER, torch_math.layer_forward
+    K_.TIMER = K_.KernelTimer()
+
+    def _no_recompute(*a, **k):
+        raise AssertionError("autograd recompute used for %s" % name)
+    torch_math.layer_forward = _no_recompute
+    try:
+        loss.backward()
+        torch.cuda.synchronize()
+        launched = set(K_.TIMER.summary())
+    finally:
+        K_.TIMER, torch_math.layer_forward = prev, prev_fwd
+    assert NATIVE_BWD[name] <= launched, launched
+    assert xg.grad is not None and all(p.grad is not None for p in layer.parameters())
+
+
+@pytest.mark.parametrize("name", ["planar_tanh", "radial", "actnorm"])
+def test_backward_batch_reductions_large(name, hip_device):
+    """Parameter gradients are batch sums over many row chunks (70,000 rows:
+    the column reductions' chunk cap): oracle autograd in fp64 as reference."""
+    make, d, _ = LAYERS[name]
+    torch.manual_seed(5)
+    layer = make()
+    B = 70000
+    x = torch.randn(B, d, generator=torch.Generator().manual_seed(6))
+    g = torch.Generator().manual_seed(7)
+    gz = torch.randn(B, d, generator=g)
+    gld = torch.randn({"radial": (1,), "actnorm": ()}.get(name, (B,)), generator=g)
+    sd = {"l." + k: v.detach().double().clone().requires_grad_(True) for k, v in layer.named_parameters()}
+    xr = x.double().requires_grad_(True)
+    zr, ldr = orc.apply_layer(spec_of(layer, "l."), xr, sd, inverse=False)
+    ((zr * gz.double()).sum() + (ldr * gld.double()).sum()).backward()
+    layer = layer.to(hip_device)
+    xg = x.to(hip_device).requires_grad_(True)
+    z, ld = layer(xg)
+    ((z * gz.to(hip_device)).sum() + (ld * gld.to(hip_device)).sum()).backward()
+    rel_close(xg.grad, xr.grad, what="x.grad")
+    for k, p in layer.named_parameters():
+        rel_close(p.grad, sd["l." + k].grad, what=k)
 
 
 def _c3(n_layers, seed=1234, hidden=100):

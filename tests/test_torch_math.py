@@ -151,6 +151,8 @@ def test_layer_fn_plumbing_cpu():
     [1]-shaped Radial log|det|, parameters without grads) with a CPU stand-in
     for the kernel forward: the node must reproduce plain autograd."""
     class CpuRadial(nff.Radial):
+        _vjp = None  # the generic recompute-backward under test (Radial's own VJP is a HIP kernel)
+
         def _eval(self, x, inverse, status):
             with torch.no_grad():
                 return tm.radial(self, x, dict(self.named_parameters()), inverse)
