@@ -1065,6 +1065,30 @@ class OneByOneConv(_HipFlow):
         with torch.no_grad():
             return self._z(x, inverse).contiguous(), self._logdet_scalar(inverse)
 
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward: the batch products are library GEMMs like the forward
+        (dL/dx = gz W^T, dL/dW = x^T gz; W^-1 in the inverse), and only the
+        [dim, dim] factorisation W = P L (U + diag S) is differentiated by
+        autograd (parameter-sized, no batch dimension)."""
+        p = {n: t.detach().requires_grad_(r) for n, t, r in zip(names, params, need[1:])}
+        x = x.detach()
+        gzc = _dense(gz, x)
+        with torch.enable_grad():
+            eye = torch.diag(torch.ones(self.dim, dtype=x.dtype, device=x.device))
+            L = torch.tril(p["L"], diagonal=-1) + eye
+            US = torch.triu(p["U"], diagonal=1) + torch.diag(p["S"])
+            W = self.P.to(x.dtype) @ L @ US
+            M = torch.inverse(W) if inverse else W
+            gx = gzc @ M.t() if need[0] else None
+            outs, gouts = [M], [x.t() @ gzc]
+            if gld is not None:
+                ld = torch.sum(torch.log(torch.abs(p["S"])))
+                outs.append(-ld if inverse else ld)
+                gouts.append(gld.reshape(()))
+            wanted = [n for n in names if p[n].requires_grad]
+            got = torch.autograd.grad(outs, [p[n] for n in wanted], gouts, allow_unused=True) if wanted else []
+        return _vjp_out(names, need, gx, dict(zip(wanted, got)))
+
     def forward(self, x):
         return self._call(x, False)
 

@@ -21,8 +21,9 @@ import torch
 import torch.nn as nn
 import torch.nn.init as init
 
+from . import fcnn_grad
 from . import kernels as K_
-from .flows import FCNN, _HipFlow
+from .flows import FCNN, _HipFlow, _dense, _is_stock_fcnn, _vjp_out
 from .flows import MAF, ActNorm, NSF_CL, OneByOneConv, Planar, Radial, RealNVP  # noqa: F401
 from .flows import functional_derivatives  # noqa: F401
 
@@ -91,6 +92,40 @@ class NSF_AR(_HipFlow):
                             inverse=inverse,
                             status=None if status is None else status[i:i + 1])
         return z
+
+    def _vjp(self, x, names, params, gz, gld, inverse, need):
+        """Backward by hand for stock FCNN conditioners (else None: autograd
+        recompute).  Every net reads the layer's input, so the columns are
+        independent: per column the spline VJP (nfk_rqs_coupling_bwd), then the
+        net's (fcnn_grad) and, when periodic, the trig features'
+        (nfk_trig_features_bwd) into dL/dx[:, :i]; column 0's zero input
+        column takes no gradient."""
+        if not all(_is_stock_fcnn(n) for n in self.layers) or x.shape[1] != self.dim:
+            return None
+        p = {n: t.detach() for n, t in zip(names, params)}
+        want = {n for n, r in zip(names, need[1:]) if r}
+        x = x.detach()
+        B, b = x.shape[0], float(self.B)
+        gzc = _dense(gz, x)
+        gldc = None if gld is None else gld.contiguous()
+        gx = torch.empty_like(x)
+        grads = {}
+        for i in range(self.dim):
+            src = torch.zeros(B, 1, dtype=torch.float32, device=x.device) if i == 0 else x[:, :i]
+            feat = self.trig_transform(src) if self.periodic else src.contiguous()
+            prm, cache = fcnn_grad.forward_saved(p, "layers.%d." % i, feat)
+            gprm = torch.empty_like(prm)
+            col = self._col(i, x.device)
+            K_.rqs_coupling_bwd(x, prm, col, col, gzc, gldc, gprm, gx, K=self.K, left=-b, right=b,
+                                bottom=-b, top=b, tails=True, param_mode=0, inverse=inverse)
+            gfeat, gr = fcnn_grad.vjp(p, "layers.%d." % i, cache, gprm, i > 0, want)
+            grads.update(gr)
+            if i > 0:
+                if self.periodic:
+                    K_.trig_features_bwd(src, gfeat, gx, b)
+                else:
+                    gx[:, :i] += gfeat
+        return _vjp_out(names, need, gx, grads)
 
     def forward(self, x):
         return self._call(x, False)

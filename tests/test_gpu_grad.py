@@ -20,6 +20,7 @@ import torch.multiprocessing as mp
 import torch.nn.functional as F
 
 import nf.flows as nff
+import nf.flows_1 as nff1
 import nf.models as nfm
 from oracle import nf_oracle as orc
 
@@ -43,6 +44,9 @@ def spec_of(layer, prefix):
                     B=layer.B, mask=[int(m) for m in layer.mask])
     if isinstance(layer, nff.RealNVP):
         return dict(type="RealNVP", prefix=prefix, dim=layer.dim)
+    if isinstance(layer, nff1.NSF_AR):
+        return dict(type="NSF_AR_flows1", prefix=prefix, dim=layer.dim, K=layer.K, B=layer.B,
+                    periodic=layer.periodic)
     if isinstance(layer, nff.NSF_AR):
         return dict(type="NSF_AR", prefix=prefix, dim=layer.dim, K=layer.K, B=layer.B)
     if isinstance(layer, nff.Planar):
@@ -80,6 +84,8 @@ LAYERS = {
     "realnvp_fused": (lambda: nff.RealNVP(64, hidden_dim=100), 64, True),
     "realnvp_unfused": (lambda: nff.RealNVP(10, hidden_dim=20), 10, True),
     "nsfar": (lambda: nff.NSF_AR(dim=4, K=5, B=3, hidden_dim=16), 4, True),
+    "nsfar1": (lambda: nff1.NSF_AR(dim=4, K=5, B=3, hidden_dim=16), 4, True),
+    "nsfar1_plain": (lambda: nff1.NSF_AR(dim=3, K=4, B=3, hidden_dim=12, periodic=False), 3, True),
     "planar_tanh": (lambda: nff.Planar(6), 6, False),
     "planar_elu": (lambda: nff.Planar(6, nonlinearity=F.elu), 6, False),
     "planar_leaky": (lambda: nff.Planar(6, nonlinearity=F.leaky_relu), 6, False),
@@ -140,8 +146,11 @@ NATIVE_BWD = {
     "actnorm": {"nfk_actnorm_bwd"},
     "maf": {"nfk_maf_bwd"},
     "nsfar": {"nfk_rqs_coupling_bwd", "nfk_trig_features_bwd"},
+    "nsfar1": {"nfk_rqs_coupling_bwd", "nfk_trig_features_bwd"},
+    "nsfar1_plain": {"nfk_rqs_coupling_bwd"},
     "realnvp_unfused": {"nfk_affine_coupling_bwd"},
     "nsfcl_fused": {"nfk_fused_nsf_vjp"},
+    "onebyone": set(),  # library GEMMs (no kernel of ours), but not the recompute
 }
 
 
