@@ -18,6 +18,9 @@
 // backward.  The records are re-cut into kVNS-tile sub-records of SB blocks
 // (the pack's VJP stream) and double-buffered through two LDS slots with one
 // barrier per sub-record (the RealNVP chain's schedule, nfk_fused_rnvp.hip).
+#ifndef NFK_VJP_FAST
+#define NFK_VJP_FAST 1  // hardware exp / rcp and an fp32 knot cumsum in the element backward
+#endif
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
             }
             const float xv = tile[sl * XS + m_up_in[j]];
             const float go = (a.gz != nullptr) ? a.gz[b * a.ldgz + m_up_out[j]] : 0.0f;
-            const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false>(xv, wr, hr, dr, a.c, go, gl);
+            const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, wr, hr, dr, a.c, go, gl);
             if (row_ok) {
                 a.gx[b * a.ldgx + m_up_in[j]] = gxv;
                 float* g = a.gp + (b * n_up + j) * P;

@@ -9,10 +9,11 @@
 namespace nfk_bwd {
 
 // d softplus(v) / dv as torch's softplus_backward (beta 1, threshold 20)
+template <bool FAST = false>
 __device__ __forceinline__ float softplus_grad(float v) {
     if (v > 20.0f) return 1.0f;
-    const float e = expf(v);
-    return e / (e + 1.0f);
+    const float e = nfk_exp<FAST>(v);
+    return nfk_div<FAST>(e, e + 1.0f);
 }
 
 // softmax backward in place: g <- s * (g - sum(g * s))
@@ -26,15 +27,18 @@ __device__ __forceinline__ void softmax_bwd(const float (&s)[K], float (&g)[K]) 
 }
 
 // softmax forward, reference summation order (shared with the forward kernels)
-template <int K>
+template <int K, bool FAST = false>
 __device__ __forceinline__ void softmax_fwd(const float (&u)[K], float (&s)[K]) {
 #pragma unroll
     for (int i = 0; i < K; ++i) s[i] = u[i];
-    nfk_softmax<K>(s);
+    nfk_softmax<K, FAST>(s);
 }
 
 // One side (widths or heights): logits -> (s0 if PRE) -> s1 -> edges.
-template <int K, bool PRE>
+// FAST: hardware exp / reciprocal and an fp32 cumulative sum (the fused VJP
+// kernel, whose forward recompute is itself the lean arithmetic); otherwise
+// the reference's op order with the double-accumulated cumsum.
+template <int K, bool PRE, bool FAST = false>
 struct KnotSide {
     float s0[K];  // first softmax (PRE only)
     float s1[K];  // second softmax
@@ -43,20 +47,29 @@ struct KnotSide {
     __device__ __forceinline__ void build(const float (&u)[K], float scale2b, float lo, float hi,
                                           float span, float min_b, float fb) {
         if (PRE) {
-            softmax_fwd<K>(u, s0);
+            softmax_fwd<K, FAST>(u, s0);
 #pragma unroll
             for (int i = 0; i < K; ++i) s1[i] = scale2b * s0[i];
         } else {
 #pragma unroll
             for (int i = 0; i < K; ++i) s1[i] = u[i];
         }
-        nfk_softmax<K>(s1);
-        double acc = 0.0;
+        nfk_softmax<K, FAST>(s1);
         edge[0] = lo;
+        if constexpr (FAST) {
+            float acc = 0.0f;
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            acc += (double)(min_b + fb * s1[i]);
-            edge[i + 1] = span * (float)acc + lo;
+            for (int i = 0; i < K; ++i) {
+                acc += min_b + fb * s1[i];
+                edge[i + 1] = span * acc + lo;
+            }
+        } else {
+            double acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                acc += (double)(min_b + fb * s1[i]);
+                edge[i + 1] = span * (float)acc + lo;
+            }
         }
         edge[K] = hi;
     }
@@ -87,7 +100,8 @@ template <int K>
 __device__ __forceinline__ float sel(const float (&a)[K], int k) { return nfk_sel<K>(a, k); }
 
 // Backward of one spline element.  wr/hr/dr in: logits; out: their gradients.
-template <int K, bool INV, bool PRE, bool DFULL>
+// FAST: hardware exp / log / reciprocal throughout (see KnotSide).
+template <int K, bool INV, bool PRE, bool DFULL, bool FAST = false>
 __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float (&hr)[K],
                                                  float (&dr)[NfkDN<K, DFULL>::n],
                                                  const NfkSplineConst& c, float gout, float gl) {
@@ -100,7 +114,7 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
         for (int i = 0; i < DN; ++i) dr[i] = 0.0f;
         return gout;
     }
-    KnotSide<K, PRE> W, H;
+    KnotSide<K, PRE, FAST> W, H;
     W.build(wr, c.scale2b, c.lo, c.hi, c.span, c.min_w, c.fw);
     H.build(hr, c.scale2b, c.ylo, c.yhi, c.yspan, c.min_h, c.fh);
     const int k = nfk_bin<K>(INV ? H.edge : W.edge, x, c.knot_eps);
@@ -134,12 +148,12 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
             if (j == i0) r0 = dr[j];
             if (j == i1) r1 = dr[j];
         }
-        if (i0 >= 0) v0 = PRE ? nfk_softplus(r0) : r0;
-        if (i1 >= 0) v1 = PRE ? nfk_softplus(r1) : r1;
+        if (i0 >= 0) v0 = PRE ? nfk_splus<FAST>(r0) : r0;
+        if (i1 >= 0) v1 = PRE ? nfk_splus<FAST>(r1) : r1;
     }
-    const float d0 = c.min_d + nfk_softplus(v0);
-    const float d1 = c.min_d + nfk_softplus(v1);
-    const float delta = h_k / w_k;
+    const float d0 = c.min_d + nfk_splus<FAST>(v0);
+    const float d1 = c.min_d + nfk_splus<FAST>(v1);
+    const float delta = nfk_div<FAST>(h_k, w_k);
     const float gap = (d0 + d1) - 2.0f * delta;
 
     float th;
@@ -149,17 +163,17 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
         const float qb = h_k * d0 - y * gap;
         const float qc = (-delta) * y;
         const float disc = qb * qb - (4.0f * qa) * qc;
-        th = (2.0f * qc) / (-qb - sqrtf(fmaxf(disc, 0.0f)));
+        th = nfk_div<FAST>(2.0f * qc, -qb - sqrtf(fmaxf(disc, 0.0f)));
     } else {
-        th = (x - cw_k) / w_k;
+        th = nfk_div<FAST>(x - cw_k, w_k);
     }
     const float s = th * (1.0f - th);
     const float omt = 1.0f - th;
     const float Dn = delta + gap * s;
     const float N = h_k * (delta * th * th + d0 * s);
-    const float R = N / Dn;
+    const float R = nfk_div<FAST>(N, Dn);
     const float M = delta * delta * (d1 * th * th + 2.0f * delta * s + d0 * omt * omt);
-    const float iDn = 1.0f / Dn, iM = 1.0f / M;
+    const float iDn = nfk_div<FAST>(1.0f, Dn), iM = nfk_div<FAST>(1.0f, M);
     const float one_m2t = 1.0f - 2.0f * th;
     // partials of Dn, N, M over the base variables
     const float Dn_t = gap * one_m2t, Dn_dl = 1.0f - 2.0f * s, Dn_d0 = s, Dn_d1 = s;
@@ -174,13 +188,13 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
     const float f_h = N_h * iDn, f_d0 = (N_d0 - R * Dn_d0) * iDn, f_d1 = (-R * Dn_d1) * iDn;
     const float l_t = M_t * iM - 2.0f * Dn_t * iDn, l_dl = M_dl * iM - 2.0f * Dn_dl * iDn;
     const float l_d0 = M_d0 * iM - 2.0f * Dn_d0 * iDn, l_d1 = M_d1 * iM - 2.0f * Dn_d1 * iDn;
-    const float iw = 1.0f / w_k;
+    const float iw = nfk_div<FAST>(1.0f, w_k);
 
     float a, b, gx;  // g_bin = a * f_bin + b * lad_bin
     if (INV) {
         const float fprime = f_t * iw;
         const float gbar = gout - gl * (l_t * iw);
-        gx = gbar / fprime;
+        gx = nfk_div<FAST>(gbar, fprime);
         a = -gx;
         b = -gl;
     } else {
@@ -199,10 +213,10 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
     W.backward(k, g_cw, g_w, c.span, c.fw, c.scale2b, wr);
     H.backward(k, g_ch, g_h, c.yspan, c.fh, c.scale2b, hr);
     // derivative logits: d = min_d + softplus(v); v = softplus(r) under PRE
-    float gv0 = g_d0 * softplus_grad(v0), gv1 = g_d1 * softplus_grad(v1);
+    float gv0 = g_d0 * softplus_grad<FAST>(v0), gv1 = g_d1 * softplus_grad<FAST>(v1);
     if (PRE && !DFULL) {
-        gv0 *= softplus_grad(r0);
-        gv1 *= softplus_grad(r1);
+        gv0 *= softplus_grad<FAST>(r0);
+        gv1 *= softplus_grad<FAST>(r1);
     }
 #pragma unroll
     for (int j = 0; j < DN; ++j) {
