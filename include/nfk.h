@@ -377,6 +377,20 @@ int nfk_maf_bwd(const float* x, int64_t ldx, const float* init_param, const floa
 int nfk_trig_features_bwd(const float* x, int64_t ldx, const float* gfeat, int64_t ldgf, float* gx,
                           int64_t ldgx, int64_t batch, int32_t n, double B, nfk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Input-gradient GEMMs of the FCNN conditioner's backward (nfk_fcnn_bwd.hip;
+ * the dX chain of flows.py:20-35 differentiated), tanh's backward fused:
+ *   out[b, j] = (sum_p g[b, p] W[p, j]) * (1 - h[b, j]^2)    (h NULL: no factor)
+ * W [P, H] row-major (an nn.Linear weight, out x in) re-packed once by
+ * nfk_fcnn_dh_pack into nfk_fcnn_dh_pack_floats(P, H) floats (0: unsupported:
+ * P a multiple of 4, H <= 128).  fp16 two-way split on the matrix cores, fp32
+ * accumulation, per-row power-of-two scaling of g.  g rows 16-byte aligned.
+ * ------------------------------------------------------------------------- */
+int64_t nfk_fcnn_dh_pack_floats(int32_t P, int32_t H);
+int nfk_fcnn_dh_pack(const float* W, int32_t P, int32_t H, float* pack, nfk_stream_t stream);
+int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh,
+                int32_t H, float* out, int64_t ldo, int64_t batch, nfk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

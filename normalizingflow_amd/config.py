@@ -19,6 +19,9 @@ USE_CHAIN      in inference, run consecutive fused NSF_CL layers of one shape as
 USE_FUSED_VJP  training: NSF_CL's backward through nfk_fused_nsf_vjp (conditioner
                recompute on the matrix cores + spline VJP in one kernel) where
                the shape is supported; off: recompute GEMMs + nfk_rqs_coupling_bwd.
+USE_FCNN_DH    training: the stock FCNN backward's input-gradient GEMMs (g W,
+               tanh's backward fused) on nfk_fcnn_dh (fp16-split MFMA) where
+               the shape is supported; off: fp32 library GEMMs + tanh_backward.
 SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
                fp16-split products on the fp16 matrix cores (split_gemm.py,
                fp32-accurate) instead of fp32 GEMMs.  Off: torch.mm with
@@ -29,4 +32,5 @@ STRICT_CHECKS = True
 USE_FUSED = True
 USE_CHAIN = True
 USE_FUSED_VJP = True
+USE_FCNN_DH = True
 SPLIT_GEMM = False

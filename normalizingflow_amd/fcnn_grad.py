@@ -19,6 +19,9 @@ from __future__ import annotations
 
 import torch
 
+from . import config
+from . import kernels as K_
+
 _WG_ROWS = 8192   # rows per split-K slice of the weight-gradient GEMMs
 _WG_SLICES = 64   # at most this many slices
 
@@ -61,6 +64,23 @@ def wgrad(g, h):
     return out
 
 
+def dh(g, W, h):
+    """(g @ W) * (1 - h^2) (h None: g @ W): nfk_fcnn_dh on the matrix cores
+    where the shape allows (config.USE_FCNN_DH), else a library GEMM."""
+    if config.USE_FCNN_DH and g.is_cuda and g.dtype == torch.float32 and g.is_contiguous() \
+            and K_.fcnn_dh_pack_floats(*W.shape) > 0 and g.data_ptr() % 16 == 0:
+        # packed at every call: in training the weights change every step, and
+        # a cache keyed on storage pointers can be fooled by a freed weight's
+        # address coming back
+        pk = K_.fcnn_dh_pack(W)
+        if pk is not None:
+            out = torch.empty(g.shape[0], W.shape[1], dtype=g.dtype, device=g.device)
+            K_.fcnn_dh(g, pk, tuple(W.shape), h, out)
+            return out
+    y = g @ W
+    return y if h is None else torch.ops.aten.tanh_backward(y, h)
+
+
 def vjp(p, pre, cache, g, need_x, need):
     """(dL/dx or None, {name: grad}) of psi at the cached activations for the
     output gradient g; ``need``: the parameter names whose gradient is wanted."""
@@ -82,12 +102,12 @@ def vjp(p, pre, cache, g, need_x, need):
                 grads[nb] = wb[:, -1].contiguous()
 
     put(2, g, h2a)
-    ga2 = torch.ops.aten.tanh_backward(g @ W3, h2)
+    ga2 = dh(g, W3, h2)
     put(1, ga2, h1a)
-    ga1 = torch.ops.aten.tanh_backward(ga2 @ W2, h1)
+    ga1 = dh(ga2, W2, h1)
     if names[0] in need:
         grads[names[0]] = wgrad(ga1, x)
     if names[1] in need:
         grads[names[1]] = ga1.sum(0)
-    gx = ga1 @ W1 if need_x else None
+    gx = dh(ga1, W1, None) if need_x else None
     return gx, grads

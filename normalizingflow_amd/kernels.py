@@ -299,6 +299,37 @@ def radial_apply(x, x0, log_alpha, beta, sumsq, z, ld_scalar, *, logdet=None,
               _stream(dev))
 
 
+# ---- FCNN backward input-gradient GEMMs (nfk_fcnn_bwd.hip)
+def fcnn_dh_pack_floats(P, H):
+    return int(_lib.load().nfk_fcnn_dh_pack_floats(int(P), int(H)))
+
+
+def fcnn_dh_pack(W):
+    """Pack an nn.Linear weight W [P, H] for fcnn_dh (None: shape unsupported)."""
+    P, H = W.shape
+    n = fcnn_dh_pack_floats(P, H)
+    if n == 0:
+        return None
+    dev = _require_hip(W)
+    Wc = W.detach().to(F32).contiguous()
+    pack = torch.empty(n, dtype=F32, device=W.device)
+    _lib.call("nfk_fcnn_dh_pack", Wc.data_ptr(), P, H, pack.data_ptr(), _stream(dev))
+    return pack
+
+
+def fcnn_dh(g, pack, W_shape, h, out):
+    """out = (g @ W) * (1 - h^2) (h None: g @ W), W packed by fcnn_dh_pack."""
+    dev = _require_hip(g, pack, h, out)
+    P, H = W_shape
+    B = g.shape[0]
+    gp_, ldg = _mat(g, "g")
+    if g.shape[1] != P or out.shape != (B, H) or (h is not None and h.shape != (B, H)):
+        raise ValueError("fcnn_dh: shape mismatch")
+    hp, ldh = _mat(h, "h") if h is not None else (None, 0)
+    op, ldo = _mat(out, "out")
+    _timed("nfk_fcnn_dh", dev, "nfk_fcnn_dh", gp_, ldg, P, pack.data_ptr(), hp, ldh, H, op, ldo, B, _stream(dev))
+
+
 # ---- training backward of the remaining flow classes (nfk_flows_bwd.hip)
 def flows_bwd_workspace(batch, dim, device):
     """Scratch of nfk_flows_bwd_workspace_bytes (uint8, 256-byte aligned by the allocator)."""

@@ -61,12 +61,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle train step")
+    ap.add_argument("--no-fcnn-dh", action="store_true",
+                    help="library GEMMs + tanh_backward for the FCNN input gradients (config.USE_FCNN_DH off)")
     ap.add_argument("--split-gemm", action="store_true",
                     help="fp16-split conditioner GEMMs in the NSF_CL backward (config.SPLIT_GEMM on; "
                          "default off: hand-written fp32 backward, fcnn_grad)")
     args = ap.parse_args()
     from normalizingflow_amd import config
     config.SPLIT_GEMM = args.split_gemm
+    config.USE_FCNN_DH = not args.no_fcnn_dh
     dev = torch.device("cuda", 0)
     model, sd, _ = bench.build_model(args.workload, dev)
     x = torch.randn(args.batch, bench.WORKLOADS[args.workload][3], device=dev)
@@ -77,7 +80,8 @@ def main():
         return -torch.mean(plp + ld)
 
     res = {"metric": "samples/sec train step (NLL fwd + bwd + Adam)", "workload": args.workload,
-           "batch": args.batch, "steps": args.steps, "split_gemm": config.SPLIT_GEMM}
+           "batch": args.batch, "steps": args.steps, "split_gemm": config.SPLIT_GEMM,
+           "fcnn_dh": config.USE_FCNN_DH}
     t = timed(ours, opt, x, args.steps, args.warmup)
     res["hip"] = {"ms_per_step": round(t * 1e3, 3), "samples_per_s": round(args.batch / t, 1)}
     if not args.no_torch:
