@@ -115,8 +115,10 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
 
     // k-step 0 into slot 0
     for (int i = threadIdx.x; i < SLOT; i += 64 * kDhWaves) slot[0][i] = body[i];
-    float4 u, v;
+    // g two k-steps ahead: (u, v) this step, (u1, v1) the next
+    float4 u, v, u1, v1;
     load(0, u, v);
+    if (KB > 1) load(1, u1, v1);
     __syncthreads();
 
     f32x4 acc[NT];
@@ -135,8 +137,8 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
                 const int i = threadIdx.x + r * 64 * kDhWaves;
                 if (i < SLOT) nx[r] = body[(int64_t)(kb + 1) * SLOT + i];
             }
-            load(kb + 1, un, vn);
         }
+        if (kb + 2 < KB) load(kb + 2, un, vn);
         float mx = fmaxf(fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))),
                          fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
@@ -175,8 +177,12 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
                 const int i = threadIdx.x + r * 64 * kDhWaves;
                 if (i < SLOT) slot[cur ^ 1][i] = nx[r];
             }
-            u = un;
-            v = vn;
+        }
+        u = u1;
+        v = v1;
+        if (kb + 2 < KB) {
+            u1 = un;
+            v1 = vn;
         }
         __syncthreads();
     }
