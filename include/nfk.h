@@ -385,11 +385,14 @@ int nfk_trig_features_bwd(const float* x, int64_t ldx, const float* gfeat, int64
  * nfk_fcnn_dh_pack into nfk_fcnn_dh_pack_floats(P, H) floats (0: unsupported:
  * P a multiple of 4, H <= 128).  fp16 two-way split on the matrix cores, fp32
  * accumulation, per-row power-of-two scaling of g.  g rows 16-byte aligned.
+ * out element (b, j) is out[b*ldo + j*out_col_stride]; accumulate != 0 adds
+ * to it (e.g. the lower columns of a layer's dL/dx, written in place).
  * ------------------------------------------------------------------------- */
 int64_t nfk_fcnn_dh_pack_floats(int32_t P, int32_t H);
 int nfk_fcnn_dh_pack(const float* W, int32_t P, int32_t H, float* pack, nfk_stream_t stream);
 int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh,
-                int32_t H, float* out, int64_t ldo, int64_t batch, nfk_stream_t stream);
+                int32_t H, float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate,
+                int64_t batch, nfk_stream_t stream);
 
 #ifdef __cplusplus
 }

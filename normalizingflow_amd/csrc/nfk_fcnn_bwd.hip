@@ -89,7 +89,7 @@ template <int NT>
 __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ g, int64_t ldg, int P,
                                                       const float* __restrict__ pack, const float* __restrict__ h,
                                                       int64_t ldh, int H, float* __restrict__ out, int64_t ldo,
-                                                      int64_t B) {
+                                                      int64_t cso, int acc_out, int64_t B) {
     constexpr int SLOT = NT * 2 * 64;  // h8 fragments per k-step
     __shared__ h8 slot[2][SLOT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
     const float inv = ldexpf(1.0f, -es) * pack[0];
     // 4 consecutive features j0 .. j0 + 3 of one row per tile: one 16-byte h
     // load and out store where the rows allow it
-    const bool vec = ((ldh & 3) == 0 || h == nullptr) && (ldo & 3) == 0 &&
+    const bool vec = cso == 1 && ((ldh & 3) == 0 || h == nullptr) && (ldo & 3) == 0 &&
                      ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(h)) & 15) == 0;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -208,7 +208,15 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
                 d[2] *= 1.0f - hv.z * hv.z;
                 d[3] *= 1.0f - hv.w * hv.w;
             }
-            *reinterpret_cast<float4*>(out + row * ldo + j0) = make_float4(d[0], d[1], d[2], d[3]);
+            float4* o = reinterpret_cast<float4*>(out + row * ldo + j0);
+            if (acc_out) {
+                const float4 w = *o;
+                d[0] += w.x;
+                d[1] += w.y;
+                d[2] += w.z;
+                d[3] += w.w;
+            }
+            *o = make_float4(d[0], d[1], d[2], d[3]);
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -219,7 +227,8 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
                         const float hv = h[row * ldh + j];
                         v *= 1.0f - hv * hv;
                     }
-                    out[row * ldo + j] = v;
+                    float* o = out + row * ldo + (int64_t)j * cso;
+                    *o = acc_out ? *o + v : v;
                 }
             }
         }
@@ -250,7 +259,9 @@ extern "C" int nfk_fcnn_dh_pack(const float* W, int32_t P, int32_t H, float* pac
 }
 
 extern "C" int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh,
-                           int32_t H, float* out, int64_t ldo, int64_t batch, nfk_stream_t stream) {
+                           int32_t H, float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate,
+                           int64_t batch, nfk_stream_t stream) {
+    if (out_col_stride < 1) return nfk_set_error("nfk_fcnn_dh: bad output column stride");
     if (nfk_fcnn_dh_pack_floats(P, H) == 0 || batch < 0) return nfk_set_error("nfk_fcnn_dh: unsupported shape");
     if (batch == 0) return 0;
     if (!g || !pack || !out) return nfk_set_error("nfk_fcnn_dh: null pointer");
@@ -262,7 +273,7 @@ extern "C" int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* 
 #define CASE(nt)                                                                                                   \
     case nt:                                                                                                       \
         hipLaunchKernelGGL(k_dh<nt>, dim3((unsigned)blocks), dim3(64 * kDhWaves), 0, st, g, ldg, P, pack, h, ldh, H, \
-                           out, ldo, batch);                                                                       \
+                           out, ldo, out_col_stride, accumulate ? 1 : 0, batch);                                   \
         break;
     switch (NT) {
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)

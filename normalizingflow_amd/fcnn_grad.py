@@ -64,9 +64,11 @@ def wgrad(g, h):
     return out
 
 
-def dh(g, W, h):
+def dh(g, W, h, into=None):
     """(g @ W) * (1 - h^2) (h None: g @ W): nfk_fcnn_dh on the matrix cores
-    where the shape allows (config.USE_FCNN_DH), else a library GEMM."""
+    where the shape allows (config.USE_FCNN_DH), else a library GEMM.  With
+    ``into`` (a [B, H] view, any column stride) the result is added to it in
+    place and None is returned."""
     if config.USE_FCNN_DH and g.is_cuda and g.dtype == torch.float32 and g.is_contiguous() \
             and K_.fcnn_dh_pack_floats(*W.shape) > 0 and g.data_ptr() % 16 == 0:
         # packed at every call: in training the weights change every step, and
@@ -74,16 +76,25 @@ def dh(g, W, h):
         # address coming back
         pk = K_.fcnn_dh_pack(W)
         if pk is not None:
+            if into is not None:
+                K_.fcnn_dh(g, pk, tuple(W.shape), h, into, accumulate=True)
+                return None
             out = torch.empty(g.shape[0], W.shape[1], dtype=g.dtype, device=g.device)
             K_.fcnn_dh(g, pk, tuple(W.shape), h, out)
             return out
     y = g @ W
-    return y if h is None else torch.ops.aten.tanh_backward(y, h)
+    y = y if h is None else torch.ops.aten.tanh_backward(y, h)
+    if into is not None:
+        into += y
+        return None
+    return y
 
 
-def vjp(p, pre, cache, g, need_x, need):
+def vjp(p, pre, cache, g, need_x, need, gx_into=None):
     """(dL/dx or None, {name: grad}) of psi at the cached activations for the
-    output gradient g; ``need``: the parameter names whose gradient is wanted."""
+    output gradient g; ``need``: the parameter names whose gradient is wanted.
+    With ``gx_into`` (a view of the caller's dL/dx, e.g. the lower columns),
+    dL/dx is added into it and None returned in its place."""
     x, h1a, h2a = cache
     H = h1a.shape[1] - 1
     h1, h2 = h1a[:, :H], h2a[:, :H]
@@ -109,5 +120,5 @@ def vjp(p, pre, cache, g, need_x, need):
         grads[names[0]] = wgrad(ga1, x)
     if names[1] in need:
         grads[names[1]] = ga1.sum(0)
-    gx = dh(ga1, W1, None) if need_x else None
+    gx = dh(ga1, W1, None, into=gx_into) if need_x else None
     return gx, grads

@@ -443,6 +443,13 @@ class _SplineMaps:
         self.up_in, self.up_out = mk(up_in), mk(up_out)
         self.lo_in_long = self.lo_in.long()
         self.lists = (list(lo_in), list(lo_out), list(up_in), list(up_out))
+        # (start, stride) when the lower input columns are an arithmetic
+        # progression (every single-coordinate mask): x's lower columns are then
+        # a strided view, read and written in place
+        li = list(lo_in)
+        st = li[1] - li[0] if len(li) > 1 else 1
+        self.lo_prog = (li[0], st) if li and st > 0 and all(li[i] == li[0] + st * i for i in range(len(li))) \
+            else None
 
 
 class NSF_CL(_HipFlow):
@@ -581,10 +588,18 @@ class NSF_CL(_HipFlow):
                              None if gz is None else gz.contiguous(), None if gld is None else gld.contiguous(),
                              gp, gx, hbuf[0], hbuf[1], K=self.K, tail_bound=float(self.B), inverse=inverse)
             pmap = {n: t.detach() for n, t in zip(names, params)}
-            lower = x.index_select(1, maps.lo_in_long)
             want = {n for n, r in zip(names, need[1:]) if r}
+            n_lo = len(maps.lists[0])
+            if maps.lo_prog is not None:
+                # lower columns as strided views: no gather of x, and dL/dx of
+                # the lower columns added in place by the last input-gradient GEMM
+                a, st = maps.lo_prog
+                lower = x[:, a::st][:, :n_lo]
+                into = gx[:, a::st][:, :n_lo] if need[0] else None
+            else:
+                lower, into = x.index_select(1, maps.lo_in_long), None
             g_lower, grads = fcnn_grad.vjp(pmap, "psi.", (lower, hbuf[0][:, :H + 1], hbuf[1][:, :H + 1]),
-                                           gp, need[0], want)
+                                           gp, need[0], want, gx_into=into)
             if g_lower is not None:
                 gx.index_add_(1, maps.lo_in_long, g_lower)
             return [gx if need[0] else None] + [grads.get(n) for n in names]

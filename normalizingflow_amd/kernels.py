@@ -317,17 +317,22 @@ def fcnn_dh_pack(W):
     return pack
 
 
-def fcnn_dh(g, pack, W_shape, h, out):
-    """out = (g @ W) * (1 - h^2) (h None: g @ W), W packed by fcnn_dh_pack."""
+def fcnn_dh(g, pack, W_shape, h, out, *, accumulate=False):
+    """out (+)= (g @ W) * (1 - h^2) (h None: g @ W), W packed by fcnn_dh_pack;
+    out may be a column-strided view (e.g. x's lower columns)."""
     dev = _require_hip(g, pack, h, out)
     P, H = W_shape
     B = g.shape[0]
     gp_, ldg = _mat(g, "g")
-    if g.shape[1] != P or out.shape != (B, H) or (h is not None and h.shape != (B, H)):
+    if g.shape[1] != P or tuple(out.shape) != (B, H) or (h is not None and h.shape != (B, H)):
         raise ValueError("fcnn_dh: shape mismatch")
+    if out.dtype != F32 or out.dim() != 2:
+        raise ValueError("fcnn_dh: out must be a 2-D float32 tensor")
     hp, ldh = _mat(h, "h") if h is not None else (None, 0)
-    op, ldo = _mat(out, "out")
-    _timed("nfk_fcnn_dh", dev, "nfk_fcnn_dh", gp_, ldg, P, pack.data_ptr(), hp, ldh, H, op, ldo, B, _stream(dev))
+    ldo = out.stride(0) if B > 1 else H * max(out.stride(1), 1)
+    cso = out.stride(1) if H > 1 else 1
+    _timed("nfk_fcnn_dh", dev, "nfk_fcnn_dh", gp_, ldg, P, pack.data_ptr(), hp, ldh, H, out.data_ptr(), ldo,
+           cso, 1 if accumulate else 0, B, _stream(dev))
 
 
 # ---- training backward of the remaining flow classes (nfk_flows_bwd.hip)

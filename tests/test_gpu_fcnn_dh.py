@@ -87,3 +87,17 @@ def test_fcnn_vjp_kernel_vs_library(hip_device):
     torch.testing.assert_close(gx_k, gx_l, rtol=1e-4, atol=1e-5 * float(gx_l.abs().max()))
     for k in p:
         torch.testing.assert_close(gr_k[k], gr_l[k], rtol=1e-4, atol=1e-5 * float(gr_l[k].abs().max()))
+
+
+def test_fcnn_dh_accumulate_into_strided_columns(hip_device):
+    """dL/dx of a layer's lower columns added in place into x's gradient
+    (columns a, a + st, ...: the single-coordinate NSF_CL masks)."""
+    B, P, H = 700, 100, 32
+    g = torch.randn(B, P, device=hip_device)
+    W = torch.randn(P, H, device=hip_device) * 0.1
+    for a, st in ((0, 2), (1, 2), (0, 1)):
+        gx = torch.randn(B, 64, device=hip_device)
+        ref = gx.clone().double()
+        ref[:, a::st][:, :H] += g.double() @ W.double()
+        assert fcnn_grad.dh(g, W, None, into=gx[:, a::st][:, :H]) is None
+        torch.testing.assert_close(gx.double(), ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
