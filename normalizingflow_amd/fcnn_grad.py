@@ -58,7 +58,9 @@ def wgrad(g, h):
     if S <= 1:
         return g.t() @ h
     R = B // S
-    out = torch.bmm(g[:S * R].view(S, R, -1).transpose(1, 2), h[:S * R].view(S, R, -1)).sum(0)
+    # (h^T g)^T: the batched GEMM with the narrow operand first measured 3 %
+    # faster than g^T h at c3's [736 x 101] (tools/ubench_wgrad.py)
+    out = torch.bmm(h[:S * R].view(S, R, -1).transpose(1, 2), g[:S * R].view(S, R, -1)).sum(0).t()
     if S * R < B:
         out += g[S * R:].t() @ h[S * R:]
     return out
