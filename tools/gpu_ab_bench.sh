@@ -9,7 +9,7 @@ for w in $WL; do
     for v in cur $V; do
       if [ $v = cur ]; then unset NFK_LIBRARY; else export NFK_LIBRARY=build_ab/$v/libnfk.so; fi
       timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline --parity-rows 4096 > $O/$w-$v-$r.json 2> $O/$w-$v-$r.err || { echo "bench $w $v failed"; tail -5 $O/$w-$v-$r.err; exit 1; }
-      echo "$w $v $r: $(python3 -c "import json;d=json.loads(open('$O/$w-$v-$r.json').read().strip().splitlines()[-1]);print(round(d["value"]/1e6,2), "M/s", round(d["ms_per_step"],3), "ms", "parity", d.get("parity",{}).get("pass"))")"
+      echo "$w $v $r: $(python3 tools/bench_line.py $O/$w-$v-$r.json)"
     done
   done
 done
