@@ -34,8 +34,11 @@ def linears(p, pre):
 def _with_ones(B, H, like):
     """[B, H + 1] with a ones last column: the hidden activations are written
     into [:, :H], so one GEMM against it yields a weight gradient and, in its
-    last column, the bias gradient (the column sum of the output gradient)."""
-    a = torch.empty(B, H + 1, dtype=like.dtype, device=like.device)
+    last column, the bias gradient (the column sum of the output gradient).
+    Rows are padded to a multiple of 4 floats (16-byte aligned), so nfk_fcnn_dh
+    reads the activations as float4s."""
+    ld = (H + 1 + 3) // 4 * 4
+    a = torch.empty(B, ld, dtype=like.dtype, device=like.device)[:, :H + 1]
     a[:, H].fill_(1.0)
     return a
 
