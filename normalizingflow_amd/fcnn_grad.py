@@ -5,10 +5,12 @@ The layer kernels save only their input; the backward recomputes the three
 activations and forms the vector-Jacobian products by hand instead of through
 autograd, so each product is a GEMM of the shape that suits the device:
 
-* input and hidden gradients (g @ W, M = batch): one GEMM each;
-* weight gradients g^T h reduce over the batch (against [h | 1], so the same
-  GEMM's last column is the bias gradient) (K = 2^20 rows against 100 x 100
-  or 736 x 100 outputs).  A single GEMM of that shape has a few dozen output
+* input and hidden gradients (g @ W, M = batch, tanh's backward fused):
+  nfk_fcnn_dh on the matrix cores (dh), else one library GEMM each;
+* weight gradients g^T h reduce over the batch (against [h | 1] when the
+  activations come with a ones column, as nfk_fused_nsf_vjp writes them, so
+  the same GEMM's last column is the bias gradient; else a GEMM and a column
+  sum) (K = 2^20 rows against 100 x 100 or 736 x 100 outputs).  A single GEMM of that shape has a few dozen output
   tiles for 256 CUs, so the batch is split into S slices and the S partial
   products (one batched GEMM) summed: split-K by hand (wgrad).
 
@@ -31,27 +33,14 @@ def linears(p, pre):
     return tuple(p[pre + "network.%d.%s" % (i, k)] for i in (0, 2, 4) for k in ("weight", "bias"))
 
 
-def _with_ones(B, H, like):
-    """[B, H + 1] with a ones last column: the hidden activations are written
-    into [:, :H], so one GEMM against it yields a weight gradient and, in its
-    last column, the bias gradient (the column sum of the output gradient).
-    Rows are padded to a multiple of 4 floats (16-byte aligned), so nfk_fcnn_dh
-    reads the activations as float4s."""
-    ld = (H + 1 + 3) // 4 * 4
-    a = torch.empty(B, ld, dtype=like.dtype, device=like.device)[:, :H + 1]
-    a[:, H].fill_(1.0)
-    return a
-
-
 def forward_saved(p, pre, x):
-    """psi(x) and the activations its backward needs: (x, [h1 | 1], [h2 | 1])."""
+    """psi(x) and the activations its backward needs: (x, h1, h2), dense [B, H]."""
     W1, b1, W2, b2, W3, b3 = linears(p, pre)
-    B, H = x.shape[0], W1.shape[0]
-    h1a = _with_ones(B, H, x)
-    torch.tanh(torch.addmm(b1, x, W1.t()), out=h1a[:, :H])
-    h2a = _with_ones(B, H, x)
-    torch.tanh(torch.addmm(b2, h1a[:, :H], W2.t()), out=h2a[:, :H])
-    return torch.addmm(b3, h2a[:, :H], W3.t()), (x, h1a, h2a)
+    # W^T materialised: with the transposed view hipBLASLt picked a kernel 2.1x
+    # slower for the 100 x 100 layer at 2^20 rows (tools/ubench_linear2.py)
+    h1 = torch.tanh(torch.addmm(b1, x, W1.t().contiguous()))
+    h2 = torch.tanh(torch.addmm(b2, h1, W2.t().contiguous()))
+    return torch.addmm(b3, h2, W3.t().contiguous()), (x, h1, h2)
 
 
 def wgrad(g, h):
@@ -101,21 +90,30 @@ def vjp(p, pre, cache, g, need_x, need, gx_into=None):
     With ``gx_into`` (a view of the caller's dL/dx, e.g. the lower columns),
     dL/dx is added into it and None returned in its place."""
     x, h1a, h2a = cache
-    H = h1a.shape[1] - 1
-    h1, h2 = h1a[:, :H], h2a[:, :H]
     W1, b1, W2, b2, W3, b3 = linears(p, pre)
+    H = W1.shape[0]
+    # the activations come as [B, H] or, from nfk_fused_nsf_vjp, as [h | 1]
+    ones = h1a.shape[1] == H + 1
+    h1, h2 = h1a[:, :H], h2a[:, :H]
     names = [pre + "network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias")]
     grads = {}
 
     def put(i, g_out, act_a):
-        """weight and bias gradient of Linear i from ONE GEMM against [act | 1]"""
+        """weight and bias gradient of Linear i: one GEMM against [act | 1] (its
+        last column the bias gradient), or a GEMM and a column sum"""
         nw, nb = names[2 * i], names[2 * i + 1]
         if nw in need or nb in need:
-            wb = wgrad(g_out, act_a)
-            if nw in need:
-                grads[nw] = wb[:, :-1].contiguous()
-            if nb in need:
-                grads[nb] = wb[:, -1].contiguous()
+            if ones:
+                wb = wgrad(g_out, act_a)
+                if nw in need:
+                    grads[nw] = wb[:, :-1].contiguous()
+                if nb in need:
+                    grads[nb] = wb[:, -1].contiguous()
+            else:
+                if nw in need:
+                    grads[nw] = wgrad(g_out, act_a).contiguous()
+                if nb in need:
+                    grads[nb] = g_out.sum(0)
 
     put(2, g, h2a)
     ga2 = dh(g, W3, h2)
