@@ -58,10 +58,10 @@ namespace nfk_fused {
 constexpr int kWideFB = NFK_WIDE_FB;             // f16 blocks of a frame
 constexpr int kWideSlotBlocks = kWideFB + 1;     // + the record's bias block
 constexpr int kWideWaves = NFK_WIDE_NW;          // waves per workgroup
-constexpr int kWideWGs = 8 / kWideWaves;         // workgroups per CU
+constexpr int kWideWGs = kWideWaves == 4 ? 2 : 1;  // workgroups per CU
 constexpr int kWideTile = 16 * 32;               // floats of a wave's chunk-pair tile
 static_assert(kWideFB == 32 || kWideFB == 64, "frame of 32 or 64 blocks");
-static_assert(kWideWaves == 4 || kWideWaves == 8, "4- or 8-wave workgroups");
+static_assert(kWideWaves == 4 || kWideWaves == 8 || kWideWaves == 12, "4-, 8- or 12-wave workgroups");
 
 // k-blocks per sub-record of a record with nt tiles
 __host__ __device__ constexpr int wide_g(int nt, int kbh) {
