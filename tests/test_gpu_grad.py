@@ -468,3 +468,23 @@ def test_split_gemm_linear_vs_fp64():
     rel_close(x.grad, xd.grad, 2e-6, "gx")
     rel_close(w.grad, wd.grad, 2e-6, "gw")
     rel_close(b.grad, bd.grad, 2e-6, "gb")
+
+
+@pytest.mark.parametrize("name", ["planar_tanh", "radial", "actnorm", "maf"])
+def test_backward_bitwise_reproducible(name, hip_device):
+    """The parameter gradients are batch sums formed in a fixed order (no
+    atomics, nfk_flows_bwd.hip): two backward passes agree bit for bit."""
+    make, d, _ = LAYERS[name]
+    torch.manual_seed(21)
+    layer = make().to(hip_device)
+    x = torch.randn(5000, d, device=hip_device)
+    gz = torch.randn(5000, d, device=hip_device)
+    got = []
+    for _ in range(2):
+        layer.zero_grad(set_to_none=True)
+        xg = x.clone().requires_grad_(True)
+        z, ld = layer(xg)
+        ((z * gz).sum() + ld.sum()).backward()
+        got.append([xg.grad.clone()] + [p.grad.clone() for p in layer.parameters()])
+    for a, b in zip(*got):
+        assert torch.equal(a, b)
