@@ -393,6 +393,14 @@ int nfk_fcnn_dh_pack(const float* W, int32_t P, int32_t H, float* pack, nfk_stre
 int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh,
                 int32_t H, float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate,
                 int64_t batch, nfk_stream_t stream);
+/* The same kernel in forward form, for the training recompute of one FCNN
+ * Linear (flows.py:26-31, nn.Linear + optional nn.Tanh):
+ *   out[b, j] = act(sum_p x[b, p] W[p, j] + bias[j])   act = tanh if tanh_out
+ * W [P, H] is the nn.Linear weight TRANSPOSED (in x out), packed by
+ * nfk_fcnn_dh_pack; bias may be NULL.  x rows 16-byte aligned, out dense rows. */
+int nfk_fcnn_linear(const float* x, int64_t ldx, int32_t P, const float* pack, const float* bias,
+                    int32_t tanh_out, int32_t H, float* out, int64_t ldo, int64_t batch,
+                    nfk_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -22,6 +22,9 @@ USE_FUSED_VJP  training: NSF_CL's backward through nfk_fused_nsf_vjp (conditione
 USE_FCNN_DH    training: the stock FCNN backward's input-gradient GEMMs (g W,
                tanh's backward fused) on nfk_fcnn_dh (fp16-split MFMA) where
                the shape is supported; off: fp32 library GEMMs + tanh_backward.
+USE_FCNN_FWD   training: the stock FCNN's recompute forward (Linear + bias +
+               Tanh) on nfk_fcnn_linear, the same kernel in forward form;
+               off: library GEMMs (addmm) + tanh.
 SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
                fp16-split products on the fp16 matrix cores (split_gemm.py,
                fp32-accurate) instead of fp32 GEMMs.  Off: torch.mm with
@@ -33,4 +36,5 @@ USE_FUSED = True
 USE_CHAIN = True
 USE_FUSED_VJP = True
 USE_FCNN_DH = True
+USE_FCNN_FWD = True
 SPLIT_GEMM = False

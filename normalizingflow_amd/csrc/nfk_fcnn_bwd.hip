@@ -89,7 +89,8 @@ template <int NT>
 __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ g, int64_t ldg, int P,
                                                       const float* __restrict__ pack, const float* __restrict__ h,
                                                       int64_t ldh, int H, float* __restrict__ out, int64_t ldo,
-                                                      int64_t cso, int acc_out, int64_t B) {
+                                                      int64_t cso, int acc_out, const float* __restrict__ bias,
+                                                      int tanh_out, int64_t B) {
     constexpr int SLOT = NT * 2 * 64;  // h8 fragments per k-step
     __shared__ h8 slot[2][SLOT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
@@ -199,7 +200,12 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
         if (j0 >= H) continue;
         float d[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) d[r] = acc[t][r] * inv;
+        for (int r = 0; r < 4; ++r) {
+            // forward form (nfk_fcnn_linear): + bias, then tanh
+            d[r] = acc[t][r] * inv;
+            if (bias != nullptr && j0 + r < H) d[r] += bias[j0 + r];
+            if (tanh_out) d[r] = tanhf(d[r]);
+        }
         if (vec && j0 + 4 <= H) {
             if (h != nullptr) {
                 const float4 hv = *reinterpret_cast<const float4*>(h + row * ldh + j0);
@@ -258,9 +264,30 @@ extern "C" int nfk_fcnn_dh_pack(const float* W, int32_t P, int32_t H, float* pac
     return launch_status("nfk_fcnn_dh_pack");
 }
 
+namespace {
+int dh_launch(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh, int32_t H,
+              float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate, const float* bias, int tanh_out,
+              int64_t batch, hipStream_t st);
+}
+
 extern "C" int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh,
                            int32_t H, float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate,
                            int64_t batch, nfk_stream_t stream) {
+    return dh_launch(g, ldg, P, pack, h, ldh, H, out, ldo, out_col_stride, accumulate, nullptr, 0, batch,
+                     (hipStream_t)stream);
+}
+
+extern "C" int nfk_fcnn_linear(const float* x, int64_t ldx, int32_t P, const float* pack, const float* bias,
+                               int32_t tanh_out, int32_t H, float* out, int64_t ldo, int64_t batch,
+                               nfk_stream_t stream) {
+    return dh_launch(x, ldx, P, pack, nullptr, 0, H, out, ldo, 1, 0, bias, tanh_out ? 1 : 0, batch,
+                     (hipStream_t)stream);
+}
+
+namespace {
+int dh_launch(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh, int32_t H,
+              float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate, const float* bias, int tanh_out,
+              int64_t batch, hipStream_t st) {
     if (out_col_stride < 1) return nfk_set_error("nfk_fcnn_dh: bad output column stride");
     if (nfk_fcnn_dh_pack_floats(P, H) == 0 || batch < 0) return nfk_set_error("nfk_fcnn_dh: unsupported shape");
     if (batch == 0) return 0;
@@ -268,12 +295,11 @@ extern "C" int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* 
     if ((ldg & 3) || (reinterpret_cast<uintptr_t>(g) & 15))
         return nfk_set_error("nfk_fcnn_dh: g rows must be 16-byte aligned");
     const int64_t blocks = (batch + 16 * kDhWaves - 1) / (16 * kDhWaves);
-    hipStream_t st = (hipStream_t)stream;
     const int NT = (H + 15) / 16;
 #define CASE(nt)                                                                                                   \
     case nt:                                                                                                       \
         hipLaunchKernelGGL(k_dh<nt>, dim3((unsigned)blocks), dim3(64 * kDhWaves), 0, st, g, ldg, P, pack, h, ldh, H, \
-                           out, ldo, out_col_stride, accumulate ? 1 : 0, batch);                                   \
+                           out, ldo, out_col_stride, accumulate ? 1 : 0, bias, tanh_out, batch);                   \
         break;
     switch (NT) {
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
@@ -282,3 +308,4 @@ extern "C" int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* 
 #undef CASE
     return launch_status("nfk_fcnn_dh");
 }
+}  // namespace

@@ -36,6 +36,16 @@ def linears(p, pre):
 def forward_saved(p, pre, x):
     """psi(x) and the activations its backward needs: (x, h1, h2), dense [B, H]."""
     W1, b1, W2, b2, W3, b3 = linears(p, pre)
+    if config.USE_FCNN_FWD and _kernel_ok(x) and all(K_.fcnn_dh_pack_floats(W.shape[1], W.shape[0]) > 0
+                                                     for W in (W1, W2, W3)):
+        # nfk_fcnn_linear: bias and tanh in the GEMM's epilogue
+        def lin(a, W, b, act):
+            out = torch.empty(a.shape[0], W.shape[0], dtype=a.dtype, device=a.device)
+            K_.fcnn_linear(a, K_.fcnn_dh_pack(W.t()), (W.shape[1], W.shape[0]), b.contiguous(), out, tanh=act)
+            return out
+        h1 = lin(x, W1, b1, True)
+        h2 = lin(h1, W2, b2, True)
+        return lin(h2, W3, b3, False), (x, h1, h2)
     # W^T materialised: with the transposed view hipBLASLt picked a kernel 2.1x
     # slower for the 100 x 100 layer at 2^20 rows (tools/ubench_linear2.py)
     h1 = torch.tanh(torch.addmm(b1, x, W1.t().contiguous()))
@@ -58,13 +68,20 @@ def wgrad(g, h):
     return out
 
 
+def _kernel_ok(a):
+    """a can feed nfk_fcnn_dh / nfk_fcnn_linear: HIP fp32, unit column
+    stride, rows 16-byte aligned (a row-strided view such as x's lower half is
+    fine)."""
+    return a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and a.shape[0] > 0 \
+        and (a.shape[1] == 1 or a.stride(1) == 1) and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0
+
+
 def dh(g, W, h, into=None):
     """(g @ W) * (1 - h^2) (h None: g @ W): nfk_fcnn_dh on the matrix cores
     where the shape allows (config.USE_FCNN_DH), else a library GEMM.  With
     ``into`` (a [B, H] view, any column stride) the result is added to it in
     place and None is returned."""
-    if config.USE_FCNN_DH and g.is_cuda and g.dtype == torch.float32 and g.is_contiguous() \
-            and K_.fcnn_dh_pack_floats(*W.shape) > 0 and g.data_ptr() % 16 == 0:
+    if config.USE_FCNN_DH and _kernel_ok(g) and K_.fcnn_dh_pack_floats(*W.shape) > 0:
         # packed at every call: in training the weights change every step, and
         # a cache keyed on storage pointers can be fooled by a freed weight's
         # address coming back

@@ -335,6 +335,20 @@ def fcnn_dh(g, pack, W_shape, h, out, *, accumulate=False):
            cso, 1 if accumulate else 0, B, _stream(dev))
 
 
+def fcnn_linear(x, pack, W_shape, bias, out, *, tanh=False):
+    """out = x @ W + bias (tanh'd when ``tanh``), W [P, H] packed by fcnn_dh_pack
+    (an nn.Linear's weight transposed): the FCNN forward on the same kernel."""
+    dev = _require_hip(x, pack, bias, out)
+    P, H = W_shape
+    B = x.shape[0]
+    xp, ldx = _mat(x, "x")
+    op, ldo = _mat(out, "out")
+    if x.shape[1] != P or tuple(out.shape) != (B, H):
+        raise ValueError("fcnn_linear: shape mismatch")
+    _timed("nfk_fcnn_linear", dev, "nfk_fcnn_linear", xp, ldx, P, pack.data_ptr(), _vec(bias, H, "bias"),
+           1 if tanh else 0, H, op, ldo, B, _stream(dev))
+
+
 # ---- training backward of the remaining flow classes (nfk_flows_bwd.hip)
 def flows_bwd_workspace(batch, dim, device):
     """Scratch of nfk_flows_bwd_workspace_bytes (uint8, 256-byte aligned by the allocator)."""

@@ -101,3 +101,46 @@ def test_fcnn_dh_accumulate_into_strided_columns(hip_device):
         ref[:, a::st][:, :H] += g.double() @ W.double()
         assert fcnn_grad.dh(g, W, None, into=gx[:, a::st][:, :H]) is None
         torch.testing.assert_close(gx.double(), ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("B,P,H,tanh,strided", [(3000, 32, 100, True, True), (1000, 100, 100, True, False),
+                                                (777, 100, 32, False, False), (65, 4, 7, True, False)])
+def test_fcnn_linear_vs_fp64(B, P, H, tanh, strided, hip_device):
+    """nfk_fcnn_linear, the forward form: act(x W^T + b) against fp64, with the
+    split's bound (on the pre-activation; tanh is 1-Lipschitz) plus a few ulps
+    of tanhf; x may be a row-strided view (RealNVP's lower half)."""
+    gen = torch.Generator().manual_seed(B + P)
+    lin = torch.nn.Linear(P, H)
+    xs = torch.randn(B, 2 * P if strided else P, generator=gen) * 2
+    x = xs[:, :P]
+    W, b = lin.weight.detach(), lin.bias.detach()
+    pre = x.double() @ W.double().t() + b.double()
+    ref = torch.tanh(pre) if tanh else pre
+    bound = x.double().abs().sum(1, keepdim=True) * W.double().abs().max()
+    xd = xs.to(hip_device)[:, :P]
+    Wd, bd = W.to(hip_device), b.to(hip_device)
+    out = torch.empty(B, H, device=hip_device)
+    K_.fcnn_linear(xd, K_.fcnn_dh_pack(Wd.t()), (P, H), bd, out, tanh=tanh)
+    err = (out.cpu().double() - ref).abs()
+    assert bool((err <= 8e-6 * bound + 4e-7 * (1 + ref.abs())).all()), float(err.max())
+
+
+def test_forward_saved_kernel_vs_library(hip_device):
+    torch.manual_seed(5)
+    net = torch.nn.Sequential(torch.nn.Linear(32, 100), torch.nn.Tanh(), torch.nn.Linear(100, 100),
+                              torch.nn.Tanh(), torch.nn.Linear(100, 32)).to(hip_device)
+    p = {"s.network.%d.%s" % (i, k): getattr(net[i], k).detach() for i in (0, 2, 4) for k in ("weight", "bias")}
+    x = torch.randn(5000, 64, device=hip_device)[:, 32:]
+    prev = config.USE_FCNN_FWD
+    try:
+        config.USE_FCNN_FWD = True
+        y_k, c_k = fcnn_grad.forward_saved(p, "s.", x)
+        config.USE_FCNN_FWD = False
+        y_l, c_l = fcnn_grad.forward_saved(p, "s.", x)
+    finally:
+        config.USE_FCNN_FWD = prev
+    torch.testing.assert_close(y_k, y_l, rtol=1e-5, atol=2e-5 * float(y_l.abs().max()))
+    for a, b_ in zip(c_k[1:], c_l[1:]):
+        torch.testing.assert_close(a, b_, rtol=1e-5, atol=2e-6)
+    with torch.no_grad():
+        torch.testing.assert_close(y_l, net(x), rtol=1e-5, atol=1e-5)

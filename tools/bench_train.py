@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle train step")
+    ap.add_argument("--no-fcnn-fwd", action="store_true",
+                    help="recompute forward of FCNN conditioners on library GEMMs")
     ap.add_argument("--no-fcnn-dh", action="store_true",
                     help="library GEMMs + tanh_backward for the FCNN input gradients (config.USE_FCNN_DH off)")
     ap.add_argument("--split-gemm", action="store_true",
@@ -70,6 +72,7 @@ def main():
     from normalizingflow_amd import config
     config.SPLIT_GEMM = args.split_gemm
     config.USE_FCNN_DH = not args.no_fcnn_dh
+    config.USE_FCNN_FWD = not args.no_fcnn_fwd
     dev = torch.device("cuda", 0)
     model, sd, _ = bench.build_model(args.workload, dev)
     x = torch.randn(args.batch, bench.WORKLOADS[args.workload][3], device=dev)
@@ -81,7 +84,7 @@ def main():
 
     res = {"metric": "samples/sec train step (NLL fwd + bwd + Adam)", "workload": args.workload,
            "batch": args.batch, "steps": args.steps, "split_gemm": config.SPLIT_GEMM,
-           "fcnn_dh": config.USE_FCNN_DH}
+           "fcnn_dh": config.USE_FCNN_DH, "fcnn_fwd": config.USE_FCNN_FWD}
     t = timed(ours, opt, x, args.steps, args.warmup)
     res["hip"] = {"ms_per_step": round(t * 1e3, 3), "samples_per_s": round(args.batch / t, 1)}
     if not args.no_torch:
