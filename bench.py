@@ -342,13 +342,16 @@ def main():
                     help="one fused launch per layer instead of one chained launch per run of layers")
     ap.add_argument("--sync-checks", action="store_true",
                     help="status checks with a host sync per call (config.STRICT_CHECKS = True)")
+    ap.add_argument("--dist", action="store_true",
+                    help="a process group and the NLL all-reduce even at N = 1 (RCCL on a one-GPU box)")
     args = ap.parse_args()
 
     from normalizingflow_amd import config, dist as nfdist, kernels
     from normalizingflow_amd import flush_status_checks
     import torch.distributed as dist
 
-    rank, world, local = nfdist.init_from_env(backend=args.backend)
+    rank, world, local = nfdist.init_from_env(backend=args.backend, force=args.dist)
+    use_dist = world > 1 or args.dist
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     # gloo runs share one device when there are fewer devices than ranks (tests)
@@ -376,7 +379,7 @@ def main():
     def step():
         nonlocal nll
         lp = model.log_prob(x)
-        if world > 1:
+        if use_dist:
             nll = nfdist.nll_allreduce(lp)
         return lp
 
@@ -387,19 +390,19 @@ def main():
     timer = None
     if not args.no_timer:
         timer = kernels.TIMER = kernels.KernelTimer()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         lp = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     kernels.TIMER = None
     flush_status_checks()  # the reference's errors, if any step raised one
-    if world > 1:
+    if use_dist:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -437,7 +440,7 @@ def main():
             "config": {"workload": args.workload + ": " + desc, "global_batch": total,
                        "per_gpu_batch": B, "parallelism": "dp%d (sample sharding)" % world,
                        "scaling": args.scaling,
-                       "backend": (args.backend or "nccl") if world > 1 else None,
+                       "backend": (args.backend or "nccl") if use_dist else None,
                        "fused_layer_kernel": bool(config.USE_FUSED),
                        "chained_layers": bool(config.USE_FUSED and config.USE_CHAIN),
                        "status_checks": "sync per call" if args.sync_checks else
@@ -451,7 +454,7 @@ def main():
             "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4)} for k, v in summary.items()},
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

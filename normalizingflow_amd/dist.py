@@ -63,17 +63,19 @@ def attach_process_group(model, group=None):
     return model
 
 
-def init_from_env(backend=None):
+def init_from_env(backend=None, force=False):
     """torchrun-style init: RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* from env.
     Returns (rank, world, local_rank); a no-op single process when WORLD_SIZE
-    is unset."""
+    is unset, unless ``force`` (a world of one still gets a process group, so
+    the collectives run through the backend, e.g. RCCL on a one-GPU box)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world)

@@ -61,3 +61,35 @@ def test_bench_world2_nll_vs_oracle(hip_device, scaling, rows):
     ref = orc.model_log_prob(bench.specs_for("c3"), {k: v.cpu() for k, v in sd.items()}, x)
     nll_ref = float(-ref.double().mean())
     assert abs(line["nll"] - nll_ref) <= 1e-5 * abs(nll_ref), (line["nll"], nll_ref)
+
+
+def test_bench_rccl_world1_nll_vs_oracle(hip_device):
+    """The RCCL leg of the same path: one rank under torchrun with a real
+    "nccl" (RCCL) process group (--dist keeps the group and the NLL
+    all-reduce at N = 1), so the collective the driver's 8-GPU run uses
+    executes on the hardware; the all-reduced NLL equals the oracle's."""
+    sys.path.insert(0, REPO)
+    import bench
+    from oracle import nf_oracle as orc
+
+    rows = 8192
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "1", "--backend", "nccl", "--dist",
+           "--batch", str(rows), "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+           "--parity-rows", "1024"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["config"]["backend"] == "nccl"
+    assert line["value"] > 0 and line["parity"]["pass"] and line["nll"] is not None
+
+    g = torch.Generator(device=hip_device).manual_seed(0)
+    x = torch.randn(rows, 64, generator=g, device=hip_device).cpu()
+    _, sd, _ = bench.build_model("c3", hip_device)
+    ref = orc.model_log_prob(bench.specs_for("c3"), {k: v.cpu() for k, v in sd.items()}, x)
+    nll_ref = float(-ref.double().mean())
+    assert abs(line["nll"] - nll_ref) <= 1e-5 * abs(nll_ref), (line["nll"], nll_ref)
