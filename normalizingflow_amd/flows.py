@@ -20,10 +20,13 @@ What runs where (ROCm device only -- CPU tensors raise, there is no fallback):
   OneByOneConv   x @ P @ L @ (U + diag S) as library GEMMs -- flows_1.py:218-252
 Gradients: when autograd needs them (grad mode on and x or a parameter
 requires grad) a layer runs as ``_LayerFn``: the forward is the same HIP
-kernel chain; backward recomputes the layer from the saved input with the
-differentiable torch restatement (``torch_math``) on the same device and
-back-propagates through it (activation memory = one input per layer, like
-gradient checkpointing).  Hand-written backward kernels are the next step.
+kernel chain; backward starts from the saved input (activation memory = one
+input per layer, like gradient checkpointing) and runs hand-written kernels:
+nfk_fused_nsf_vjp (NSF_CL conditioner recompute + spline VJP), fcnn_grad
+(conditioner backward), nfk_affine_coupling_bwd (RealNVP) and the per-row
+VJP kernels of nfk_flows_bwd.hip (Planar, Radial, ActNorm, MAF, NSF_AR).
+Only user-supplied (non-FCNN) conditioners back-propagate through the
+differentiable torch restatement (``torch_math``).
 """
 from __future__ import annotations
 

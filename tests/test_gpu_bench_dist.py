@@ -93,3 +93,15 @@ def test_bench_rccl_world1_nll_vs_oracle(hip_device):
     ref = orc.model_log_prob(bench.specs_for("c3"), {k: v.cpu() for k, v in sd.items()}, x)
     nll_ref = float(-ref.double().mean())
     assert abs(line["nll"] - nll_ref) <= 1e-5 * abs(nll_ref), (line["nll"], nll_ref)
+
+
+def test_bench_c1_moons_vs_oracle(hip_device):
+    """BASELINE c1 (2-D two moons, 4-layer RealNVP, H=100, B=4096) through
+    bench.py on the GPU: the benched log_prob of every row vs the oracle."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "c1", "--steps", "5",
+           "--warmup", "2", "--no-cpu-baseline", "--parity-rows", "4096"]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["config"]["global_batch"] == 4096 and line["value"] > 0
+    assert line["parity"]["rows"] == 4096 and line["parity"]["pass"], line["parity"]

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 cd "$ROOT"
 fatal() { case $1 in 0|1) return 1;; *) echo "FATAL rc=$1 in $2"; exit $1;; esac; }
 
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+timeout -k 10 900 python -m pytest tests -m gpu -q -rfs > "$OUT/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"; fatal $rc pytest
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; fatal $rc smoke
