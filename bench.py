@@ -384,6 +384,9 @@ def main():
                     help="one fused launch per layer instead of one chained launch per run of layers")
     ap.add_argument("--sync-checks", action="store_true",
                     help="status checks with a host sync per call (config.STRICT_CHECKS = True)")
+    ap.add_argument("--graph", default="auto", choices=("auto", "on", "off"),
+                    help="replay log_prob as one HIP graph (graphs.GraphedLogProb); auto: for the "
+                         "small-batch workloads (c1), where launches bound the step")
     ap.add_argument("--dist", action="store_true",
                     help="a process group and the NLL all-reduce even at N = 1 (RCCL on a one-GPU box)")
     args = ap.parse_args()
@@ -420,10 +423,15 @@ def main():
     x = make_x(args.workload, B, g, device)  # resident in HBM before timing
 
     nll = None
+    use_graph = args.graph == "on" or (args.graph == "auto" and args.workload in DEFAULT_BATCH)
+    graphed = None
+    if use_graph:
+        from normalizingflow_amd.graphs import GraphedLogProb
+        graphed = GraphedLogProb(model, x)
 
     def step():
         nonlocal nll
-        lp = model.log_prob(x)
+        lp = graphed() if graphed is not None else model.log_prob(x)
         if use_dist:
             nll = nfdist.nll_allreduce(lp)
         return lp
@@ -433,7 +441,7 @@ def main():
     torch.cuda.synchronize()
     flush_status_checks()
     timer = None
-    if not args.no_timer:
+    if not args.no_timer and graphed is None:  # a replay launches nothing from the host to time
         timer = kernels.TIMER = kernels.KernelTimer()
     if use_dist:
         dist.barrier()
@@ -488,6 +496,7 @@ def main():
                        "scaling": args.scaling,
                        "backend": (args.backend or "nccl") if use_dist else None,
                        "fused_layer_kernel": bool(config.USE_FUSED),
+                       "hip_graph": graphed is not None,
                        "chained_layers": bool(config.USE_FUSED and config.USE_CHAIN),
                        "status_checks": "sync per call" if args.sync_checks else
                        "deferred (no host sync per step; flushed after the timed loop)",

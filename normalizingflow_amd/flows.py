@@ -186,10 +186,19 @@ class _StatusQueue:
 _STATUS_QUEUE = _StatusQueue()
 
 
+# graphs.GraphedLogProb: while a call is being captured into a HIP graph its
+# status words are collected here (no host read can be captured) and checked
+# after each replay instead
+_CAPTURE_SINK = None
+
+
 def check_status(status, n_slots=None, prior=None):
     """Raise the reference's errors for ``status`` per config.STRICT_CHECKS:
     True -> now (one device->host read, which waits for the kernels);
     "deferred" -> at a later call or flush_status_checks(); False -> never."""
+    if _CAPTURE_SINK is not None and status is not None:
+        _CAPTURE_SINK.append((status, n_slots, prior))
+        return
     mode = config.STRICT_CHECKS
     if not mode or status is None:
         return

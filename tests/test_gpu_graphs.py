@@ -1,0 +1,88 @@
+"""GPU: graphs.GraphedLogProb, log_prob (nf/models.py:37-40) of a fixed batch
+shape replayed as one HIP graph.
+
+* bitwise the eager call on the same rows, for the launch-bound c1 shape
+  (2-D two moons, 4-layer RealNVP, H=100: library GEMM conditioners +
+  nfk_affine_coupling) and for a chained NSF_CL model (one fused launch);
+* new rows copied into the static input give the eager result for them;
+* against the CPU oracle at the c1 bench's tolerance;
+* after a weight update, ``recapture()`` follows the new weights;
+* the reference's data-dependent error (no element inside [-B, B],
+  nf/utils.py:63) is raised from the replay's status words.
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+import nf.flows as nff
+import nf.models as nfm
+from normalizingflow_amd import flush_status_checks
+from normalizingflow_amd.graphs import GraphedLogProb
+from oracle import nf_oracle as orc
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _to(model, D, dev):
+    model = model.to(dev)
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(D, device=dev), torch.eye(D, device=dev))
+    return model
+
+
+def test_graphed_c1_bitwise_and_vs_oracle(hip_device):
+    import bench
+    model, sd, _ = bench.build_model("c1", hip_device)
+    g = torch.Generator().manual_seed(0)
+    x = bench.moons(4096, generator=g).to(hip_device)
+    gl = GraphedLogProb(model, x)
+    out = gl().clone()
+    ref = model.log_prob(x)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # new rows through the static input
+    x2 = bench.moons(4096, generator=g).to(hip_device)
+    out2 = gl(x2).clone()
+    assert torch.equal(out2, model.log_prob(x2))
+    flush_status_checks()
+    lp = orc.model_log_prob(bench.specs_for("c1"), sd, x2.cpu())
+    torch.testing.assert_close(out2.cpu(), lp.float(), rtol=1e-5, atol=1e-5)
+
+
+def _nsf_model(dev, n_layers=4):
+    torch.manual_seed(1234)
+    flows = [nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=100, mask=[i % 2]) for i in range(n_layers)]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(64), torch.eye(64))
+    model = nfm.NormalizingFlowModel(prior, flows)
+    return _to(model, 64, dev)
+
+
+def test_graphed_nsf_chain_bitwise_and_recapture(hip_device):
+    model = _nsf_model(hip_device)
+    g = torch.Generator(device=hip_device).manual_seed(3)
+    x = torch.randn(5000, 64, generator=g, device=hip_device)
+    gl = GraphedLogProb(model, x)
+    assert torch.equal(gl().clone(), model.log_prob(x))
+    # a weight update: the graph keeps the captured packs until recaptured
+    with torch.no_grad():
+        model.flows[1].psi.network[2].weight.mul_(1.5)
+    model.invalidate_caches()
+    eager = model.log_prob(x)
+    assert torch.equal(gl.recapture()().clone(), eager)
+    flush_status_checks()
+
+
+def test_graphed_raises_reference_error_after_replay(hip_device):
+    model = _nsf_model(hip_device, n_layers=2)
+    x = torch.randn(256, 64, device=hip_device)
+    gl = GraphedLogProb(model, x)
+    gl()
+    flush_status_checks()
+    bad = torch.full_like(x, 10.0)  # every element outside [-3, 3]: torch.min of an empty tensor
+    with pytest.raises(RuntimeError, match="numel"):  # at the replay (strict) or the flush (deferred)
+        gl(bad)
+        flush_status_checks()
+    with pytest.raises(ValueError):
+        gl(torch.zeros(10, 64, device=hip_device))
