@@ -304,6 +304,24 @@ def _dense(g, like):
     return torch.zeros_like(like) if g is None else g.contiguous()
 
 
+def rnvp_pad(x, h, hp):
+    """[B, 2h] -> [B, 2hp]: the halves at columns [0, h) and [hp, hp + h), zeros
+    elsewhere (x itself when hp == h)."""
+    if hp == h:
+        return x
+    xp = torch.zeros(x.shape[0], 2 * hp, dtype=x.dtype, device=x.device)
+    xp[:, :h] = x[:, :h]
+    xp[:, hp:hp + h] = x[:, h:]
+    return xp
+
+
+def rnvp_unpad(zp, h, hp):
+    """Inverse of rnvp_pad."""
+    if hp == h:
+        return zp
+    return torch.cat([zp[:, :h], zp[:, hp:hp + h]], 1)
+
+
 class RealNVP(_HipFlow):
     """Affine coupling, two halves per layer (flows.py:38-76).
 
@@ -320,6 +338,17 @@ class RealNVP(_HipFlow):
         self.s2 = base_network(dim // 2, dim // 2, hidden_dim)
         self._pack_cache = None
 
+    def _fused_half(self, hidden):
+        """Half-dimension the fused kernel runs this layer at: dim // 2 when the
+        kernel takes it, else the next multiple of 16 it takes (the halves
+        zero-padded: padded inputs meet zero weight columns and the padded s, t
+        outputs are exactly 0, so z and log|det| are unchanged), else None."""
+        h = self.dim // 2
+        if K_.fused_realnvp_supported(h, hidden):
+            return h
+        hp = (h + 15) // 16 * 16
+        return hp if K_.fused_realnvp_supported(hp, hidden) else None
+
     def _fused_pack(self, device):
         """Weights of the four conditioners re-packed for nfk_fused_realnvp;
         rebuilt when any weight changes (None when the fused kernel does not apply)."""
@@ -328,7 +357,10 @@ class RealNVP(_HipFlow):
             return None
         h = self.dim // 2
         hidden = self.s1.network[0].out_features
-        if any(n.network[0].out_features != hidden for n in nets) or not K_.fused_realnvp_supported(h, hidden):
+        if any(n.network[0].out_features != hidden for n in nets):
+            return None
+        hp = self._fused_half(hidden)
+        if hp is None or torch.device(device).type != "cuda":
             return None
         params = [t for n in nets for i in (0, 2, 4) for t in (n.network[i].weight, n.network[i].bias)]
         if any(p.device != device or p.dtype != torch.float32 for p in params):
@@ -336,18 +368,31 @@ class RealNVP(_HipFlow):
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._pack_cache is not None and self._pack_cache[0] == key:
             return self._pack_cache[1]
-        pack = K_.fused_realnvp_pack(params, h, hidden)
-        self._pack_cache = (key, pack, hidden)
+        if hp != h:
+            # zero-padded first-layer input columns, last-layer output rows and biases
+            padded = []
+            for j, t in enumerate(params):
+                t = t.detach()
+                if j % 6 == 0:    # W0 [H, h]
+                    t = torch.nn.functional.pad(t, (0, hp - h))
+                elif j % 6 == 4:  # W4 [h, H]
+                    t = torch.nn.functional.pad(t, (0, 0, 0, hp - h))
+                elif j % 6 == 5:  # b4 [h]
+                    t = torch.nn.functional.pad(t, (0, hp - h))
+                padded.append(t)
+            params = padded
+        pack = K_.fused_realnvp_pack(params, hp, hidden)
+        self._pack_cache = (key, pack, hidden, hp)
         return pack
 
     def _chain_shape(self, device):
-        """("rnvp", half_dim, hidden) when this layer runs as the fused kernel and
-        the chain form applies (so it may join an nfk_fused_realnvp_chain launch
-        with layers of the same shape), else None."""
+        """("rnvp", kernel half_dim, hidden, half_dim) when this layer runs as the
+        fused kernel and the chain form applies (so it may join an
+        nfk_fused_realnvp_chain launch with layers of the same shape), else None."""
         if self.dim % 2 or self._fused_pack(device) is None:
             return None
-        h, hidden = self.dim // 2, self._pack_cache[2]
-        return ("rnvp", h, hidden) if K_.fused_realnvp_chain_max(h, hidden) > 0 else None
+        hidden, hp = self._pack_cache[2], self._pack_cache[3]
+        return ("rnvp", hp, hidden, self.dim // 2) if K_.fused_realnvp_chain_max(hp, hidden) > 0 else None
 
     def _run(self, x, inverse, logdet, mode, status):
         h = self.dim // 2
@@ -355,12 +400,14 @@ class RealNVP(_HipFlow):
             # the reference fails the same way (shape broadcast in flows.py:56)
             raise RuntimeError("RealNVP needs an even feature dimension equal to dim=%d (got %d)"
                                % (self.dim, x.shape[1]))
-        z = torch.empty_like(x, memory_format=torch.contiguous_format)
         pack = self._fused_pack(x.device)
         if pack is not None:
-            K_.fused_realnvp(x, pack, h, self._pack_cache[2], z, logdet=logdet, logdet_mode=mode,
-                             inverse=inverse)
-            return z
+            hidden, hp = self._pack_cache[2], self._pack_cache[3]
+            xk = rnvp_pad(x, h, hp)
+            zk = torch.empty_like(xk, memory_format=torch.contiguous_format)
+            K_.fused_realnvp(xk, pack, hp, hidden, zk, logdet=logdet, logdet_mode=mode, inverse=inverse)
+            return rnvp_unpad(zk, h, hp)
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
         lo, up = x[:, :h], x[:, h:]
         zlo, zup = z[:, :h], z[:, h:]
         m2 = K_.MODE_ACC if mode != K_.MODE_NONE else K_.MODE_NONE

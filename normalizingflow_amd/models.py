@@ -15,12 +15,15 @@ nfk_normal_logprob epilogue; any other prior object is called as is.
 """
 from __future__ import annotations
 
+import math
+
 import torch
 import torch.nn as nn
 
 from . import config
 from . import kernels as K_
 from .flows import NSF_CL, RealNVP, _HipFlow, _check_input, _invalidate_after_load, _needs_grad, check_status
+from .flows import rnvp_pad, rnvp_unpad
 
 __all__ = ["NormalizingFlowModel", "NormalizingFlow"]
 
@@ -203,7 +206,9 @@ class NormalizingFlowModel(nn.Module):
         RealNVP layers) that share one fused-kernel shape replaced by (run,
         shape) tuples of at most nfk_fused_nsf_chain_max /
         nfk_fused_realnvp_chain_max layers (inference only; runs of one stay
-        single).  RealNVP shapes are ("rnvp", half_dim, hidden)."""
+        single).  RealNVP shapes are ("rnvp", kernel half_dim, hidden, half_dim):
+        a half-dimension the kernel does not take runs zero-padded to one it
+        does (RealNVP._fused_half)."""
         if grad or not (config.USE_FUSED and config.USE_CHAIN):
             return list(flows)
         out, run, shape = [], [], None
@@ -261,13 +266,16 @@ class NormalizingFlowModel(nn.Module):
         run, shape, iso, wp, cm = plan
         out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
         if self._is_rnvp(shape):
-            _, h, hidden = shape
+            _, hp, hidden, h = shape
             if not self._chain_layout_ok(x, 2 * h):
                 return None
             status = torch.zeros(1, dtype=torch.int32, device=x.device)  # the prior's NaN-z word
-            K_.fused_realnvp_chain(x, wp, len(run), h, hidden, None, logdet=None, logdet_mode=K_.MODE_NONE,
-                                   inverse=False, status=status, log_prob=out, prior_scale=iso[0],
-                                   prior_hld=iso[1])
+            # padded halves: z's padded columns are 0, and the kernel's constant
+            # 2 hp log(2 pi) is brought back to the true 2 h log(2 pi) through hld
+            hld = iso[1] - (hp - h) * math.log(2 * math.pi)
+            K_.fused_realnvp_chain(rnvp_pad(x, h, hp), wp, len(run), hp, hidden, None, logdet=None,
+                                   logdet_mode=K_.MODE_NONE, inverse=False, status=status, log_prob=out,
+                                   prior_scale=iso[0], prior_hld=hld)
             check_status(status, 0, prior=self.prior)
             return out
         n_lo, n_up, hidden, K, B = shape
@@ -308,20 +316,21 @@ class NormalizingFlowModel(nn.Module):
 
     @classmethod
     def _shape_dim(cls, shape):
-        return 2 * shape[1] if cls._is_rnvp(shape) else shape[0] + shape[1]
+        return 2 * shape[3] if cls._is_rnvp(shape) else shape[0] + shape[1]
 
     def _run_chain(self, run, shape, x, inverse, logdet, status):
         if self._is_rnvp(shape):
-            _, h, hidden = shape
+            _, hp, hidden, h = shape
             if not self._chain_layout_ok(x, 2 * h):
                 for flow in run:  # not the chain's layout: one launch per layer
                     x = flow._run(x, inverse, logdet, K_.MODE_ACC, None)
                 return x
             wp, _ = self._chain_args(run, 2 * h, inverse, x)
-            z = torch.empty_like(x, memory_format=torch.contiguous_format)
-            K_.fused_realnvp_chain(x, wp, len(run), h, hidden, z, logdet=logdet, logdet_mode=K_.MODE_ACC,
+            xk = rnvp_pad(x, h, hp)
+            z = torch.empty_like(xk, memory_format=torch.contiguous_format)
+            K_.fused_realnvp_chain(xk, wp, len(run), hp, hidden, z, logdet=logdet, logdet_mode=K_.MODE_ACC,
                                    inverse=inverse)
-            return z
+            return rnvp_unpad(z, h, hp)
         n_lo, n_up, hidden, K, B = shape
         D = n_lo + n_up
         if not self._chain_layout_ok(x, D):

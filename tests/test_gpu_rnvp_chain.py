@@ -121,3 +121,41 @@ def test_rnvp_chain_roundtrip_and_nan(hip_device):
             model.log_prob(xn)
     finally:
         config.STRICT_CHECKS = prev
+
+
+# half-dimensions the kernels do not take run zero-padded to the next multiple
+# of 16 (RealNVP._fused_half): c1's D = 2 (H = 100), D = 6, D = 40 (-> 32)
+PAD_CASES = [(4, 2, 100), (3, 6, 64), (2, 40, 100)]
+
+
+@pytest.mark.parametrize("case", PAD_CASES, ids=lambda c: "L%d_d%d_h%d" % c)
+def test_rnvp_padded_halves_vs_oracle(case, hip_device):
+    n, dim, hidden = case
+    model, sd = _model(n, dim, hidden, hip_device)
+    assert model.flows[0]._chain_shape(hip_device)[1] % 16 == 0
+    x = torch.randn(3000, dim, generator=torch.Generator().manual_seed(9)) * 1.3
+    xd = x.to(hip_device)
+    model.log_prob(xd)  # pack
+    assert _launches(lambda: model.log_prob(xd)) == {"nfk_fused_realnvp_chain": 1}
+    with torch.no_grad():
+        (zc, plc, ldc), (zs, pls, lds) = _both(lambda: model(xd))
+        (lpc,), (lps,) = _both(lambda: (model.log_prob(xd),))
+        (xic, ldic), (xis, ldis) = _both(lambda: model.inverse(xd))
+    for a, b in ((zc, zs), (ldc, lds), (xic, xis), (ldic, ldis)):
+        assert torch.equal(a, b)
+    assert zc.shape == xd.shape and xic.shape == xd.shape
+    specs = orc.realnvp_specs(n, dim)
+    ref = orc.model_log_prob(specs, sd, x)
+    torch.testing.assert_close(lpc.cpu(), ref, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(lps.cpu(), ref, rtol=1e-5, atol=1e-4)
+    xr, ldr = orc.model_inverse(specs, sd, x)
+    torch.testing.assert_close(xic.cpu(), xr, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(ldic.cpu(), ldr, rtol=1e-5, atol=3e-4)
+    # the library-GEMM path (fused kernels off) agrees as well
+    prev = config.USE_FUSED
+    config.USE_FUSED = False
+    try:
+        lpu = model.log_prob(xd)
+    finally:
+        config.USE_FUSED = prev
+    torch.testing.assert_close(lpu.cpu(), ref, rtol=1e-5, atol=1e-4)
