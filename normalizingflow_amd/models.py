@@ -267,8 +267,8 @@ class NormalizingFlowModel(nn.Module):
         out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
         if self._is_rnvp(shape):
             _, hp, hidden, h = shape
-            if not self._chain_layout_ok(x, 2 * h):
-                return None
+            if x.shape[1] != 2 * h or (hp == h and not self._chain_layout_ok(x, 2 * h)):
+                return None  # (a padded copy is laid out for the chain by construction)
             status = torch.zeros(1, dtype=torch.int32, device=x.device)  # the prior's NaN-z word
             # padded halves: z's padded columns are 0, and the kernel's constant
             # 2 hp log(2 pi) is brought back to the true 2 h log(2 pi) through hld
@@ -321,7 +321,7 @@ class NormalizingFlowModel(nn.Module):
     def _run_chain(self, run, shape, x, inverse, logdet, status):
         if self._is_rnvp(shape):
             _, hp, hidden, h = shape
-            if not self._chain_layout_ok(x, 2 * h):
+            if x.shape[1] != 2 * h or (hp == h and not self._chain_layout_ok(x, 2 * h)):
                 for flow in run:  # not the chain's layout: one launch per layer
                     x = flow._run(x, inverse, logdet, K_.MODE_ACC, None)
                 return x
