@@ -31,6 +31,7 @@ differentiable torch restatement (``torch_math``).
 from __future__ import annotations
 
 import collections
+import functools
 
 import math
 import warnings
@@ -304,6 +305,14 @@ def _dense(g, like):
     return torch.zeros_like(like) if g is None else g.contiguous()
 
 
+@functools.lru_cache(maxsize=None)
+def _rnvp_fused_half(h, hidden):
+    if K_.fused_realnvp_supported(h, hidden):
+        return h
+    hp = (h + 15) // 16 * 16
+    return hp if K_.fused_realnvp_supported(hp, hidden) else None
+
+
 def rnvp_pad(x, h, hp):
     """[B, 2h] -> [B, 2hp]: the halves at columns [0, h) and [hp, hp + h), zeros
     elsewhere (x itself when hp == h)."""
@@ -343,11 +352,7 @@ class RealNVP(_HipFlow):
         kernel takes it, else the next multiple of 16 it takes (the halves
         zero-padded: padded inputs meet zero weight columns and the padded s, t
         outputs are exactly 0, so z and log|det| are unchanged), else None."""
-        h = self.dim // 2
-        if K_.fused_realnvp_supported(h, hidden):
-            return h
-        hp = (h + 15) // 16 * 16
-        return hp if K_.fused_realnvp_supported(hp, hidden) else None
+        return _rnvp_fused_half(self.dim // 2, hidden)
 
     def _fused_pack(self, device):
         """Weights of the four conditioners re-packed for nfk_fused_realnvp;
