@@ -32,12 +32,14 @@ from .flows import check_status, flush_status_checks
 
 
 class _Graphed:
-    def __init__(self, fn, example, warmup=2):
-        if not example.is_cuda:
-            raise ValueError("GraphedLogProb needs a HIP tensor (got %s)" % example.device)
+    """A no-argument call ``fn`` on ``device`` captured once and replayed."""
+
+    def __init__(self, fn, device, warmup=2):
+        if torch.device(device).type != "cuda":
+            raise ValueError("graph capture needs a HIP device (got %s)" % device)
         self._fn = fn
+        self._device = torch.device(device)
         self._warmup = warmup
-        self.x = example.detach().clone()
         self.graph = None
         self.out = None
         self._status = []
@@ -47,13 +49,13 @@ class _Graphed:
         """(Re)capture the call: eager warm-up calls on a side stream fill the
         model's weight-pack and plan caches (no allocation or host copy may
         happen under capture), then one call is captured."""
-        dev = self.x.device
+        dev = self._device
         side = torch.cuda.Stream(dev)
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             for _ in range(self._warmup):
-                self._fn(self.x)
+                self._fn()
         cur.wait_stream(side)
         torch.cuda.synchronize(dev)
         flush_status_checks()  # the warm-up's errors surface here, before capture
@@ -62,18 +64,13 @@ class _Graphed:
         prev, _flows._CAPTURE_SINK = _flows._CAPTURE_SINK, sink
         try:
             with torch.cuda.graph(self.graph):
-                self.out = self._fn(self.x)
+                self.out = self._fn()
         finally:
             _flows._CAPTURE_SINK = prev
         self._status = sink
         return self
 
-    def __call__(self, x=None):
-        if x is not None:
-            if x.shape != self.x.shape or x.dtype != self.x.dtype:
-                raise ValueError("graphed call captured for %s %s, got %s %s"
-                                 % (tuple(self.x.shape), self.x.dtype, tuple(x.shape), x.dtype))
-            self.x.copy_(x)
+    def replay(self):
         self.graph.replay()
         for status, n, prior in self._status:
             check_status(status, n, prior)
@@ -84,4 +81,26 @@ class GraphedLogProb(_Graphed):
     """``model.log_prob`` on batches of ``example_x``'s shape as one graph replay."""
 
     def __init__(self, model, example_x, warmup=2):
-        super().__init__(model.log_prob, example_x, warmup)
+        self.x = example_x.detach().clone()
+        super().__init__(lambda: model.log_prob(self.x), self.x.device, warmup)
+
+    def __call__(self, x=None):
+        if x is not None:
+            if x.shape != self.x.shape or x.dtype != self.x.dtype:
+                raise ValueError("graphed call captured for %s %s, got %s %s"
+                                 % (tuple(self.x.shape), self.x.dtype, tuple(x.shape), x.dtype))
+            self.x.copy_(x)
+        return self.replay()
+
+
+class GraphedSample(_Graphed):
+    """``model.sample(n)`` as one graph replay: the prior draw (torch's device
+    generator, graph-safe: every replay draws fresh values), the inverse chain
+    and the prior log-density.  Returns the graph's static (x, log_px, z)."""
+
+    def __init__(self, model, n_samples, warmup=2):
+        self.n = int(n_samples)
+        super().__init__(lambda: model.sample(self.n), model.prior.loc.device, warmup)
+
+    def __call__(self):
+        return self.replay()
