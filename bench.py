@@ -253,7 +253,7 @@ def mfma_per_wave_layer(workload):
     HT = 2 * KBH + T1
     per_tile = 3 * KBH + T1
     if kind == "RealNVP":
-        n = kw["dim"] // 2
+        n = (kw["dim"] // 2 + 15) // 16 * 16  # the kernel's half-dimension (c1's D = 2 runs padded to 16)
         NO, KBI = n // 16, (n // 16 + 1) // 2
         return 4 * (KBI * HT * 3 + HT * per_tile + NO * per_tile)
     n_lo, n_up = kw["size"], kw["size"] * (kw["dim"] - 1)

@@ -82,7 +82,10 @@ LAYERS = {
     # 3 coordinates, non-prefix mask: FCNN + nfk_rqs_coupling
     "nsfcl_unfused": (lambda: nff.NSF_CL(size=6, dim=3, K=5, B=3, hidden_dim=24, mask=[1]), 18, True),
     "realnvp_fused": (lambda: nff.RealNVP(64, hidden_dim=100), 64, True),
-    "realnvp_unfused": (lambda: nff.RealNVP(10, hidden_dim=20), 10, True),
+    # half-dimension 5 runs zero-padded to 16 on the fused kernel (RealNVP._fused_half)
+    "realnvp_padded": (lambda: nff.RealNVP(10, hidden_dim=20), 10, True),
+    # H = 140 is past the fused kernels: library GEMM conditioners + nfk_affine_coupling
+    "realnvp_unfused": (lambda: nff.RealNVP(10, hidden_dim=140), 10, True),
     "nsfar": (lambda: nff.NSF_AR(dim=4, K=5, B=3, hidden_dim=16), 4, True),
     "nsfar1": (lambda: nff1.NSF_AR(dim=4, K=5, B=3, hidden_dim=16), 4, True),
     "nsfar1_plain": (lambda: nff1.NSF_AR(dim=3, K=4, B=3, hidden_dim=12, periodic=False), 3, True),
@@ -149,6 +152,7 @@ NATIVE_BWD = {
     "nsfar1": {"nfk_rqs_coupling_bwd", "nfk_trig_features_bwd"},
     "nsfar1_plain": {"nfk_rqs_coupling_bwd"},
     "realnvp_unfused": {"nfk_affine_coupling_bwd"},
+    "realnvp_padded": {"nfk_affine_coupling_bwd"},
     "nsfcl_fused": {"nfk_fused_nsf_vjp"},
     "onebyone": set(),  # library GEMMs (no kernel of ours), but not the recompute
 }
