@@ -159,3 +159,23 @@ def test_rnvp_padded_halves_vs_oracle(case, hip_device):
     finally:
         config.USE_FUSED = prev
     torch.testing.assert_close(lpu.cpu(), ref, rtol=1e-5, atol=1e-4)
+
+
+def test_rnvp_padded_halves_edge_batches(hip_device):
+    """Padded halves (D = 2): an empty batch, one row and a column-strided view
+    give the oracle's values (the reference accepts all three)."""
+    model, sd = _model(4, 2, 100, hip_device)
+    specs = orc.realnvp_specs(4, 2)
+    assert model.log_prob(torch.empty(0, 2, device=hip_device)).shape == (0,)
+    x1 = torch.tensor([[0.3, -1.2]])
+    torch.testing.assert_close(model.log_prob(x1.to(hip_device)).cpu(), orc.model_log_prob(specs, sd, x1),
+                               rtol=1e-5, atol=1e-5)
+    wide = torch.randn(500, 5, generator=torch.Generator().manual_seed(2))
+    xv = wide[:, 1:5:2]  # [500, 2] view with row stride 5 and column stride 2
+    lp = model.log_prob(wide.to(hip_device)[:, 1:5:2])
+    torch.testing.assert_close(lp.cpu(), orc.model_log_prob(specs, sd, xv.contiguous()), rtol=1e-5, atol=1e-5)
+    with torch.no_grad():
+        z, _, ld = model(wide.to(hip_device)[:, 1:5:2])
+    zr, _, ldr = orc.model_forward(specs, sd, xv.contiguous())
+    torch.testing.assert_close(z.cpu(), zr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ld.cpu(), ldr, rtol=1e-5, atol=1e-5)
