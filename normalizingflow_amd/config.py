@@ -25,6 +25,10 @@ USE_FCNN_DH    training: the stock FCNN backward's input-gradient GEMMs (g W,
 USE_FCNN_FWD   training: the stock FCNN's recompute forward (Linear + bias +
                Tanh) on nfk_fcnn_linear, the same kernel in forward form;
                off: library GEMMs (addmm) + tanh.
+USE_WGRAD_MFMA training: the stock FCNN backward's weight-gradient GEMMs (g^T [h | 1],
+               the batch as the reduction) on nfk_wgrad (bf16 three-way split
+               MFMA, deterministic batch slices) where the shape is supported;
+               off: split-K fp32 library GEMMs (fcnn_grad.wgrad).
 SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
                fp16-split products on the fp16 matrix cores (split_gemm.py,
                fp32-accurate) instead of fp32 GEMMs.  Off: torch.mm with
@@ -37,4 +41,5 @@ USE_CHAIN = True
 USE_FUSED_VJP = True
 USE_FCNN_DH = True
 USE_FCNN_FWD = True
+USE_WGRAD_MFMA = True
 SPLIT_GEMM = False

@@ -26,6 +26,7 @@ from . import kernels as K_
 
 _WG_ROWS = 8192   # rows per split-K slice of the weight-gradient GEMMs
 _WG_SLICES = 64   # at most this many slices
+_WG_ROWS_MFMA = 2048  # rows per batch slice of nfk_wgrad
 
 
 def linears(p, pre):
@@ -54,8 +55,13 @@ def forward_saved(p, pre, x):
 
 
 def wgrad(g, h):
-    """g^T h for g [B, M], h [B, N]: split over the batch (see module doc)."""
+    """g^T h for g [B, M], h [B, N]: split over the batch (see module doc); on
+    nfk_wgrad (bf16 three-way split MFMA) where the shape allows
+    (config.USE_WGRAD_MFMA), else split-K fp32 library GEMMs."""
     B = g.shape[0]
+    if config.USE_WGRAD_MFMA and B >= _WG_ROWS and _wgrad_ok(g) and _wgrad_ok(h) \
+            and K_.wgrad_supported(g.shape[1], h.shape[1]):
+        return K_.wgrad(g, h, rows_per_slice=_WG_ROWS_MFMA)
     S = min(_WG_SLICES, B // _WG_ROWS)
     if S <= 1:
         return g.t() @ h
@@ -66,6 +72,11 @@ def wgrad(g, h):
     if S * R < B:
         out += g[S * R:].t() @ h[S * R:]
     return out
+
+
+def _wgrad_ok(a):
+    """a can feed nfk_wgrad: HIP fp32, 2-D, unit column stride."""
+    return a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and (a.shape[1] == 1 or a.stride(1) == 1)
 
 
 def _kernel_ok(a):
