@@ -28,7 +28,9 @@ USE_FCNN_FWD   training: the stock FCNN's recompute forward (Linear + bias +
 USE_WGRAD_MFMA training: the stock FCNN backward's weight-gradient GEMMs (g^T [h | 1],
                the batch as the reduction) on nfk_wgrad (bf16 three-way split
                MFMA, deterministic batch slices) where the shape is supported;
-               off: split-K fp32 library GEMMs (fcnn_grad.wgrad).
+               off (the default): split-K fp32 library GEMMs (fcnn_grad.wgrad).
+               Measured: 1.49 vs 1.70 ms for c3's 736 x 101 product at 2^20
+               rows, but the c3 train step 56.2-56.5 vs 55.5-56.1 ms with it.
 SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
                fp16-split products on the fp16 matrix cores (split_gemm.py,
                fp32-accurate) instead of fp32 GEMMs.  Off: torch.mm with
@@ -41,5 +43,5 @@ USE_CHAIN = True
 USE_FUSED_VJP = True
 USE_FCNN_DH = True
 USE_FCNN_FWD = True
-USE_WGRAD_MFMA = True
+USE_WGRAD_MFMA = False
 SPLIT_GEMM = False

@@ -27,6 +27,7 @@ from . import kernels as K_
 _WG_ROWS = 8192   # rows per split-K slice of the weight-gradient GEMMs
 _WG_SLICES = 64   # at most this many slices
 _WG_ROWS_MFMA = 2048  # rows per batch slice of nfk_wgrad
+_WG_MFMA_MIN_M = 512  # nfk_wgrad for g with at least this many columns
 
 
 def linears(p, pre):
@@ -59,8 +60,11 @@ def wgrad(g, h):
     nfk_wgrad (bf16 three-way split MFMA) where the shape allows
     (config.USE_WGRAD_MFMA), else split-K fp32 library GEMMs."""
     B = g.shape[0]
-    if config.USE_WGRAD_MFMA and B >= _WG_ROWS and _wgrad_ok(g) and _wgrad_ok(h) \
-            and K_.wgrad_supported(g.shape[1], h.shape[1]):
+    # the kernel gathers its operands by 4-byte loads; it beats the library
+    # GEMMs only for wide outputs (c3's 736-column output layer: 1.49 vs
+    # 1.70 ms at 2^20 rows; 0.51 vs 0.27 ms at 100 x 101, tools/ubench_wgrad_mfma.py)
+    if config.USE_WGRAD_MFMA and B >= _WG_ROWS and g.shape[1] >= _WG_MFMA_MIN_M and _wgrad_ok(g) \
+            and _wgrad_ok(h) and K_.wgrad_supported(g.shape[1], h.shape[1]):
         return K_.wgrad(g, h, rows_per_slice=_WG_ROWS_MFMA)
     S = min(_WG_SLICES, B // _WG_ROWS)
     if S <= 1:

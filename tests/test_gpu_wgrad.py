@@ -7,7 +7,8 @@ applications/src/train.py:26) on bf16 three-way split MFMA.
   N and batch (not a multiple of 32 or of the slice), strided rows, and
   gradients of magnitude 1e-30 (bf16 keeps fp32's exponent: no scaling);
 * deterministic: two calls are bitwise equal;
-* fcnn_grad.vjp with the kernel vs the split-K library GEMMs at B = 20,000.
+* fcnn_grad.vjp with the kernel (forced on; config.USE_WGRAD_MFMA is off by
+  default) vs the split-K library GEMMs at B = 20,000.
 """
 import pytest
 import torch
