@@ -9,10 +9,12 @@
 A step = one NormalizingFlowModel.log_prob pass over this rank's rows of
 synthetic x ~ N(0, I), already resident in HBM (c3: 8 NSF_CL RQS coupling
 layers, D=64, K=8, H=100).  Sample sharding, replicated weights:
-  --scaling weak   (default) every rank owns --batch rows (2^20): BASELINE
-                   config c4 (8M rows over 8 GPUs);
+  --scaling weak   (default at N = 1) every rank owns --batch rows (2^20):
+                   BASELINE config c4 (8M rows over 8 GPUs);
   --scaling strong the --global-batch rows (2^20) are split over the ranks
-                   (dist.shard_range): the north star's strong-scaling target.
+                   (dist.shard_range): the north star's strong-scaling target;
+  --scaling both   (default at N > 1) both loops in one invocation: weak is
+                   the line's value, strong is its "strong" sub-object.
 With N > 1 each step ends with the NLL all-reduce of [sum log p, count]
 (RCCL; --backend gloo runs the same path over gloo, e.g. N ranks on one
 device in a test).  Status checks run deferred (config.STRICT_CHECKS =
@@ -163,10 +165,42 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(workload, sd, budget_s=15.0):
-    """Time the CPU oracle on a bounded sample (about budget_s of CPU work):
-    warm-ups that size the sample, then the best of 3 timed runs
-    (BASELINE.md's CPU-baseline plan).  A workload quoted at a small batch
+def host_cores():
+    """CPUs this process may run on (the affinity mask; os.cpu_count() on the
+    GPU box counts the whole machine's, not the job's share)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(workload, sd, budget_s=12.0):
+    """BASELINE.md's CPU-baseline plan: the CPU oracle on all host cores and
+    at the job's thread share (OMP_NUM_THREADS, 16 on the GPU box), each on a
+    bounded sample (about budget_s of CPU work); the reported value is the
+    faster of the two (the better CPU baseline), both are in the record."""
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or torch.get_num_threads()
+    allc = host_cores()
+    prev = torch.get_num_threads()
+    runs = {}
+    try:
+        for n in sorted({share, allc}):
+            torch.set_num_threads(n)
+            runs[n] = _cpu_baseline_at(workload, sd, budget_s)
+    finally:
+        torch.set_num_threads(prev)
+    best = max(runs.values(), key=lambda r: r["value"])
+    out = dict(best)
+    out["by_threads"] = {str(n): {"value": round(r["value"], 1), "runs_s": r["runs_s"]}
+                         for n, r in runs.items()}
+    out["all_host_cores"] = allc
+    out["thread_share"] = share
+    return out
+
+
+def _cpu_baseline_at(workload, sd, budget_s):
+    """The oracle at the current torch thread count: warm-ups that size the
+    sample, then the best of 3 timed runs.  A workload quoted at a small batch
     (c1: 4096 rows) is timed as repeated passes over one batch of that size."""
     from oracle import nf_oracle as orc
     D = WORKLOADS[workload][3]
@@ -321,9 +355,11 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
         bound, t_floor, floors = _floors(f16, f32, B, per, insts, name, workload, n_steps)
         achieved = flops / (mean_ms * 1e-3) / 1e12
         peak = flops / (t_floor * 1e-3) / 1e12
+        alg = (D * 4 + 4) * B if name.endswith("_chain") else (2 * D * 4 + 8) * B  # x (+ z, log|det|) or log p
         return {"kernel": name, "bound": bound, "achieved": round(achieved, 2),
                 "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": traffic, "launches": n_launch, "mean_ms": round(mean_ms, 4),
+                "traffic": traffic, **hbm_fields(traffic, alg, mean_ms),
+                "launches": n_launch, "mean_ms": round(mean_ms, 4),
                 "floor_ms": round(t_floor, 4), "floors": floors,
                 "per_launch": "%d samples x %g layers x %.0f flop (fp32-equivalent)"
                               % (B, per, flops / B / per),
@@ -344,11 +380,26 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
     achieved = byts / (mean_ms * 1e-3) / 1e9
     return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+            **hbm_fields(traffic, byts, mean_ms),
             "launches": n_launch, "mean_ms": round(mean_ms, 4),
             "per_launch": "%d samples x %.0f B" % (B, byts / B)}
 
 
-def load_traffic(kernel, workload):
+def hbm_fields(traffic, alg_bytes, mean_ms):
+    """The launch against the HBM roofline: algorithmic bytes and, when a PMC
+    summary is committed, the measured HBM bytes (traffic), each / the
+    launch time, as GB/s and as a fraction of the 8 TB/s peak."""
+    t = mean_ms * 1e-3
+    out = {"alg_hbm_bytes": int(alg_bytes), "alg_hbm_gbs": round(alg_bytes / t / 1e9, 1),
+           "alg_hbm_frac": round(alg_bytes / t / 1e9 / PEAK_HBM_GBS, 4),
+           "hbm_gbs": None, "hbm_frac": None}
+    if traffic:
+        out["hbm_gbs"] = round(traffic / t / 1e9, 1)
+        out["hbm_frac"] = round(traffic / t / 1e9 / PEAK_HBM_GBS, 4)
+    return out
+
+
+def load_traffic(kernel, workload, batch=None):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
     (profiles/pmc_traffic.json: entries keyed "<workload>:<kernel>", or by the
     kernel alone for the c3 default)."""
@@ -361,7 +412,11 @@ def load_traffic(kernel, workload):
     rec = tab.get("%s:%s" % (workload, kernel))
     if rec is None and workload == "c3":
         rec = tab.get(kernel)
-    return None if rec is None else rec.get("bytes_per_launch")
+    if rec is None or not rec.get("bytes_per_launch"):
+        return None
+    # every entry was measured at 2^20 rows per launch: scaled to this batch
+    scale = 1.0 if batch is None else batch / float(rec.get("batch", 1 << 20))
+    return int(rec["bytes_per_launch"] * scale)
 
 
 def main():
@@ -370,8 +425,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
-                    help="weak: --batch rows per GPU; strong: --global-batch rows split over the GPUs")
+    ap.add_argument("--scaling", default=None, choices=("weak", "strong", "both"),
+                    help="weak: --batch rows per GPU; strong: --global-batch rows split over the GPUs; "
+                         "both (the default for N > 1): weak is the line's value, strong its 'strong' object")
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (weak scaling; default 2^20, c1 4096)")
     ap.add_argument("--global-batch", type=int, default=None,
@@ -412,70 +468,83 @@ def main():
     config.USE_FUSED = not args.unfused
     config.USE_CHAIN = not args.no_chain
     config.STRICT_CHECKS = True if args.sync_checks else "deferred"
+    # N > 1 times both modes by default: weak (the line's value, c4) and strong
+    # (the metric's 1M x 64 split over the ranks, in the line's "strong" object)
+    scaling = args.scaling or ("both" if world > 1 else "weak")
+    modes = ["weak", "strong"] if scaling == "both" else [scaling]
 
     model, sd, _ = build_model(args.workload, device)
-    D = WORKLOADS[args.workload][3]
-    if args.scaling == "strong":
-        lo, hi = nfdist.shard_range(args.global_batch, rank, world)
-        B = hi - lo
-        total = args.global_batch
-    else:
-        B = args.batch
-        total = world * B
-    g = torch.Generator(device=device).manual_seed(rank)
-    x = make_x(args.workload, B, g, device)  # resident in HBM before timing
-
-    nll = None
     use_graph = args.graph == "on" or (args.graph == "auto" and args.workload in DEFAULT_BATCH)
-    graphed = None
-    if use_graph:
-        from normalizingflow_amd.graphs import GraphedLogProb
-        graphed = GraphedLogProb(model, x)
 
-    def step():
-        nonlocal nll
-        lp = graphed() if graphed is not None else model.log_prob(x)
+    def run(mode):
+        """One mode's timed loop: W warm-up steps, then K steps bracketed by a
+        barrier + synchronize, max over ranks."""
+        if mode == "strong":
+            lo, hi = nfdist.shard_range(args.global_batch, rank, world)
+            B, total = hi - lo, args.global_batch
+        else:
+            B, total = args.batch, world * args.batch
+        g = torch.Generator(device=device).manual_seed(rank)
+        x = make_x(args.workload, B, g, device)  # resident in HBM before timing
+        graphed = None
+        if use_graph:
+            from normalizingflow_amd.graphs import GraphedLogProb
+            graphed = GraphedLogProb(model, x)
+        res = {"nll": None}
+
+        def step():
+            lp = graphed() if graphed is not None else model.log_prob(x)
+            if use_dist:
+                res["nll"] = nfdist.nll_allreduce(lp)
+            return lp
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        flush_status_checks()
+        timer = None
+        if not args.no_timer and graphed is None:  # a replay launches nothing from the host to time
+            timer = kernels.TIMER = kernels.KernelTimer()
         if use_dist:
-            nll = nfdist.nll_allreduce(lp)
-        return lp
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            lp = step()
+        torch.cuda.synchronize()
+        if use_dist:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        kernels.TIMER = None
+        flush_status_checks()  # the reference's errors, if any step raised one
+        if use_dist:
+            t = torch.tensor([dt], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        res.update(mode=mode, B=B, total=total, x=x, lp=lp, dt=dt, graphed=graphed is not None,
+                   summary=timer.summary() if timer is not None else {})
+        return res
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    flush_status_checks()
-    timer = None
-    if not args.no_timer and graphed is None:  # a replay launches nothing from the host to time
-        timer = kernels.TIMER = kernels.KernelTimer()
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        lp = step()
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    kernels.TIMER = None
-    flush_status_checks()  # the reference's errors, if any step raised one
-    if use_dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    summary = timer.summary() if timer is not None else {}
-
+    results = [run(m) for m in modes]
     if rank == 0:
-        value = total * args.steps / dt
-        dom = max(summary.items(), key=lambda kv: kv[1][2])[0] if summary else None
-        rl = roofline(args.workload, summary, B, load_traffic(dom, args.workload) if dom else None,
-                      args.steps)
         sd_cpu = {k: v.cpu() for k, v in sd.items()}
         n_par = args.parity_rows if args.parity_rows is not None else \
             (4096 if args.workload == "c5" else 16384)
-        par = None
-        if n_par > 0:
-            n_par = min(n_par, B)
-            par = parity(args.workload, sd_cpu, x[:n_par].cpu(), lp[:n_par].cpu())
+
+        def record(r):
+            value = r["total"] * args.steps / r["dt"]
+            summary = r["summary"]
+            dom = max(summary.items(), key=lambda kv: kv[1][2])[0] if summary else None
+            rl = roofline(args.workload, summary, r["B"],
+                          load_traffic(dom, args.workload, r["B"]) if dom else None, args.steps)
+            par = None
+            if n_par > 0:
+                n = min(n_par, r["B"])
+                par = parity(args.workload, sd_cpu, r["x"][:n].cpu(), r["lp"][:n].cpu())
+            return value, rl, par
+
+        main_r = results[0]
+        value, rl, par = record(main_r)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             cpu = cpu_baseline(args.workload, sd_cpu)
@@ -487,20 +556,20 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "ms_per_step": round(main_r["dt"] / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": args.scaling,
+            "scaling": main_r["mode"],
             "vs_baseline": (round(value / BASELINE_CPU[args.workload], 3)
                             if args.workload in BASELINE_CPU else None),
             "dtype": DTYPE_FUSED if config.USE_FUSED else "fp32",
             "data": ("synthetic two moons (noise 0.05)" if args.workload == "c1" else "synthetic x ~ N(0, I)")
                     + " resident in HBM; random-init weights (seed 1234)",
-            "config": {"workload": args.workload + ": " + desc, "global_batch": total,
-                       "per_gpu_batch": B, "parallelism": "dp%d (sample sharding)" % world,
-                       "scaling": args.scaling,
+            "config": {"workload": args.workload + ": " + desc, "global_batch": main_r["total"],
+                       "per_gpu_batch": main_r["B"], "parallelism": "dp%d (sample sharding)" % world,
+                       "scaling": main_r["mode"],
                        "backend": (args.backend or "nccl") if use_dist else None,
                        "fused_layer_kernel": bool(config.USE_FUSED),
-                       "hip_graph": graphed is not None,
+                       "hip_graph": main_r["graphed"],
                        "chained_layers": bool(config.USE_FUSED and config.USE_CHAIN),
                        "status_checks": "sync per call" if args.sync_checks else
                        "deferred (no host sync per step; flushed after the timed loop)",
@@ -509,9 +578,20 @@ def main():
             "roofline": rl,
             "parity": par,
             "cpu_baseline": cpu,
-            "nll": None if nll is None else float(nll),
-            "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4)} for k, v in summary.items()},
+            "nll": None if main_r["nll"] is None else float(main_r["nll"]),
+            "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4)}
+                        for k, v in main_r["summary"].items()},
         }
+        if len(results) > 1:
+            r = results[1]
+            v2, rl2, par2 = record(r)
+            out["strong"] = {
+                "value": round(v2, 1), "unit": "samples/s", "ms_per_step": round(r["dt"] / args.steps * 1e3, 4),
+                "global_batch": r["total"], "per_gpu_batch": r["B"], "scaling": "strong",
+                "nll": None if r["nll"] is None else float(r["nll"]),
+                "roofline": rl2, "parity": par2,
+                "note": "the metric's 1M x 64 batch split over the ranks (dist.shard_range), timed in the "
+                        "same invocation after the weak loop"}
         print(json.dumps(out), flush=True)
     if use_dist:
         dist.barrier()

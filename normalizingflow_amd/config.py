@@ -31,11 +31,6 @@ USE_WGRAD_MFMA training: the stock FCNN backward's weight-gradient GEMMs (g^T [h
                off (the default): split-K fp32 library GEMMs (fcnn_grad.wgrad).
                Measured: 1.49 vs 1.70 ms for c3's 736 x 101 product at 2^20
                rows, but the c3 train step 56.2-56.5 vs 55.5-56.1 ms with it.
-SPLIT_GEMM     training: the NSF_CL conditioner's recompute-backward GEMMs as
-               fp16-split products on the fp16 matrix cores (split_gemm.py,
-               fp32-accurate) instead of fp32 GEMMs.  Off: torch.mm with
-               out_dtype=float32 measured 3.5x slower than the fp32 GEMMs
-               (c3 train step 468 vs 135 ms at 2^20).
 """
 STRICT_CHECKS = True
 USE_FUSED = True
@@ -44,4 +39,3 @@ USE_FUSED_VJP = True
 USE_FCNN_DH = True
 USE_FCNN_FWD = True
 USE_WGRAD_MFMA = False
-SPLIT_GEMM = False

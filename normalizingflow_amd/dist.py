@@ -11,7 +11,8 @@ The only exchanges are the ones the path really has:
     fp64 squared norm before its elementwise step (``attach_process_group``);
   * training (train.py:22-28 run data-parallel): the parameter gradients,
     averaged by DistributedDataParallel's bucketed all_reduce, overlapped with
-    the backward (``data_parallel``).  The c3 model has 8 x 0.55 M fp32
+    the backward (``data_parallel``), of the per-rank loss ``sharded_nll``
+    (exact for uneven shards).  The c3 model has 8 x 0.55 M fp32
     parameters = 17.6 MB of gradient per step, one or two 25 MB buckets.
 """
 from __future__ import annotations
@@ -23,8 +24,8 @@ import torch.distributed as dist
 
 from .flows import Radial
 
-__all__ = ["shard_range", "shard", "nll_allreduce", "attach_process_group", "init_from_env",
-           "data_parallel"]
+__all__ = ["shard_range", "shard", "nll_allreduce", "sharded_nll", "attach_process_group",
+           "init_from_env", "data_parallel"]
 
 
 def shard_range(n, rank, world):
@@ -51,6 +52,26 @@ def nll_allreduce(log_prob, group=None):
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=group)
     return (-(acc[0] / acc[1])).to(log_prob.dtype)
+
+
+def sharded_nll(log_prob, n_global=None, group=None):
+    """This rank's training loss for ``data_parallel``: -sum(log p) * world / N
+    over its rows, N the global row count (all-reduced from the shards when
+    not given).  DistributedDataParallel averages the gradients over the
+    world, so the averaged gradient is exactly that of the global
+    -mean(log p) (train.py:23-27) for ANY split of the rows -- averaging per
+    rank means (-mean of each shard) is that only when the shards are equal.
+    The mean over ranks of the returned values is the global NLL."""
+    world = 1
+    if dist.is_available() and dist.is_initialized():
+        world = dist.get_world_size(group)
+        if n_global is None:
+            cnt = torch.tensor([float(log_prob.numel())], dtype=torch.float64, device=log_prob.device)
+            dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+            n_global = float(cnt.item())
+    if n_global is None:
+        n_global = log_prob.numel()
+    return -log_prob.sum() * (world / float(n_global))
 
 
 def attach_process_group(model, group=None):
@@ -85,9 +106,9 @@ def init_from_env(backend=None, force=False):
 def data_parallel(model, device=None, bucket_cap_mb=25, **kw):
     """Wrap a model for sample-sharded training: batch-global layers get the
     process group, then DistributedDataParallel averages the gradients across
-    ranks.  Each rank feeds its own rows (``shard``) and minimises the mean
-    NLL of its rows; with equal shards the averaged gradient is the gradient
-    of the global mean NLL (train.py:23-27)."""
+    ranks.  Each rank feeds its own rows (``shard``) and minimises
+    ``sharded_nll`` of its rows, whose averaged gradient is the gradient of
+    the global mean NLL (train.py:23-27) for equal and unequal shards alike."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     attach_process_group(model)
     ids = None

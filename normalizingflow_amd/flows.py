@@ -45,7 +45,6 @@ import torch.nn.init as init
 from . import config
 from . import fcnn_grad
 from . import kernels as K_
-from . import split_gemm
 from . import torch_math
 from ._lib import ST_INSIDE_SEEN, ST_NAN_Z, ST_NEG_DISC
 
@@ -116,6 +115,11 @@ def _check_input(x, what="x"):
     return x
 
 
+def _validates(prior):
+    """True when ``prior`` validates its arguments (torch's support check)."""
+    return prior is not None and bool(getattr(prior, "_validate_args", False))
+
+
 def raise_on_status(status, n_slots=None, prior=None):
     """Reference-compatible errors from the kernels' status words (one sync).
 
@@ -126,8 +130,8 @@ def raise_on_status(status, n_slots=None, prior=None):
     in any word (a NaN in z reached the Normal prior) raises torch's
     ValueError when ``prior`` validates its arguments (MultivariateNormal's
     support check in prior.log_prob, models.py:19), after every layer."""
-    if status is None:
-        return
+    if status is None or (n_slots == 0 and not _validates(prior)):
+        return  # nothing this word set can raise: no device->host read
     st = status.cpu().tolist()
     n = len(st) if n_slots is None else n_slots
     for w in st[:n]:
@@ -137,8 +141,7 @@ def raise_on_status(status, n_slots=None, prior=None):
         if w & ST_NEG_DISC:
             raise AssertionError("negative discriminant in the inverse rational-quadratic spline "
                                  "(nf/utils.py:121)")
-    if prior is not None and getattr(prior, "_validate_args", False) \
-            and any(w & ST_NAN_Z for w in st):
+    if _validates(prior) and any(w & ST_NAN_Z for w in st):
         raise ValueError("Expected value argument to be within the support (IndependentConstraint("
                          "Real(), 1)) of the distribution %s, but found invalid values (NaN in z)"
                          % type(prior).__name__)
@@ -201,11 +204,13 @@ def check_status(status, n_slots=None, prior=None):
         _CAPTURE_SINK.append((status, n_slots, prior))
         return
     mode = config.STRICT_CHECKS
-    if not mode or status is None:
+    if not mode or status is None or (n_slots == 0 and not _validates(prior)):
         return
     if mode == "deferred":
-        _STATUS_QUEUE.poll()
+        # queue this call's words first: an earlier call's error raised by the
+        # poll must not drop them
         _STATUS_QUEUE.push(status, n_slots, prior)
+        _STATUS_QUEUE.poll()
     else:
         raise_on_status(status, n_slots, prior)
 
@@ -635,7 +640,7 @@ class NSF_CL(_HipFlow):
         maps = self._maps(x.device)
         # stock FCNN: recompute and differentiate by hand (fcnn_grad: split-K
         # weight gradients); any other conditioner through autograd
-        manual = _is_stock_fcnn(self.psi) and not config.SPLIT_GEMM and set(names) == set(
+        manual = _is_stock_fcnn(self.psi) and set(names) == set(
             "psi.network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias"))
         vpack = self._vjp_pack(x.device) if manual else None
         if vpack is not None:
@@ -675,10 +680,7 @@ class NSF_CL(_HipFlow):
             with torch.enable_grad():
                 lower = x.detach().index_select(1, maps.lo_in_long).requires_grad_(need[0])
                 pd = {n: t.detach().requires_grad_(r) for n, t, r in zip(names, params, need[1:])}
-                if config.SPLIT_GEMM and _is_stock_fcnn(self.psi):
-                    raw = split_gemm.fcnn(pd, "psi.", lower)  # fp16-split GEMMs (fp32-accurate)
-                else:
-                    raw = torch_math.conditioner(self, pd, "psi", lower)
+                raw = torch_math.conditioner(self, pd, "psi", lower)
         rawc = raw.detach().contiguous()
         gp = torch.empty_like(rawc)
         gx = torch.empty(x.shape, dtype=x.dtype, device=x.device)

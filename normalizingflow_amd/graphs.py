@@ -16,9 +16,14 @@ Contract:
     copies x into the static input (or pass None after writing ``.x``);
   * the returned tensor is the graph's static output, overwritten by the
     next replay (clone it to keep it);
-  * the weights are baked in as the packed buffers of the capture: after a
-    parameter update call ``recapture()`` (the model's caches are keyed on
-    parameter versions, so eager calls are never stale, but a graph is);
+  * the weights are baked in as the packed buffers of the capture: the graph
+    holds strong references to every cache entry the captured call used (the
+    layers' weight packs, the chained-launch pointer tables and maps, the
+    log_prob plan), so an eager call or ``invalidate_caches()`` after a
+    parameter update cannot free memory the graph reads; ``replay()`` compares
+    the parameters' (storage, version) with those of the capture and
+    recaptures when they changed (``recapture()`` does it by hand, e.g. after
+    writes through ``p.data`` that bump no version);
   * the reference's errors (status words of the spline layers and the prior)
     are checked after every replay per ``config.STRICT_CHECKS``, like an
     eager call ("deferred": raised by a later call or flush_status_checks()).
@@ -31,15 +36,40 @@ from . import flows as _flows
 from .flows import check_status, flush_status_checks
 
 
-class _Graphed:
-    """A no-argument call ``fn`` on ``device`` captured once and replayed."""
+_CACHE_ATTRS = ("_pack_cache", "_vjp_cache", "_chain_cache", "_lp_plan_cache")
 
-    def __init__(self, fn, device, warmup=2):
+
+def _cache_refs(model):
+    """Strong references to every parameter-derived cache entry of ``model``
+    (the buffers a captured call's kernels read by raw pointer)."""
+    refs = []
+    for m in model.modules():
+        for name in _CACHE_ATTRS:
+            v = m.__dict__.get(name)
+            if v is None:
+                continue
+            refs.append(tuple(v.values()) if isinstance(v, dict) else v)
+    return refs
+
+
+def _param_key(model):
+    return tuple((p.data_ptr(), p._version) for p in model.parameters())
+
+
+class _Graphed:
+    """A no-argument call ``fn`` on ``device`` captured once and replayed.
+    With ``model`` the capture pins the model's caches and replays recapture
+    when its parameters changed."""
+
+    def __init__(self, fn, device, warmup=2, model=None):
         if torch.device(device).type != "cuda":
             raise ValueError("graph capture needs a HIP device (got %s)" % device)
         self._fn = fn
         self._device = torch.device(device)
         self._warmup = warmup
+        self._model = model
+        self._keep = []
+        self._key = None
         self.graph = None
         self.out = None
         self._status = []
@@ -68,9 +98,19 @@ class _Graphed:
         finally:
             _flows._CAPTURE_SINK = prev
         self._status = sink
+        if self._model is not None:
+            # the capture's packs, pointer tables and plan live as long as the graph
+            self._keep = _cache_refs(self._model)
+            self._key = _param_key(self._model)
         return self
 
+    def stale(self):
+        """True when the model's parameters changed since the capture."""
+        return self._model is not None and _param_key(self._model) != self._key
+
     def replay(self):
+        if self.stale():
+            self.recapture()
         self.graph.replay()
         for status, n, prior in self._status:
             check_status(status, n, prior)
@@ -82,7 +122,7 @@ class GraphedLogProb(_Graphed):
 
     def __init__(self, model, example_x, warmup=2):
         self.x = example_x.detach().clone()
-        super().__init__(lambda: model.log_prob(self.x), self.x.device, warmup)
+        super().__init__(lambda: model.log_prob(self.x), self.x.device, warmup, model=model)
 
     def __call__(self, x=None):
         if x is not None:
@@ -100,7 +140,7 @@ class GraphedSample(_Graphed):
 
     def __init__(self, model, n_samples, warmup=2):
         self.n = int(n_samples)
-        super().__init__(lambda: model.sample(self.n), model.prior.loc.device, warmup)
+        super().__init__(lambda: model.sample(self.n), model.prior.loc.device, warmup, model=model)
 
     def __call__(self):
         return self.replay()

@@ -26,41 +26,69 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("scaling,rows", [("strong", 32768), ("weak", 12288)])
-def test_bench_world2_nll_vs_oracle(hip_device, scaling, rows):
-    sys.path.insert(0, REPO)
+def _nll_ref(hip_device, sizes):
+    """The oracle's -mean(log_prob) over the rows the ranks benched: rank r
+    draws its rows from a device generator seeded by r."""
     import bench
-    from normalizingflow_amd.dist import shard_range
     from oracle import nf_oracle as orc
+    xs = []
+    for rank, n in enumerate(sizes):
+        g = torch.Generator(device=hip_device).manual_seed(rank)
+        xs.append(torch.randn(n, 64, generator=g, device=hip_device).cpu())
+    x = torch.cat(xs)
+    _, sd, _ = bench.build_model("c3", hip_device)
+    ref = orc.model_log_prob(bench.specs_for("c3"), {k: v.cpu() for k, v in sd.items()}, x)
+    return float(-ref.double().mean())
 
-    size_arg = ["--global-batch", str(rows)] if scaling == "strong" else ["--batch", str(rows)]
+
+def _bench_world2(extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--scaling", scaling,
-           *size_arg, "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--parity-rows", "1024"]
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--parity-rows", "1024", *extra]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    line = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_bench_world2_weak_and_strong_nll_vs_oracle(hip_device):
+    """The driver's N > 1 invocation (no --scaling): ONE line with the weak
+    loop (c4: --batch rows per rank) as its value and the strong loop (the
+    metric's global batch split over the ranks) as its "strong" object, each
+    NLL equal to the oracle's over the rows it ran."""
+    sys.path.insert(0, REPO)
+    from normalizingflow_amd.dist import shard_range
+    weak_rows, strong_rows = 12288, 32769  # the strong batch does not divide by 2: shards 16385 / 16384
+    line = _bench_world2(["--batch", str(weak_rows), "--global-batch", str(strong_rows)])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["global_batch"] == 2 * weak_rows and line["config"]["backend"] == "gloo"
+    assert line["value"] > 0 and line["parity"]["pass"]
+    st = line["strong"]
+    assert st["scaling"] == "strong" and st["global_batch"] == strong_rows and st["per_gpu_batch"] == 16385
+    assert st["value"] > 0 and st["ms_per_step"] > 0 and st["parity"]["pass"]
+    ref_w = _nll_ref(hip_device, [weak_rows, weak_rows])
+    assert abs(line["nll"] - ref_w) <= 1e-5 * abs(ref_w), (line["nll"], ref_w)
+    sizes = [hi - lo for lo, hi in (shard_range(strong_rows, r, 2) for r in range(2))]
+    ref_s = _nll_ref(hip_device, sizes)
+    assert abs(st["nll"] - ref_s) <= 1e-5 * abs(ref_s), (st["nll"], ref_s)
+
+
+@pytest.mark.parametrize("scaling,rows", [("strong", 32768), ("weak", 12288)])
+def test_bench_world2_single_mode_nll_vs_oracle(hip_device, scaling, rows):
+    sys.path.insert(0, REPO)
+    from normalizingflow_amd.dist import shard_range
+    size_arg = ["--global-batch", str(rows)] if scaling == "strong" else ["--batch", str(rows)]
+    line = _bench_world2(["--scaling", scaling, *size_arg])
     total = rows if scaling == "strong" else 2 * rows
-    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling and "strong" not in line
     assert line["config"]["global_batch"] == total and line["config"]["backend"] == "gloo"
     assert line["value"] > 0 and line["parity"]["pass"]
-
-    # the same rows: each rank draws its shard from a device generator seeded by its rank
-    xs = []
-    for rank in range(2):
-        n = (lambda lo_hi: lo_hi[1] - lo_hi[0])(shard_range(rows, rank, 2)) if scaling == "strong" else rows
-        g = torch.Generator(device=hip_device).manual_seed(rank)
-        xs.append(torch.randn(n, 64, generator=g, device=hip_device).cpu())
-    x = torch.cat(xs)
-    assert x.shape[0] == total
-    _, sd, _ = bench.build_model("c3", hip_device)
-    ref = orc.model_log_prob(bench.specs_for("c3"), {k: v.cpu() for k, v in sd.items()}, x)
-    nll_ref = float(-ref.double().mean())
-    assert abs(line["nll"] - nll_ref) <= 1e-5 * abs(nll_ref), (line["nll"], nll_ref)
+    sizes = [(hi - lo) if scaling == "strong" else rows for lo, hi in (shard_range(rows, r, 2) for r in range(2))]
+    ref = _nll_ref(hip_device, sizes)
+    assert abs(line["nll"] - ref) <= 1e-5 * abs(ref), (line["nll"], ref)
 
 
 def test_bench_rccl_world1_nll_vs_oracle(hip_device):

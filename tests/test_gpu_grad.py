@@ -336,7 +336,7 @@ def _ddp_worker(rank, world, port, x, q):
         ddp = nfd.data_parallel(model, device=dev)
         xs = nfd.shard(x).to(dev)
         z, plp, ld = ddp(xs)
-        loss = -torch.mean(plp + ld)
+        loss = nfd.sharded_nll(plp + ld)  # exact for the uneven shards of x
         loss.backward()
         # numpy: pickled by value (a torch CPU tensor would be shared through a
         # file descriptor that vanishes when this process exits)
@@ -348,20 +348,24 @@ def _ddp_worker(rank, world, port, x, q):
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-def test_ddp_world2_grads_equal_full_batch():
+@pytest.mark.parametrize("world,rows", [(2, 4096), (3, 4097)])
+def test_ddp_grads_equal_full_batch(world, rows):
+    """DDP over ``world`` ranks (3 ranks: 4097 rows, shards 1366/1366/1365)
+    with dist.sharded_nll: every rank's averaged gradient is the full-batch
+    oracle gradient of -mean(log p)."""
     model = _build_mixed(21)
     specs = [spec_of(f, "flows.%d." % i) for i, f in enumerate(model.flows)]
     ref = {k: v.detach().clone().requires_grad_(True) for k, v in model.named_parameters()}
-    x = torch.randn(4096, 64, generator=torch.Generator().manual_seed(8)) * 0.8
+    x = torch.randn(rows, 64, generator=torch.Generator().manual_seed(8)) * 0.8
     _, plp, ld = orc.model_forward(specs, ref, x)
     (-torch.mean(plp + ld)).backward()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, x, q)) for r in range(2)]
+    ps = [ctx.Process(target=_ddp_worker, args=(r, world, port, x, q)) for r in range(world)]
     for p in ps:
         p.start()
-    out = [q.get(timeout=300) for _ in range(2)]
+    out = [q.get(timeout=300) for _ in range(world)]
     for p in ps:
         p.join(timeout=60)
     for rank, grads in out:
@@ -452,26 +456,6 @@ def test_app_train_steps_reduce_nll(hip_device, tmp_path):
     app.load_checkpoint(other, path)
     with torch.no_grad():
         rel_close(other.log_prob(xs[0]), model.log_prob(xs[0]), 0.0, "reloaded log_prob")
-
-
-def test_split_gemm_linear_vs_fp64():
-    """split_gemm.linear (three fp16 GEMMs, fp32 out) forward and backward vs
-    an fp64 nn.Linear, at the c3 conditioner's output-layer shape."""
-    from normalizingflow_amd import split_gemm as sg
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(4096, 100, generator=g).to(DEV).requires_grad_(True)
-    w = (torch.randn(736, 100, generator=g) * 0.1).to(DEV).requires_grad_(True)
-    b = (torch.randn(736, generator=g) * 0.1).to(DEV).requires_grad_(True)
-    gy = torch.randn(4096, 736, generator=g).to(DEV)
-    y = sg.linear(x, w, b)
-    y.backward(gy)
-    xd, wd, bd = (t.detach().double().requires_grad_(True) for t in (x, w, b))
-    yd = F.linear(xd, wd, bd)
-    yd.backward(gy.double())
-    rel_close(y, yd, 2e-6, "y")
-    rel_close(x.grad, xd.grad, 2e-6, "gx")
-    rel_close(w.grad, wd.grad, 2e-6, "gw")
-    rel_close(b.grad, bd.grad, 2e-6, "gb")
 
 
 @pytest.mark.parametrize("name", ["planar_tanh", "radial", "actnorm", "maf"])

@@ -65,11 +65,52 @@ def test_graphed_nsf_chain_bitwise_and_recapture(hip_device):
     x = torch.randn(5000, 64, generator=g, device=hip_device)
     gl = GraphedLogProb(model, x)
     assert torch.equal(gl().clone(), model.log_prob(x))
-    # a weight update: the graph keeps the captured packs until recaptured
+    # a weight update: recaptured by hand
     with torch.no_grad():
         model.flows[1].psi.network[2].weight.mul_(1.5)
     model.invalidate_caches()
     eager = model.log_prob(x)
+    assert torch.equal(gl.recapture()().clone(), eager)
+    flush_status_checks()
+
+
+def test_graphed_replay_after_update_and_eager_call(hip_device):
+    """a versioned update followed by an eager call (which replaces
+    the pack caches) must not leave the graph reading freed packs: the replay
+    sees the stale parameter key and recaptures."""
+    model = _nsf_model(hip_device)
+    x = torch.randn(3000, 64, generator=torch.Generator(device=hip_device).manual_seed(4), device=hip_device)
+    gl = GraphedLogProb(model, x)
+    before = gl().clone()
+    with torch.no_grad():
+        model.flows[0].psi.network[0].weight.mul_(0.5)  # bumps the version counter
+    eager = model.log_prob(x)                            # new packs replace the cached ones
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    assert gl.stale()
+    after = gl().clone()                                 # no recapture() call: replay recaptures
+    assert torch.equal(after, eager)
+    assert not torch.equal(after, before)
+    flush_status_checks()
+
+
+def test_graphed_keeps_captured_packs_alive(hip_device):
+    """Writes through ``p.data`` bump no version: after invalidate_caches() and
+    an eager call the graph still replays its capture's weights from the packs
+    it holds (not freed allocator memory), until recapture()."""
+    model = _nsf_model(hip_device)
+    x = torch.randn(3000, 64, generator=torch.Generator(device=hip_device).manual_seed(5), device=hip_device)
+    gl = GraphedLogProb(model, x)
+    before = gl().clone()
+    model.flows[0].psi.network[0].weight.data.mul_(0.5)
+    model.invalidate_caches()
+    eager = model.log_prob(x)
+    # churn the allocator: the freed blocks of unpinned packs would be reused here
+    junk = [torch.full((1 << 18,), float("nan"), device=hip_device) for _ in range(64)]
+    torch.cuda.synchronize()
+    assert not gl.stale()
+    assert torch.equal(gl().clone(), before)
+    del junk
     assert torch.equal(gl.recapture()().clone(), eager)
     flush_status_checks()
 

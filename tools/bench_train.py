@@ -67,12 +67,8 @@ def main():
                     help="library GEMMs + tanh_backward for the FCNN input gradients (config.USE_FCNN_DH off)")
     ap.add_argument("--no-wgrad-mfma", action="store_true",
                     help="split-K fp32 library GEMMs for the FCNN weight gradients (config.USE_WGRAD_MFMA off)")
-    ap.add_argument("--split-gemm", action="store_true",
-                    help="fp16-split conditioner GEMMs in the NSF_CL backward (config.SPLIT_GEMM on; "
-                         "default off: hand-written fp32 backward, fcnn_grad)")
     args = ap.parse_args()
     from normalizingflow_amd import config
-    config.SPLIT_GEMM = args.split_gemm
     config.USE_FCNN_DH = not args.no_fcnn_dh
     config.USE_FCNN_FWD = not args.no_fcnn_fwd
     config.USE_WGRAD_MFMA = not args.no_wgrad_mfma
@@ -86,7 +82,7 @@ def main():
         return -torch.mean(plp + ld)
 
     res = {"metric": "samples/sec train step (NLL fwd + bwd + Adam)", "workload": args.workload,
-           "batch": args.batch, "steps": args.steps, "split_gemm": config.SPLIT_GEMM,
+           "batch": args.batch, "steps": args.steps,
            "fcnn_dh": config.USE_FCNN_DH, "fcnn_fwd": config.USE_FCNN_FWD,
            "wgrad_mfma": config.USE_WGRAD_MFMA}
     t = timed(ours, opt, x, args.steps, args.warmup)
