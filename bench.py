@@ -64,6 +64,11 @@ WORKLOADS = {
     # (RealNVP._fused_half); 4096 rows are launch- and latency-bound
     "c1": ("2-D two moons (noise 0.05, seed 0), 4-layer RealNVP affine coupling (H=100), log_prob",
            "RealNVP", dict(dim=2, hidden_dim=100), 2, 4),
+    # the applications' default flow type (config.py:37) at applications/input/
+    # Gaussian.yaml's shape: 20 particles x 2 dims, nsplines 10, hidden 80,
+    # nlayers 1, B = ncellx * cell_len / 2 = 4 (setup.py:42, 58)
+    "ar": ("40-dim synthetic Gaussian, NSF_AR autoregressive RQS (Gaussian.yaml: K=10, H=80, B=4, "
+           "1 layer), log_prob", "NSF_AR", dict(dim=40, K=10, B=4.0, hidden_dim=80), 40, 1),
 }
 DEFAULT_BATCH = {"c1": 4096}
 # BASELINE.md's published figure for the same metric: c1 is quoted on the
@@ -99,6 +104,7 @@ METRICS = {
     "c2": "samples/sec log_prob (1M×64, 8 RealNVP affine coupling layers)",
     "c5": "samples/sec log_prob (1M×256, 16 RQS coupling layers, H=256, K=16)",
     "c1": "samples/sec log_prob (4096×2 two moons, 4 RealNVP affine coupling layers)",
+    "ar": "samples/sec log_prob (1M×40, 1 NSF_AR autoregressive RQS layer, K=10, H=80)",
 }
 
 
@@ -110,6 +116,7 @@ ARITH = {
     "c2": _SPLIT + _TAIL + " (nfk_fused_rnvp.hip)",
     "c5": _SPLIT + " (nfk_fused_wide.h)",
     "c1": _SPLIT + _TAIL + " (nfk_fused_rnvp.hip; the D = 2 halves zero-padded to the kernel's 16)",
+    "ar": _SPLIT + " (nfk_fused_ar.hip; layer 1 on the fp16-split trig features)",
 }
 # the line's dtype: what the path computes in (fp32 values and outputs; the
 # conditioner's products on the fp16 matrix cores as a two-way split)
@@ -134,6 +141,8 @@ def build_model(workload, device):
     torch.manual_seed(1234)  # weights seed 1234, nn.Linear default init, on CPU
     if kind == "NSF_CL":
         flows = [nff.NSF_CL(mask=[i % 2], **kw) for i in range(L)]
+    elif kind == "NSF_AR":
+        flows = [nff.NSF_AR(**kw) for _ in range(L)]
     else:
         flows = [nff.RealNVP(**kw) for _ in range(L)]
     prior = torch.distributions.MultivariateNormal(torch.zeros(D), torch.eye(D))
@@ -151,6 +160,9 @@ def specs_for(workload):
     desc, kind, kw, D, L = WORKLOADS[workload]
     if kind == "NSF_CL":
         return orc.nsf_cl_specs(L, kw["size"], kw["dim"], kw["K"], kw["B"], [[0], [1]])
+    if kind == "NSF_AR":
+        return [dict(type="NSF_AR", prefix="flows.%d." % i, dim=kw["dim"], K=kw["K"], B=kw["B"])
+                for i in range(L)]
     return orc.realnvp_specs(L, kw["dim"])
 
 
@@ -366,6 +378,8 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
                 "peak_basis": "fp32-equivalent flop per launch / the binding floor (the larger of "
                               "the MFMA floor and the VALU-issue floor, see floors)",
                 "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
+    if name == "nfk_fused_ar":
+        return roofline_ar(kw, B, L * n_steps / n_launch, n_launch, mean_ms, traffic, insts)
     if name == "nfk_rqs_coupling":
         n_up = kw["size"] * (kw["dim"] - 1)
         P = 3 * kw["K"] - 1
@@ -397,6 +411,50 @@ def hbm_fields(traffic, alg_bytes, mean_ms):
         out["hbm_gbs"] = round(traffic / t / 1e9, 1)
         out["hbm_frac"] = round(traffic / t / 1e9 / PEAK_HBM_GBS, 4)
     return out
+
+
+def ar_mfma_per_wave_layer(dim, K, H):
+    """MFMA instructions of one 16-sample wave per NSF_AR layer in
+    nfk_fused_ar's formulation: conditioner i = 1 .. dim-1 runs layer 1 over
+    ceil(2i / 32) k-blocks and HT hidden tiles (3 split products each), layer 2
+    and the output layer (ceil((3K-1) / 16) tiles) over KBH k-blocks (+1 tail
+    MFMA per tile when H = 32 KBH + 1..4)."""
+    kbf, R = divmod(H, 32)
+    T1 = 1 if (0 < R <= 4 and kbf >= 1) else 0
+    KBH = kbf if (R == 0 or T1) else kbf + 1
+    HT, NO = 2 * KBH + T1, (3 * K - 1 + 15) // 16
+    per_tile = 3 * KBH + T1
+    return sum(((2 * i + 31) // 32) * HT * 3 + (HT + NO) * per_tile for i in range(1, dim))
+
+
+def roofline_ar(kw, B, per, n_launch, mean_ms, traffic, insts):
+    """nfk_fused_ar: the reference's FCNN flops of every conditioner
+    (sum_i 2 (2i H + H H + H (3K-1)) per sample) against the binding floor of
+    the kernel's formulation (MFMA; VALU issue when PMC counts are committed)."""
+    dim, K, H = kw["dim"], kw["K"], kw["hidden_dim"]
+    fl = sum(2.0 * (2 * i * H + H * H + H * (3 * K - 1)) for i in range(1, dim))
+    flops = fl * B * per
+    n_mfma = ar_mfma_per_wave_layer(dim, K, H)
+    t_mfma = n_mfma * MFMA_CYC * (B / 16.0) * per / N_SIMD / (CLOCK_GHZ * 1e9) * 1e3
+    floors = {"mfma_ms": round(t_mfma, 4),
+              "mfma_basis": "%d MFMA per 16 samples and layer x %g cyc on 1024 SIMDs at %.1f GHz"
+                            % (n_mfma, MFMA_CYC, CLOCK_GHZ)}
+    bound, t_floor = "mfma", t_mfma
+    if insts:
+        t_valu = valu_floor_ms(insts, (B / insts["batch"]) * (per / insts.get("layers", 1)))
+        floors["valu_issue_ms"] = round(t_valu, 4)
+        if t_valu > t_mfma:
+            bound, t_floor = "valu-issue", t_valu
+    achieved = flops / (mean_ms * 1e-3) / 1e12
+    peak = flops / (t_floor * 1e-3) / 1e12
+    alg = (2 * dim * 4 + 8) * B * per
+    return {"kernel": "nfk_fused_ar", "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+            **hbm_fields(traffic, alg, mean_ms), "launches": n_launch, "mean_ms": round(mean_ms, 4),
+            "floor_ms": round(t_floor, 4), "floors": floors,
+            "per_launch": "%d samples x %g layers x %.0f flop (reference FCNN flops, fp32-equivalent)"
+                          % (B, per, fl),
+            "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
 
 
 def load_traffic(kernel, workload, batch=None):

@@ -200,6 +200,29 @@ int nfk_trig_features(const float* x, int64_t ldx, float* feat, int64_t ldf, int
                       int32_t n, double B, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Fused NSF_AR layer (nfk_fused_ar.hip): replaces NSF_AR.forward / inverse
+ * (nf/flows.py:176-209) -- every coordinate's conditioner (FCNN(2i, 3K-1,
+ * hidden) on the trig features of coordinates < i, flows.py:172-173, 183; the
+ * init_param logits for coordinate 0) and its spline, ONE launch per layer.
+ *   weights: a DEVICE array of (dim - 1) x 6 pointers, per conditioner
+ *     i = 1 .. dim-1 in order {W1 [hidden][2i], b1, W2 [hidden][hidden], b2,
+ *     W3 [3K-1][hidden], b3} (nn.Linear weight/bias, contiguous fp32);
+ *   pack: nfk_fused_ar_pack_elems() floats, written by nfk_fused_ar_pack();
+ *   x: the layer input [batch, dim] (forward: x, inverse: z); out: the output;
+ *   logdet: mode 0 none, 1 write, 2 accumulate (the layer's sum over columns
+ *     in column order); status: dim words (column i's reference errors: bit
+ *     NFK_ST_INSIDE_SEEN when an element is inside [-B, B], NFK_ST_NEG_DISC).
+ * Supported shapes: nfk_fused_ar_supported() != 0.
+ * ------------------------------------------------------------------------- */
+int nfk_fused_ar_supported(int32_t dim, int32_t hidden, int32_t K);
+int64_t nfk_fused_ar_pack_elems(int32_t dim, int32_t hidden, int32_t K);
+int nfk_fused_ar_pack(const float* const* weights, const float* init_param, int32_t dim, int32_t hidden,
+                      int32_t K, float* pack, nfk_stream_t stream);
+int nfk_fused_ar(const float* x, int64_t ldx, const float* pack, int32_t dim, int32_t hidden, int32_t K,
+                 double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,
+                 int64_t batch, int32_t inverse, int32_t* status, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Fused NSF coupling layer: conditioner MLP (FCNN, flows.py:20-35) on MFMA
  * (fp16 two-way split with power-of-two pre-scaling, fp32 accumulation) +
  * spline epilogue, one launch per layer; the [batch, n_up, 3K-1] conditioner

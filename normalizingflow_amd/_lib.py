@@ -61,6 +61,13 @@ SIGNATURES = {
     "nfk_radial_apply": (ctypes.c_int, [P, I64, P, P, P, P, P, I64, P, P, I32, I64, I32, P]),
     "nfk_normal_logprob": (ctypes.c_int, [P, I64, P, P, I64, I32, F32, F32, I32, P, P]),
     "nfk_trig_features": (ctypes.c_int, [P, I64, P, I64, I64, I32, F64, P]),
+    "nfk_fused_ar_supported": (ctypes.c_int, [I32, I32, I32]),
+    "nfk_fused_ar_pack_elems": (ctypes.c_int64, [I32, I32, I32]),
+    "nfk_fused_ar_pack": (ctypes.c_int, [P, P, I32, I32, I32, P, P]),
+    "nfk_fused_ar": (ctypes.c_int, [
+        P, I64, P, I32, I32, I32,       # x, ldx, pack, dim, hidden, K
+        F64, P, I64, P, I32,            # tail_bound, out, ldo, logdet, logdet_mode
+        I64, I32, P, P]),               # batch, inverse, status, stream
     "nfk_fused_nsf_supported": (ctypes.c_int, [I32, I32, I32, I32]),
     "nfk_fused_nsf_pack_elems": (ctypes.c_int64, [I32, I32, I32, I32]),
     "nfk_fused_nsf_pack": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P, P]),

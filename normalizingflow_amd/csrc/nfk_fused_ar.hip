@@ -1,0 +1,585 @@
+// nfk_fused_ar.hip -- one launch per NSF_AR layer (nf/flows.py:152-209).
+//
+// NSF_AR splines coordinate i with the parameters of its own conditioner
+// layers[i-1] (FCNN(2i, 3K-1, H), flows.py:20-35) applied to the trig features
+// [cos(pi v_j / B), sin(pi v_j / B)], j < i (flows.py:172-173), of the
+// layer's INPUT v = x in forward (flows.py:176-189) and of the already
+// inverted OUTPUT v = x in inverse (flows.py:191-209); coordinate 0 uses
+// init_param.  The reference runs dim host iterations of torch ops per layer;
+// the unfused path here ran ~8 launches per coordinate.
+//
+// Work decomposition: a workgroup = kArWaves waves x 16 samples.  The rows
+// stay with the workgroup for the whole layer and the conditioners of the dim
+// coordinates stream through it in order, so the inverse's sequential column
+// loop and the forward share one structure:
+//   * each conditioner is three fp16-split MFMA GEMMs (nfk_fused_impl.h
+//     gemm_h: A = packed weights from LDS, B = activations in registers,
+//     h^T = W act^T, the hidden features permuted so one layer's accumulators
+//     are the next layer's B operands) with tanh between them;
+//   * the layer-1 B operands are the trig features, kept in registers as fp16
+//     hi/lo fragments in a canonical interleaved order (feature 2j = cos of
+//     column j, 2j + 1 = sin), computed once per row in the forward and
+//     appended column by column in the inverse; conditioner i reads the first
+//     ceil(2i / 32) k-blocks of them (its weight columns are permuted to that
+//     order in the pack, the k-block past 2i masked);
+//   * the 3K-1 output logits of conditioner i land in a per-wave LDS slab
+//     [column][sample][param]; the spline (nfk_spline.h nfk_rqs_element_lean,
+//     the unfused path's element math) runs with one lane per (sample,
+//     column): in forward G = 4 coordinates at once (lane group q takes
+//     column i0 + q), in inverse one coordinate (every lane group computes
+//     it; the result feeds the next conditioners' trig features);
+//   * weights stream as uniform sub-records (SB 1-KiB blocks: NS = 2 output
+//     tiles x all k-blocks x {hi, lo}, the tail step's blocks, the record's
+//     bias block) through two LDS slots: the copy of sub-record s + 2 is issued
+//     right after the barrier that ends the GEMM of s (one barrier per
+//     sub-record), so it overlaps the GEMM of s + 1 and every epilogue between.
+// log|det| is summed per sample in column order (flows.py:188, 208) and
+// added to the layer's log|det| buffer like every layer kernel (modes 0/1/2).
+// Status words: one per coordinate (no element inside -> RuntimeError of
+// utils.py:63; negative discriminant -> AssertionError of utils.py:121).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/nfk.h"
+#include "nfk_spline.h"
+
+int nfk_set_error(const char* msg);
+NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, double top,
+                              int tails, double min_w, double min_h, double min_d);
+
+#include "nfk_fused_impl.h"
+
+using namespace nfk_fused;
+
+namespace {
+
+constexpr int kArNS = 2;     // output tiles per sub-record
+constexpr int kArWaves = 8;  // waves per workgroup (two per SIMD), 16 samples each
+constexpr int kArMaxDim = 128;
+
+struct ArDims {
+    int KBH, T1, HT, P, NO, NH, N3, SPC, NTG, KB1M, SB, PS;
+};
+
+__host__ __device__ inline ArDims ar_dims(int hidden, int K, int dim) {
+    ArDims d{};
+    const int kbf = hidden / 32, rem = hidden - 32 * kbf;
+    d.KBH = rem == 0 ? kbf : (rem <= 4 && kbf >= 1 ? kbf : kbf + 1);
+    d.T1 = (rem != 0 && rem <= 4 && kbf >= 1) ? 1 : 0;
+    d.HT = 2 * d.KBH + d.T1;
+    d.P = 3 * K - 1;
+    d.NO = (d.P + 15) / 16;
+    d.NH = (d.HT + kArNS - 1) / kArNS;
+    d.N3 = (d.NO + kArNS - 1) / kArNS;
+    d.SPC = 2 * d.NH + d.N3;
+    d.NTG = d.T1 ? (kArNS + 1) / 2 : 0;
+    d.KB1M = dim > 1 ? (2 * (dim - 1) + 31) / 32 : 1;
+    const int s1 = d.KB1M * kArNS * 2 + 1, s2 = d.KBH * kArNS * 2 + d.NTG + 1;
+    d.SB = s1 > s2 ? s1 : s2;
+    d.PS = 16 * d.NO + 4;  // slab row stride: = 4 mod 8 floats, conflict-free 16-B reads
+    return d;
+}
+__host__ __device__ inline int64_t ar_nsub(const ArDims& d, int dim) { return (int64_t)(dim - 1) * d.SPC; }
+__host__ __device__ inline int64_t ar_pack_floats(const ArDims& d, int dim) { return 256 + ar_nsub(d, dim) * d.SB * 256; }
+
+// columns splined per spline pass: in forward 4 (one per lane group; 2 when
+// the slab row is long, K > 16), in inverse 1
+__host__ __device__ constexpr int ar_group(bool inv, int ps) { return inv ? 1 : (ps <= 52 ? 4 : 2); }
+inline size_t ar_lds_bytes(const ArDims& d, int dim, bool inv) {
+    return (size_t)2 * d.SB * 1024 + (size_t)kArWaves * ar_group(inv, d.PS) * 16 * d.PS * sizeof(float) +
+           (size_t)(dim + 3) / 4 * 16;
+}
+
+// instantiated shapes (KBH, T1, K, KBX): KBX = layer-1 k-block capacity (dim <= 16 KBX + 1)
+#define NFK_AR_SHAPES(X)                                                                        \
+    X(1, 0, 4, 2)   /* golden nsfar_d4_k4 (H = 16) */                                            \
+    X(1, 0, 8, 2)   /* small test shapes (H <= 32) */                                           \
+    X(3, 0, 10, 4)  /* applications/input/Gaussian.yaml: dim 40, K 10, H 80 */                  \
+    X(3, 1, 8, 4)   /* H = 100 (config.py:40), K 8, dim <= 64 */                                 \
+    X(3, 1, 10, 4)  /* H = 100, K 10 */                                                           \
+    X(3, 1, 32, 4)  /* config.py defaults: H = 100, K 32 (nsplines), dim <= 64 */
+
+inline bool ar_instance(const ArDims& d, int K, int* kbx) {
+#define NFK_AR_CHK(h, t, k, x)                                          \
+    if (d.KBH == h && d.T1 == t && K == k && d.KB1M <= x) {             \
+        *kbx = x;                                                        \
+        return true;                                                     \
+    }
+    NFK_AR_SHAPES(NFK_AR_CHK)
+#undef NFK_AR_CHK
+    return false;
+}
+
+inline bool ar_ok(int dim, int hidden, int K) {
+    if (dim < 2 || dim > kArMaxDim || hidden < 1 || hidden > 132 || K < 2) return false;
+    const ArDims d = ar_dims(hidden, K, dim);
+    int kbx;
+    if (!ar_instance(d, K, &kbx)) return false;
+    // both directions fit one workgroup per CU
+    return ar_lds_bytes(d, dim, false) <= (size_t)kLdsBytes && ar_lds_bytes(d, dim, true) <= (size_t)kLdsBytes;
+}
+
+// ---------------------------------------------------------------------------
+// pack: header block (maxima, unscale factors, init_param), then the
+// sub-record stream of conditioners 1 .. dim-1 (layer 1, layer 2, output
+// layer), each sub-record padded to SB blocks.
+struct ArPackArgs {
+    const float* const* w;  // (dim-1) x {W1, b1, W2, b2, W3, b3}
+    const float* init;      // init_param [3K-1]
+    float* out;
+    int dim, H, K;
+    ArDims d;
+};
+
+__global__ __launch_bounds__(256) void k_ar_max(ArPackArgs a) {
+    const int i = 1 + (int)blockIdx.y;  // conditioner
+    const float* const* w = a.w + (int64_t)(i - 1) * 6;
+    const int64_t n1 = (int64_t)a.H * 2 * i, n2 = (int64_t)a.H * a.H, n3 = (int64_t)a.d.P * a.H;
+    float m1 = 0.0f, m2 = 0.0f, m3 = 0.0f;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n1 + n2 + n3;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        if (g < n1)
+            m1 = fmaxf(m1, fabsf(w[0][g]));
+        else if (g < n1 + n2)
+            m2 = fmaxf(m2, fabsf(w[2][g - n1]));
+        else
+            m3 = fmaxf(m3, fabsf(w[4][g - n1 - n2]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+        m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+        m3 = fmaxf(m3, __shfl_xor(m3, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        unsigned int* h = reinterpret_cast<unsigned int*>(a.out);
+        atomicMax(h, __float_as_uint(m1));
+        atomicMax(h + 1, __float_as_uint(m2));
+        atomicMax(h + 2, __float_as_uint(m3));
+    }
+}
+
+__device__ int ar_scale_exp(float maxw) {  // 2^s max|W| in [2^14, 2^15)
+    if (!(maxw > 0.0f) || !(maxw < 3.0e38f)) return 0;
+    int e;
+    frexpf(maxw, &e);
+    return 15 - e;
+}
+
+// Word wl of block blk of a sub-record holding tiles [T0, T0 + NS) of an
+// nt-tile record over a kbn-k-block contraction (val(t, row, k): the
+// unscaled weight of row `row` of tile t at contraction index k, 0 outside),
+// then (t1) its tail block over contraction indices 32 kbn + 0..3 and the
+// record's bias block [tile][row].  Block order and word layout are those
+// gemm_h reads (nfk_fused_impl.h: k-block fragments, tail_word, bias).
+template <class ValF, class BiasF>
+__device__ uint32_t ar_sub_word(int blk, int wl, int kbn, int t1, int nt, int T0, float sc, float bsc, ValF val,
+                                BiasF bias) {
+    const int nf = kbn * kArNS * 2, ntg = t1 ? (kArNS + 1) / 2 : 0;
+    if (blk < nf) {
+        const int part = blk & 1, idx = blk >> 1, kb = idx / kArNS, t = T0 + (idx - kb * kArNS);
+        if (t >= nt) return 0u;
+        const int lane = wl >> 2, j = 2 * (wl & 3), k0 = 32 * kb + 8 * (lane >> 4) + j;
+        return nfk_f16_part_pair(val(t, lane & 15, k0) * sc, val(t, lane & 15, k0 + 1) * sc, part);
+    }
+    if (blk < nf + ntg) {  // tail: (hi, hi, lo, 0) of tiles 2g, 2g + 1 (tail_word's layout)
+        const int g = T0 / 2 + (blk - nf);
+        const int t = 2 * g + ((wl & 3) >> 1), lane = wl >> 2, j = 2 * (wl & 1), qq = lane >> 4;
+        if (t >= nt || qq == 3) return 0u;
+        const int kb0 = 32 * kbn;
+        return nfk_f16_part_pair(val(t, lane & 15, kb0 + j) * sc, val(t, lane & 15, kb0 + j + 1) * sc,
+                                 qq == 2 ? 1 : 0);
+    }
+    if (blk == nf + ntg) {
+        const int t = wl >> 4, r = wl & 15;
+        return __float_as_uint(t < nt ? bias(t, r) * bsc : 0.0f);
+    }
+    return 0u;  // padding to SB blocks
+}
+
+__global__ __launch_bounds__(256) void k_ar_pack(ArPackArgs a) {
+    const ArDims& d = a.d;
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+    const unsigned int* hdr = reinterpret_cast<const unsigned int*>(a.out);
+    const int s1 = ar_scale_exp(__uint_as_float(hdr[0])), s2 = ar_scale_exp(__uint_as_float(hdr[1])),
+              s3 = ar_scale_exp(__uint_as_float(hdr[2]));
+    const int64_t total = ar_pack_floats(d, a.dim);
+    const int H = a.H, kbh = d.KBH;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        if (g < 256) {
+            if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -(s1 + 14)));
+            else if (g == 4) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
+            else if (g == 5) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
+            else if (g >= 8 && g < 8 + d.P) out[g] = __float_as_uint(a.init[g - 8]);
+            else if (g >= 6) out[g] = 0u;
+            continue;
+        }
+        const int64_t w = g - 256;
+        const int64_t s = w / ((int64_t)d.SB * 256);
+        const int blk = (int)((w >> 8) - s * d.SB), wl = (int)(w & 255);
+        const int i = 1 + (int)(s / d.SPC), u = (int)(s - (int64_t)(i - 1) * d.SPC);
+        const float* const* pw = a.w + (int64_t)(i - 1) * 6;
+        uint32_t v;
+        if (u < d.NH) {  // layer 1: Linear(2i, H) on the canonical trig order (k = 2j + {cos, sin})
+            const float* W1 = pw[0];
+            const float* b1 = pw[1];
+            const int kb1 = (2 * i + 31) / 32;
+            v = ar_sub_word(
+                blk, wl, kb1, 0, d.HT, kArNS * u, ldexpf(1.0f, s1), ldexpf(1.0f, s1 + 14),
+                [&](int t, int r, int k) -> float {
+                    const int f = hid_feature(t, r, kbh);
+                    if (f >= H || k >= 2 * i) return 0.0f;
+                    return W1[(int64_t)f * 2 * i + (k & 1) * i + (k >> 1)];  // cat(cos, sin) columns
+                },
+                [&](int t, int r) -> float {
+                    const int f = hid_feature(t, r, kbh);
+                    return f < H ? b1[f] : 0.0f;
+                });
+        } else if (u < 2 * d.NH) {  // layer 2: Linear(H, H)
+            const float* W2 = pw[2];
+            const float* b2 = pw[3];
+            v = ar_sub_word(
+                blk, wl, kbh, d.T1, d.HT, kArNS * (u - d.NH), ldexpf(1.0f, s2), ldexpf(1.0f, s2 + 14),
+                [&](int t, int r, int k) -> float {
+                    const int f = hid_feature(t, r, kbh);
+                    return (f < H && k < H) ? W2[(int64_t)f * H + k] : 0.0f;
+                },
+                [&](int t, int r) -> float {
+                    const int f = hid_feature(t, r, kbh);
+                    return f < H ? b2[f] : 0.0f;
+                });
+        } else {  // output layer: Linear(H, 3K-1), row 16 t + r = parameter (W, H, D logits in order)
+            const float* W3 = pw[4];
+            const float* b3 = pw[5];
+            const int P = d.P;
+            v = ar_sub_word(
+                blk, wl, kbh, d.T1, d.NO, kArNS * (u - 2 * d.NH), ldexpf(1.0f, s3), ldexpf(1.0f, s3 + 14),
+                [&](int t, int r, int k) -> float {
+                    const int p = 16 * t + r;
+                    return (p < P && k < H) ? W3[(int64_t)p * H + k] : 0.0f;
+                },
+                [&](int t, int r) -> float {
+                    const int p = 16 * t + r;
+                    return p < P ? b3[p] : 0.0f;
+                });
+        }
+        out[g] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+struct ArArgs {
+    const float* x;  // layer input (forward: x; inverse: z)
+    const float* pack;
+    float* out;      // layer output
+    float* logdet;
+    int32_t* status;  // [dim] words or null
+    int64_t ldx, ldo, batch;
+    int32_t dim, mode, sb, kb1m;
+    int64_t nsr;       // sub-records in the stream
+    float pi, bnd;     // trig features: (pi v) / B (nfk_trig_features' operation order)
+    NfkSplineConst c;
+};
+
+// GEMM over the sub-records J, J + 1, ... of an NT-tile record; end() after
+// each ends the sub-record (barrier, next copy) and moves to the next slot.
+template <int KB, bool T1, int NT, int J, class SlotF, class EndF>
+__device__ __forceinline__ void ar_parts(const h8 (&bh)[KB], const h8 (&bl)[KB], h4 bt, int lane,
+                                         f32x4 (&acc)[NT], SlotF slot, EndF end) {
+    constexpr int T0 = J * kArNS;
+    constexpr int N = (NT - T0) < kArNS ? (NT - T0) : kArNS;
+    gemm_h<KB, T1, N, kArNS, T0, NT>(bh, bl, bt, slot(), lane, acc);
+    end();
+    if constexpr (T0 + kArNS < NT) ar_parts<KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end);
+}
+
+// fp16 hi/lo of two trig features (x 2^14, the activations' split scale)
+__device__ __forceinline__ void trig_split(float v, float pi, float bnd, _Float16& ch, _Float16& cl, _Float16& sh,
+                                           _Float16& sl) {
+    const float arg = (pi * v) / bnd;
+    const float c = cosf(arg) * kActScale, s = sinf(arg) * kActScale;
+    ch = (_Float16)c;
+    cl = (_Float16)(c - (float)ch);
+    sh = (_Float16)s;
+    sl = (_Float16)(s - (float)sh);
+}
+
+template <int KBH, bool T1, int K, int KBX, bool INV>
+__global__ __launch_bounds__(64 * kArWaves, 2) void k_fused_ar(ArArgs a) {
+    constexpr int HT = 2 * KBH + (T1 ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
+    constexpr int NH = (HT + kArNS - 1) / kArNS, N3 = (NO + kArNS - 1) / kArNS, SPC = 2 * NH + N3;
+    constexpr int NTG = T1 ? (kArNS + 1) / 2 : 0;
+    constexpr int PS = 16 * NO + 4, G = ar_group(INV, PS);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4, sl = lane & 15;
+    const int D = a.dim;
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    float4* const slot0 = lds4;
+    float4* const slot1 = lds4 + a.sb * 64;
+    float* const scr = reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + wid * (G * 16 * PS);
+    int* const cst = reinterpret_cast<int*>(reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + kArWaves * G * 16 * PS);
+    const int64_t b0 = ((int64_t)blockIdx.x * kArWaves + wid) * 16;
+    const bool row_ok = b0 + sl < a.batch;
+    const int64_t brow = row_ok ? b0 + sl : a.batch - 1;  // rows past the batch re-read the last one
+
+    // sub-record s into slot s & 1: layer-1 sub-records hold ceil(2i / 32) k-blocks
+    auto stage = [&](int64_t s) {
+        if (s >= a.nsr) return;
+        const int i = 1 + (int)(s / SPC), u = (int)(s - (int64_t)(i - 1) * SPC);
+        const int nblk = u < NH ? ((2 * i + 31) / 32) * kArNS * 2 + 1 : KBH * kArNS * 2 + NTG + 1;
+        stage_record<kArWaves>(a.pack + 256 + s * a.sb * 256, nblk, (s & 1) ? slot1 : slot0, wid, lane);
+    };
+
+    // ---- prologue: status words, the first two sub-records, the trig operands
+    for (int i = threadIdx.x; i < D; i += 64 * kArWaves) cst[i] = 0;
+    const float un1 = a.pack[3], un2 = a.pack[4], un3 = a.pack[5];
+    h8 th[KBX], tl[KBX];  // layer-1 B operands: features 32 kb + 8 q + j of sample sl
+#pragma unroll
+    for (int kb = 0; kb < KBX; ++kb) {
+        th[kb] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+        tl[kb] = th[kb];
+        if constexpr (!INV) {
+            if (kb < a.kb1m) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int col = 16 * kb + 4 * q + t;
+                    const float v = col < D ? a.x[brow * a.ldx + col] : 0.0f;
+                    _Float16 ch, cl, sh, s2;
+                    trig_split(v, a.pi, a.bnd, ch, cl, sh, s2);
+                    th[kb][2 * t] = ch;
+                    th[kb][2 * t + 1] = sh;
+                    tl[kb][2 * t] = cl;
+                    tl[kb][2 * t + 1] = s2;
+                }
+            }
+        }
+    }
+    stage(0);
+    stage(1);
+    dma_barrier();
+
+    int64_t s = 0;  // the sub-record the next GEMM reads
+    auto slot = [&]() -> const float4* { return (s & 1) ? slot1 : slot0; };
+    auto end = [&]() {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stage(s + 2);
+        ++s;
+    };
+    const float c21 = -2.0f * kL2E * un1, c22 = -2.0f * kL2E * un2;
+    float ld_acc = 0.0f;  // lane group 0: this sample's log|det|, summed in column order
+    float xin = 0.0f;     // spline input of this lane's column in the current pass
+    h8 bh[KBH], bl[KBH];
+    h4 btail = h4{0, 0, 0, 0};
+
+    for (int i = 0; i < D; ++i) {
+        const int c = INV ? 0 : (i % G);  // slab of column i
+        if (c == 0) {  // first column of a pass: this lane's spline input, loaded early
+            const int col = INV ? i : i + (q < G ? q : 0);
+            xin = col < D ? a.x[brow * a.ldx + col] : 0.0f;
+        }
+        float* const slab = scr + c * 16 * PS;
+        if (i == 0) {
+            // coordinate 0: init_param (flows.py:178-180), the same logits for every sample
+            for (int e = lane; e < 16 * P; e += 64) {
+                const int r = e / P;
+                slab[r * PS + (e - r * P)] = a.pack[8 + (e - r * P)];
+            }
+        } else {
+            const int kb1 = (2 * i + 31) >> 5;
+            f32x4 h[HT];
+            // layer 1 on the trig operands of columns < i: the k-block past
+            // feature 2i is masked (its weights are zero; the mask keeps a
+            // non-finite later column out, as the reference's x[:, :i] does)
+            auto layer1 = [&](auto kbc) {
+                constexpr int KB = decltype(kbc)::value;
+                h8 mh[KB], ml[KB];
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb) mh[kb] = th[kb], ml[kb] = tl[kb];
+                if constexpr (!INV) {
+                    const int lim = 2 * i - 32 * (KB - 1) - 8 * q;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        mh[KB - 1][j] = j < lim ? mh[KB - 1][j] : (_Float16)0.0f;
+                        ml[KB - 1][j] = j < lim ? ml[KB - 1][j] : (_Float16)0.0f;
+                    }
+                }
+                ar_parts<KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end);
+            };
+            switch (kb1) {
+                case 1: layer1(std::integral_constant<int, 1>{}); break;
+                case 2: if constexpr (KBX >= 2) layer1(std::integral_constant<int, 2>{}); break;
+                case 3: if constexpr (KBX >= 3) layer1(std::integral_constant<int, 3>{}); break;
+                case 4: if constexpr (KBX >= 4) layer1(std::integral_constant<int, 4>{}); break;
+                default: break;
+            }
+            act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
+            {
+                f32x4 h2[HT];
+                ar_parts<KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+                act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
+            }
+            f32x4 o[NO];
+            ar_parts<KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+            // logits (unscaled: the exact power of two) into the slab, [sample][param]
+#pragma unroll
+            for (int t = 0; t < NO; ++t) {
+                const int p = 16 * t + 4 * q;
+                if (p < PS - 3)
+                    *reinterpret_cast<float4*>(slab + sl * PS + p) =
+                        make_float4(o[t][0] * un3, o[t][1] * un3, o[t][2] * un3, o[t][3] * un3);
+            }
+        }
+        if (!(INV || c == G - 1 || i == D - 1)) continue;
+
+        // ---- spline pass: columns i - c .. i (forward: lane group q takes
+        // column i - c + q; inverse: every lane group column i)
+        const int cl = INV ? 0 : (q < G ? q : 0);
+        const int col = INV ? i : i - c + q;
+        const bool act = INV || q <= c;  // (q <= c < G)
+        float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
+        {
+            const float* row = scr + cl * 16 * PS + sl * PS;
+#pragma unroll
+            for (int p = 0; p < K; ++p) wr[p] = row[p];
+#pragma unroll
+            for (int p = 0; p < K; ++p) hr[p] = row[K + p];
+#pragma unroll
+            for (int p = 0; p < K - 1; ++p) dr[p] = row[2 * K + p];
+        }
+        float out, lad;
+        bool inside, nd;
+        nfk_rqs_element_lean<K, INV>(xin, wr, hr, dr, a.c, out, lad, inside, nd);
+        const bool live = act && row_ok;
+        if (live && (!INV || q == 0)) a.out[(b0 + sl) * a.ldo + col] = out;
+        const float lm = act ? lad : 0.0f;
+#pragma unroll
+        for (int g = 0; g < G; ++g) ld_acc = ld_acc + __shfl(lm, sl + 16 * g, 64);
+        // status bits of each column of the pass
+        const uint64_t m_in = __ballot(live && inside), m_nd = __ballot(live && inside && nd);
+        if (lane == 0) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int cg = i - c + g;
+                if (cg > i) break;
+                const int bits = (((m_in >> (16 * g)) & 0xFFFFull) ? NFK_ST_INSIDE_SEEN : 0) |
+                                 (((m_nd >> (16 * g)) & 0xFFFFull) ? NFK_ST_NEG_DISC : 0);
+                if (bits) atomicOr(cst + cg, bits);
+            }
+        }
+        if constexpr (INV) {
+            // the inverted coordinate joins the trig features of the next
+            // conditioners: features 2i (cos) and 2i + 1 (sin)
+            if (i + 1 < D) {
+                _Float16 ch, clo, sh, s2;
+                trig_split(out, a.pi, a.bnd, ch, clo, sh, s2);
+                const int k = 2 * i, kbi = k >> 5, qq = (k >> 3) & 3, j = k & 7;
+#pragma unroll
+                for (int kb = 0; kb < KBX; ++kb)
+#pragma unroll
+                    for (int jj = 0; jj < 8; jj += 2) {
+                        const bool hit = kb == kbi && q == qq && jj == j;
+                        th[kb][jj] = hit ? ch : th[kb][jj];
+                        th[kb][jj + 1] = hit ? sh : th[kb][jj + 1];
+                        tl[kb][jj] = hit ? clo : tl[kb][jj];
+                        tl[kb][jj + 1] = hit ? s2 : tl[kb][jj + 1];
+                    }
+            }
+        }
+    }
+
+    // ---- log|det| of the layer, the status words
+    if (q == 0 && row_ok && a.mode != 0) {
+        float* ld = a.logdet + b0 + sl;
+        *ld = a.mode == 2 ? *ld + ld_acc : ld_acc;
+    }
+    __syncthreads();
+    if (a.status != nullptr) {
+        for (int i = threadIdx.x; i < D; i += 64 * kArWaves) {
+            const int bits = cst[i];
+            if (bits != 0 && (a.status[i] & bits) != bits) atomicOr(a.status + i, bits);
+        }
+    }
+}
+
+template <int KBH, int T1, int K, int KBX>
+int launch_ar(const ArArgs& a, size_t lds, bool inv, hipStream_t st) {
+    const int64_t per = (int64_t)kArWaves * 16;
+    const dim3 g((unsigned)((a.batch + per - 1) / per)), b(64 * kArWaves);
+    if (inv)
+        hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, true>), g, b, lds, st, a);
+    else
+        hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, false>), g, b, lds, st, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+extern "C" int nfk_fused_ar_supported(int32_t dim, int32_t hidden, int32_t K) { return ar_ok(dim, hidden, K) ? 1 : 0; }
+
+extern "C" int64_t nfk_fused_ar_pack_elems(int32_t dim, int32_t hidden, int32_t K) {
+    if (!ar_ok(dim, hidden, K)) return 0;
+    return ar_pack_floats(ar_dims(hidden, K, dim), dim);
+}
+
+extern "C" int nfk_fused_ar_pack(const float* const* weights, const float* init_param, int32_t dim,
+                                 int32_t hidden, int32_t K, float* pack, nfk_stream_t stream) {
+    if (!ar_ok(dim, hidden, K)) return nfk_set_error("nfk_fused_ar_pack: shape not supported");
+    if (!weights || !init_param || !pack) return nfk_set_error("nfk_fused_ar_pack: null pointer");
+    ArPackArgs a{weights, init_param, pack, dim, hidden, K, ar_dims(hidden, K, dim)};
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(pack, 0, 3 * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_ar_max, dim3(16, (unsigned)(dim - 1)), dim3(256), 0, st, a);
+    int64_t g = (ar_pack_floats(a.d, dim) + 255) / 256;
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL(k_ar_pack, dim3((unsigned)g), dim3(256), 0, st, a);
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int nfk_fused_ar(const float* x, int64_t ldx, const float* pack, int32_t dim, int32_t hidden, int32_t K,
+                            double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,
+                            int64_t batch, int32_t inverse, int32_t* status, nfk_stream_t stream) {
+    if (!ar_ok(dim, hidden, K)) return nfk_set_error("nfk_fused_ar: shape not supported");
+    if (batch < 0) return nfk_set_error("nfk_fused_ar: bad batch");
+    if (batch == 0) return 0;
+    if (!x || !pack || !out) return nfk_set_error("nfk_fused_ar: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_ar: null logdet");
+    if (ldx < dim || ldo < dim) return nfk_set_error("nfk_fused_ar: bad leading dimension");
+    const ArDims d = ar_dims(hidden, K, dim);
+    ArArgs a;
+    a.x = x;
+    a.pack = pack;
+    a.out = out;
+    a.logdet = logdet;
+    a.status = status;
+    a.ldx = ldx;
+    a.ldo = ldo;
+    a.batch = batch;
+    a.dim = dim;
+    a.mode = logdet_mode;
+    a.sb = d.SB;
+    a.kb1m = d.KB1M;
+    a.nsr = ar_nsub(d, dim);
+    a.pi = (float)M_PI;  // torch.tensor(np.pi) times an fp32 tensor: an fp32 product
+    a.bnd = (float)tail_bound;
+    // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:186-187)
+    a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+    const bool inv = inverse != 0;
+    const size_t lds = ar_lds_bytes(d, dim, inv);
+    hipStream_t st = (hipStream_t)stream;
+    int kbx = 0;
+    ar_instance(d, K, &kbx);
+#define NFK_AR_LAUNCH(h, t, k, xx) \
+    if (d.KBH == h && d.T1 == t && K == k && kbx == xx) return launch_ar<h, t, k, xx>(a, lds, inv, st);
+    NFK_AR_SHAPES(NFK_AR_LAUNCH)
+#undef NFK_AR_LAUNCH
+    return nfk_set_error("nfk_fused_ar: no kernel instance");
+}

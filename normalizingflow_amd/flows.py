@@ -735,10 +735,33 @@ class NSF_AR(_HipFlow):
             self.layers += [base_network(2 * i, 3 * K - 1, hidden_dim).to(self.device)]
         self.reset_parameters()
         self._cols = {}
+        self._pack_cache = None
 
     @property
     def _n_status(self):
         return self.dim
+
+    def _fused_pack(self, device):
+        """The fused layer kernel's pack (nfk_fused_ar: every conditioner and
+        spline of the layer in one launch), rebuilt when any parameter
+        changes; None when it does not apply (non-stock conditioners, unequal
+        hidden widths, an unsupported shape)."""
+        if not config.USE_FUSED or self.dim < 2 or not all(_is_stock_fcnn(n) for n in self.layers):
+            return None
+        lins = [[n.network[j] for j in (0, 2, 4)] for n in self.layers]
+        hidden = lins[0][0].out_features
+        if any(l[0].out_features != hidden for l in lins) or not K_.fused_ar_supported(self.dim, hidden, self.K):
+            return None
+        params = [self.init_param] + [t for l in lins for m in l for t in (m.weight, m.bias)]
+        if any(p.device != device or p.dtype != torch.float32 for p in params):
+            return None
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._pack_cache is not None and self._pack_cache[0] == key:
+            return self._pack_cache[1]
+        ws = [tuple(t for m in l for t in (m.weight, m.bias)) for l in lins]
+        pack, keep = K_.fused_ar_pack(ws, self.init_param, self.dim, hidden, self.K)
+        self._pack_cache = (key, pack, hidden, keep)
+        return pack
 
     def reset_parameters(self):
         init.uniform_(self.init_param, -1 / 2, 1 / 2)
@@ -759,6 +782,12 @@ class NSF_AR(_HipFlow):
         if x.shape[1] != self.dim:
             raise RuntimeError("NSF_AR(dim=%d) got %d features" % (self.dim, x.shape[1]))
         n = x.shape[0]
+        pack = self._fused_pack(x.device)
+        if pack is not None:
+            z = torch.empty_like(x, memory_format=torch.contiguous_format)
+            K_.fused_ar(x, pack, self.dim, self._pack_cache[2], self.K, float(self.B), z, logdet=logdet,
+                        logdet_mode=mode, inverse=inverse, status=status)
+            return z
         z = torch.zeros_like(x, memory_format=torch.contiguous_format)
         cond = z if inverse else x
         b = float(self.B)

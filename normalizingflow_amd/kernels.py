@@ -484,6 +484,44 @@ def trig_features(x, feat, B):
 
 
 # ---------------------------------------------------------------------------
+def fused_ar_supported(dim, hidden, K):
+    return bool(_lib.load().nfk_fused_ar_supported(dim, hidden, K))
+
+
+def fused_ar_pack(weights, init_param, dim, hidden, K):
+    """The fused NSF_AR pack from the conditioners' Linear parameters:
+    ``weights`` = [(W1, b1, W2, b2, W3, b3) for conditioner 1 .. dim-1].
+    Returns (pack, keep): ``keep`` holds the pointer table and any contiguous
+    copies the pack kernel read (alive until the stream has run it)."""
+    flat = [t.detach() for ws in weights for t in ws]
+    dev = _require_hip(init_param, *flat)
+    flat = [t if t.is_contiguous() and t.dtype == F32 else t.contiguous().to(F32) for t in flat]
+    if len(flat) != 6 * (dim - 1):
+        raise ValueError("fused_ar_pack: need 6 tensors per conditioner 1 .. dim-1")
+    table = torch.tensor([t.data_ptr() for t in flat], dtype=torch.int64, device=dev)
+    init = init_param.detach().to(F32).contiguous()
+    n = int(_lib.load().nfk_fused_ar_pack_elems(dim, hidden, K))
+    if n <= 0:
+        raise ValueError("nfk_fused_ar: shape not supported")
+    pack = torch.empty(n, dtype=F32, device=dev)
+    _lib.call("nfk_fused_ar_pack", table.data_ptr(), init.data_ptr(), dim, hidden, K, pack.data_ptr(),
+              _stream(dev))
+    return pack, (table, init, flat)
+
+
+def fused_ar(x, pack, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, inverse=False, status=None):
+    """One fused NSF_AR layer (include/nfk.h nfk_fused_ar)."""
+    dev = _require_hip(x, pack, out, logdet, status)
+    B = x.shape[0]
+    xp, ldx = _mat(x, "x")
+    op, ldo = _mat(out, "out")
+    if x.shape[1] != dim or out.shape != x.shape:
+        raise ValueError("fused_ar: x and out must be [B, %d]" % dim)
+    _timed("nfk_fused_ar", dev, "nfk_fused_ar", xp, ldx, pack.data_ptr(), dim, hidden, K, float(tail_bound),
+           op, ldo, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0,
+           _vec(status, dim, "status", torch.int32), _stream(dev))
+
+
 def fused_nsf_supported(n_lo, n_up, hidden, K):
     return bool(_lib.load().nfk_fused_nsf_supported(n_lo, n_up, hidden, K))
 

@@ -388,8 +388,22 @@ def main():
                                     for _ in range(4)], dim=2, var=1.0, n=256)
 
 
+def ar_cases():
+    """NSF_AR at the shapes of the fused layer kernel (nfk_fused_ar): the
+    applications' Gaussian.yaml flow (nparticles 20 x dim 2 = 40 coordinates,
+    nsplines 10, hidden 80, B = ncellx * cell_len / 2 = 4, setup.py:42-58) and
+    config.py's defaults (nsplines 32, hidden 100) at 24 coordinates."""
+    g = torch.Generator().manual_seed(31)
+    x40 = torch.randn(96, 40, generator=g) * 1.5
+    case_layer("nsfar_d40_k10_h80", rflows.NSF_AR, dict(dim=40, K=10, B=4.0, hidden_dim=80), x40)
+    x24 = torch.randn(64, 24, generator=g) * 1.2
+    case_layer("nsfar_d24_k32_h100", rflows.NSF_AR, dict(dim=24, K=32, B=3, hidden_dim=100), x24)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["extra"]:
+    if sys.argv[1:] == ["ar"]:
+        ar_cases()
+    elif sys.argv[1:] == ["extra"]:
         extra_cases()
     elif sys.argv[1:] == ["negdisc"]:
         negdisc_cases()
@@ -398,5 +412,6 @@ if __name__ == "__main__":
     else:
         main()
         extra_cases()
+        ar_cases()
         negdisc_cases()
         flows1_cases()

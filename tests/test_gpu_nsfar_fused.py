@@ -1,0 +1,156 @@
+"""GPU: the fused NSF_AR layer kernel (nfk_fused_ar.hip, one launch per layer)
+against the reference goldens, the CPU oracle and the unfused per-column
+path (nf/flows.py:152-209).
+
+Shapes: the reference-generated fixtures nsfar_d4_k4 (H 16),
+nsfar_d40_k10_h80 (applications/input/Gaussian.yaml: 20 particles x 2 dims,
+nsplines 10, hidden 80, B 4) and nsfar_d24_k32_h100 (config.py defaults:
+nsplines 32, hidden 100), plus random ones.  Tolerances: z rtol 1e-5 / atol
+2e-5, log|det| rtol 1e-5 / atol 5e-5 (a sum over dim columns), as in
+test_gpu_parity.py; the inverse conditions on its own outputs, so it is
+compared at 1e-4 absolute where the forward uses 2e-5."""
+import pytest
+import torch
+
+import golden_io as gio
+import nf.flows as nff
+import nf.models as nfm
+from normalizingflow_amd import config, flush_status_checks
+from normalizingflow_amd import kernels as K_
+from oracle import nf_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+Z_RTOL, Z_ATOL = 1e-5, 2e-5
+LD_RTOL, LD_ATOL = 1e-5, 5e-5
+
+
+def close(a, b, rtol, atol):
+    torch.testing.assert_close(a.detach().cpu(), b.detach().cpu(), rtol=rtol, atol=atol)
+
+
+def _sd(layer):
+    return {k: v.detach().cpu() for k, v in layer.state_dict().items()}
+
+
+def _launches(fn):
+    """(result, {kernel: launches}) of fn() with the per-kernel timer on."""
+    K_.TIMER = K_.KernelTimer()
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        summ = K_.TIMER.summary()
+    finally:
+        K_.TIMER = None
+    return out, {k: v[0] for k, v in summ.items()}
+
+
+@pytest.mark.parametrize("name", ["nsfar_d4_k4", "nsfar_d40_k10_h80", "nsfar_d24_k32_h100"])
+def test_fused_ar_vs_reference_golden(name, hip_device):
+    meta, data, sd = gio.load(name)
+    kw = meta["kwargs"]
+    assert K_.fused_ar_supported(kw["dim"], kw["hidden_dim"], kw["K"])
+    layer = gio.load_into(nff.NSF_AR(**kw), sd).to(hip_device)
+    x = data["x"].to(hip_device)
+    with torch.no_grad():
+        (z, ld), n = _launches(lambda: layer(x))
+        assert n == {"nfk_fused_ar": 1}, n  # the whole layer is one launch
+        close(z, data["z"], Z_RTOL, Z_ATOL)
+        close(ld, data["ld"], LD_RTOL, LD_ATOL)
+        xi, ldi = layer.inverse(z)
+        close(xi, data["rt_x"], 1e-5, 1e-4)
+        close(ldi, data["rt_ld"], 1e-5, 1e-4)
+        xa, lda = layer.inverse(x)
+        close(xa, data["inv_x"], 1e-5, 1e-4)
+        close(lda, data["inv_ld"], 1e-5, 1e-4)
+    flush_status_checks()
+
+
+@pytest.mark.parametrize("dim,K,H,B,rows", [(40, 10, 80, 4.0, 3000), (17, 8, 100, 3.0, 1000),
+                                           (64, 10, 100, 3.0, 2049), (2, 4, 16, 3.0, 77),
+                                           (33, 32, 100, 2.5, 640)])
+def test_fused_ar_vs_oracle_and_unfused(dim, K, H, B, rows, hip_device):
+    """Random weights and ragged batches: the fused layer vs the oracle, and
+    the unfused per-column path (library GEMMs + nfk_rqs_coupling) vs the
+    same oracle."""
+    torch.manual_seed(7 + dim)
+    layer = nff.NSF_AR(dim=dim, K=K, B=B, hidden_dim=H)
+    sd = _sd(layer)
+    layer = layer.to(hip_device)
+    x = torch.randn(rows, dim, generator=torch.Generator().manual_seed(dim)) * 1.3
+    with torch.no_grad():
+        z_ref, ld_ref = orc.nsf_ar(x, sd, "", dim, K, B)
+        xi_ref, ldi_ref = orc.nsf_ar(x, sd, "", dim, K, B, inverse=True)
+    xd = x.to(hip_device)
+    with torch.no_grad():
+        assert layer._fused_pack(xd.device) is not None
+        z, ld = layer(xd)
+        xi, ldi = layer.inverse(xd)
+        prev = config.USE_FUSED
+        config.USE_FUSED = False
+        try:
+            layer.invalidate_caches()
+            zu, ldu = layer(xd)
+        finally:
+            config.USE_FUSED = prev
+    close(z, z_ref, Z_RTOL, Z_ATOL)
+    close(ld, ld_ref, LD_RTOL, LD_ATOL)
+    close(zu, z_ref, Z_RTOL, Z_ATOL)
+    close(ldu, ld_ref, LD_RTOL, LD_ATOL)
+    close(xi, xi_ref, 1e-5, 1e-4)
+    close(ldi, ldi_ref, 1e-5, 1e-4)
+    flush_status_checks()
+
+
+def test_fused_ar_round_trip_and_logdet_cancel(hip_device):
+    """inverse(forward(x)) = x and the two log|det| cancel, on 2^16 rows of
+    the Gaussian.yaml shape (size-independent properties)."""
+    torch.manual_seed(3)
+    layer = nff.NSF_AR(dim=40, K=10, B=4.0, hidden_dim=80).to(hip_device)
+    x = torch.randn(1 << 16, 40, device=hip_device) * 1.5
+    with torch.no_grad():
+        z, ld = layer(x)
+        xr, ldr = layer.inverse(z)
+    assert float((xr - x).abs().max()) < 1e-4
+    assert float((ld + ldr).abs().max()) < 1e-3
+    flush_status_checks()
+
+
+def test_fused_ar_model_log_prob_and_sample(hip_device):
+    """A 3-layer NSF_AR model (config.py's nlayers) through the model API:
+    log_prob vs the oracle; sample() draws through the fused inverse and its
+    log_px matches log_prob of the drawn x."""
+    torch.manual_seed(11)
+    flows = [nff.NSF_AR(dim=40, K=10, B=4.0, hidden_dim=80) for _ in range(3)]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(40), torch.eye(40))
+    model = nfm.NormalizingFlowModel(prior, flows)
+    sd = _sd(model)
+    specs = [dict(type="NSF_AR", prefix="flows.%d." % i, dim=40, K=10, B=4.0) for i in range(3)]
+    x = torch.randn(1024, 40, generator=torch.Generator().manual_seed(2))
+    ref = orc.model_log_prob(specs, sd, x)
+    model = model.to(hip_device)
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(40, device=hip_device),
+                                                        torch.eye(40, device=hip_device))
+    (lp, n) = _launches(lambda: model.log_prob(x.to(hip_device)))
+    assert n.get("nfk_fused_ar") == 3, n
+    close(lp, ref, 1e-5, 1e-4)
+    xs, lpx, zs = model.sample(2000)
+    lp2 = model.log_prob(xs)
+    close(lpx, lp2, 1e-5, 2e-3)
+    flush_status_checks()
+
+
+def test_fused_ar_no_element_inside_raises(hip_device):
+    """A column with every element outside [-B, B] raises the reference's
+    RuntimeError (torch.min of an empty tensor, utils.py:63)."""
+    torch.manual_seed(5)
+    layer = nff.NSF_AR(dim=12, K=8, B=3.0, hidden_dim=100).to(hip_device)
+    x = torch.randn(500, 12, device=hip_device)
+    x[:, 7] = 10.0
+    prev = config.STRICT_CHECKS
+    config.STRICT_CHECKS = True
+    try:
+        with torch.no_grad(), pytest.raises(RuntimeError, match="numel"):
+            layer(x)
+    finally:
+        config.STRICT_CHECKS = prev
