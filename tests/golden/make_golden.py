@@ -388,6 +388,94 @@ def main():
                                     for _ in range(4)], dim=2, var=1.0, n=256)
 
 
+def _steep_nsfcl(B, size, K, mask, seed):
+    """An NSF_CL layer whose psi output layer has zero weights and a crafted
+    bias, so every row shares knots that make one bin per upper coordinate as
+    steep as NSF_CL's double softmax allows (width at the 1e-3 floor, height
+    ~1 - K 1e-3 of the range: slope ~990) with the smallest interior knot
+    derivative (softplus(softplus(-30)) + 1e-3 = 0.694) at its top.  Returns
+    (layer, top): top[j] = the fp32 top knot (in y) of coordinate j's steep bin."""
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    layer = rflows.NSF_CL(size=size, dim=2, K=K, B=B, hidden_dim=16, mask=mask)
+    n_up = size
+    bias = torch.zeros(n_up, 3 * K - 1)
+    ks = []
+    for j in range(n_up):
+        k = j % (K - 1)                  # an interior top knot k + 1
+        m = (k + 2 + j // (K - 1)) % K   # the widest-bin of the x knots (never k)
+        m = m if m != k else (k + 1) % K
+        uw = torch.randn(K, generator=g)
+        uw[m] = 40.0
+        uh = torch.randn(K, generator=g)
+        uh[k] = 40.0
+        bias[j] = torch.cat([uw, uh, torch.full((K - 1,), -30.0)])
+        ks.append(k)
+    with torch.no_grad():
+        layer.psi.network[4].weight.zero_()
+        layer.psi.network[4].bias.copy_(bias.reshape(-1))
+    ch = _knot_stack(2 * B * torch.softmax(bias[:, K:2 * K], dim=-1), K, B)
+    top = torch.stack([ch[j, ks[j] + 1] for j in range(n_up)])
+    return layer, top
+
+
+def negdisc_cl_cases():
+    """NSF_CL inputs on the knife edge of utils.py:121's assert.
+    At the top knot y_k+1 of a bin the exact discriminant is (h d_k+1)^2, a
+    fraction (d_k+1 / 2 delta)^2 ~ 1.2e-7 of b^2 at NSF_CL's steepest bins
+    (the double softmax caps delta = h / w near 990, interior derivatives are
+    >= 0.694): one or two fp32 ulps.  The fixture puts every upper coordinate
+    of 1,024 rows 0-5 ulps under such a top knot (8,192 knife-edge elements)
+    and records what the reference does -- its inverse (layer and 2-layer
+    model) and the fp64 truth."""
+    K, B, size = 8, 6.0, 8
+    g = torch.Generator().manual_seed(91)
+    layer, top = _steep_nsfcl(B, size, K, [0], 91)
+    n = 1024
+    x = torch.randn(n, 2 * size, generator=g)
+    ulps = torch.randint(0, 6, (n, size), generator=g)
+    for j in range(size):
+        x[:, 2 * j + 1] = _below(top[j].expand(n).clone(), ulps[:, j] + 1)
+    with torch.no_grad():
+        asserts = _asserts(lambda: layer.inverse(x.clone()))
+        row_asserts = [i for i in range(n) if _asserts(lambda: layer.inverse(x[i:i + 1].clone()))]
+        xi, ldi = (None, None) if asserts else layer.inverse(x.clone())
+        x64, ld64 = _f64(layer).inverse(x.double())
+    arrays = dict(x=x, ulps=ulps, ref_asserts=np.array(asserts), row_asserts=np.array(row_asserts, dtype=np.int64),
+                  inv_x_f64=x64, inv_ld_f64=ld64)
+    if xi is not None:
+        arrays.update(inv_x=xi, inv_ld=ldi)
+    _save("negdisc_nsfcl_edge", dict(kind="negdisc_edge", type="NSF_CL",
+                                     kwargs=dict(size=size, dim=2, K=K, B=B, hidden_dim=16, mask=[0]),
+                                     seed=91), arrays, layer)
+    print("layer: reference asserts on %d of %d knife-edge rows" % (len(row_asserts), n))
+
+    # 2-layer model (a chained launch in inference): the last layer (mask [1],
+    # the first inverted) steep on the knife edge, the first steep as well
+    l0, _ = _steep_nsfcl(B, size, K, [0], 92)
+    l1, top1 = _steep_nsfcl(B, size, K, [1], 93)
+    prior = torch.distributions.MultivariateNormal(torch.zeros(2 * size), torch.eye(2 * size))
+    model = rmodels.NormalizingFlowModel(prior, [l0, l1])
+    z = torch.randn(n, 2 * size, generator=g)
+    ulps1 = torch.randint(0, 6, (n, size), generator=g)
+    for j in range(size):  # mask [1]: the upper coordinate of particle j is column 2 j
+        z[:, 2 * j] = _below(top1[j].expand(n).clone(), ulps1[:, j] + 1)
+    with torch.no_grad():
+        m_asserts = _asserts(lambda: model.inverse(z.clone()))
+        m_rows = [i for i in range(n) if _asserts(lambda: model.inverse(z[i:i + 1].clone()))]
+        xm, ldm = (None, None) if m_asserts else model.inverse(z.clone())
+        xm64, ldm64 = _f64(model).inverse(z.double())
+    arrays = dict(z=z, ulps=ulps1, ref_asserts=np.array(m_asserts), row_asserts=np.array(m_rows, dtype=np.int64),
+                  inv_x_f64=xm64, inv_ld_f64=ldm64)
+    if xm is not None:
+        arrays.update(inv_x=xm, inv_ld=ldm)
+    _save("negdisc_model_edge", dict(kind="negdisc_edge_model", dim=2 * size, var=1.0, seed=92,
+                                     layers=[dict(type="NSF_CL", kwargs=dict(size=size, dim=2, K=K, B=B,
+                                                                              hidden_dim=16, mask=mk))
+                                             for mk in ([0], [1])]), arrays, model)
+    print("model: reference asserts on %d of %d knife-edge rows" % (len(m_rows), n))
+
+
 def ar_cases():
     """NSF_AR at the shapes of the fused layer kernel (nfk_fused_ar): the
     applications' Gaussian.yaml flow (nparticles 20 x dim 2 = 40 coordinates,
@@ -403,6 +491,8 @@ def ar_cases():
 if __name__ == "__main__":
     if sys.argv[1:] == ["ar"]:
         ar_cases()
+    elif sys.argv[1:] == ["negdisc_cl"]:
+        negdisc_cl_cases()
     elif sys.argv[1:] == ["extra"]:
         extra_cases()
     elif sys.argv[1:] == ["negdisc"]:
@@ -413,5 +503,6 @@ if __name__ == "__main__":
         main()
         extra_cases()
         ar_cases()
+        negdisc_cl_cases()
         negdisc_cases()
         flows1_cases()

@@ -131,3 +131,17 @@ def test_nan_conditioner_model_fixture():
         z, l = orc.apply_layer(s, z, sd)
         ld = ld + l
     _close(z, d["z"]); _close(ld, d["ld"], atol=1e-5)
+
+
+def test_knife_edge_fixtures():
+    """negdisc_*_edge: inputs 1-6 ulps under the steepest NSF_CL bins' top
+    knots.  The reference asserted on none of them; the oracle (same torch
+    CPU ops) must not either, and reproduces the reference's inverse."""
+    meta, d, sd = gio.load("negdisc_nsfcl_edge")
+    assert not bool(d["ref_asserts"])
+    xi, ldi = orc.apply_layer(gio.layer_spec(meta), d["x"], sd, inverse=True)
+    _close(xi, d["inv_x"]); _close(ldi, d["inv_ld"], atol=1e-4)
+    meta, d, sd = gio.load("negdisc_model_edge")
+    assert not bool(d["ref_asserts"])
+    xm, ldm = orc.model_inverse(_model_specs(meta), sd, d["z"])
+    _close(xm, d["inv_x"]); _close(ldm, d["inv_ld"], atol=1e-4)
