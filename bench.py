@@ -177,13 +177,47 @@ def _cpu_model():
     return None
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A timestamped progress line on stderr (long GPU-box runs must keep writing)."""
+    print("[bench %7.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
+def cgroup_cpus():
+    """The job's CPU quota in whole CPUs from cgroup v2 cpu.max (v1's
+    cfs_quota / cfs_period), or None when unlimited / unreadable."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+            if parse is not None:
+                q, per = parse(txt)
+                if q == "max":
+                    return None
+                return max(1, int(int(q) // int(per)))
+            q = int(txt)
+            if q <= 0:
+                return None
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                return max(1, q // int(f.read().strip()))
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def host_cores():
-    """CPUs this process may run on (the affinity mask; os.cpu_count() on the
-    GPU box counts the whole machine's, not the job's share)."""
+    """CPUs this job may use: the affinity mask, capped by the cgroup CPU
+    quota (os.cpu_count() on the GPU box counts the whole machine's 256, of
+    which a one-GPU job gets a 16-CPU share: 256 threads on it thrash)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cgroup_cpus()
+    return min(n, q) if q else n
 
 
 def cpu_baseline(workload, sd, budget_s=12.0):
@@ -193,12 +227,23 @@ def cpu_baseline(workload, sd, budget_s=12.0):
     faster of the two (the better CPU baseline), both are in the record."""
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or torch.get_num_threads()
     allc = host_cores()
+    skipped = None
+    settings = {share, allc}
+    if cgroup_cpus() is None and allc > 2 * share:
+        # no readable quota and far more CPUs in the mask than the job's thread
+        # share (the one-GPU box: 256 vs 16): a 256-thread run measured > 170 s
+        # for one 4096-row warm-up there (thrashing), so only the share is timed
+        settings = {share}
+        skipped = "%d threads (affinity mask) not timed: no cgroup quota readable and the job's " \
+                  "share is OMP_NUM_THREADS=%d" % (allc, share)
     prev = torch.get_num_threads()
     runs = {}
     try:
-        for n in sorted({share, allc}):
+        for n in sorted(settings):
             torch.set_num_threads(n)
+            progress("cpu baseline: %d threads" % n)
             runs[n] = _cpu_baseline_at(workload, sd, budget_s)
+            progress("cpu baseline: %d threads -> %.1f samples/s" % (n, runs[n]["value"]))
     finally:
         torch.set_num_threads(prev)
     best = max(runs.values(), key=lambda r: r["value"])
@@ -207,6 +252,9 @@ def cpu_baseline(workload, sd, budget_s=12.0):
                          for n, r in runs.items()}
     out["all_host_cores"] = allc
     out["thread_share"] = share
+    out["cgroup_cpus"] = cgroup_cpus()
+    out["skipped"] = skipped
+    out["affinity_cpus"] = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     return out
 
 
@@ -239,6 +287,7 @@ def _cpu_baseline_at(workload, sd, budget_s):
             for _ in range(reps):
                 orc.model_log_prob(specs, sd, x)
             runs.append(time.perf_counter() - t0)
+            progress("cpu baseline run: %d x %d rows in %.2f s" % (reps, n, runs[-1]))
     dt = min(runs)
     return {"value": n * reps / dt, "unit": "samples/s", "cores": torch.get_num_threads(),
             "kind": "port", "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
@@ -380,7 +429,10 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
                 "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
     if name == "nfk_fused_ar":
         return roofline_ar(kw, B, L * n_steps / n_launch, n_launch, mean_ms, traffic, insts)
-    if name == "nfk_rqs_coupling":
+    if name == "nfk_rqs_coupling" and kind == "NSF_AR":
+        P = 3 * kw["K"] - 1
+        byts = (4 + P * 4 + 4 + 8) * B                            # one column: x, params, z, log|det| RMW
+    elif name == "nfk_rqs_coupling":
         n_up = kw["size"] * (kw["dim"] - 1)
         P = 3 * kw["K"] - 1
         byts = (D * 4 + n_up * P * 4 + D * 4 + 8) * B            # 3,464 B/sample
@@ -556,10 +608,12 @@ def main():
                 res["nll"] = nfdist.nll_allreduce(lp)
             return lp
 
+        progress("%s: %d rows per rank, warm-up" % (mode, B))
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
         flush_status_checks()
+        progress("%s: timed loop" % mode)
         timer = None
         if not args.no_timer and graphed is None:  # a replay launches nothing from the host to time
             timer = kernels.TIMER = kernels.KernelTimer()
@@ -579,6 +633,7 @@ def main():
             t = torch.tensor([dt], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
+        progress("%s: %.4f ms per step" % (mode, dt / args.steps * 1e3))
         res.update(mode=mode, B=B, total=total, x=x, lp=lp, dt=dt, graphed=graphed is not None,
                    summary=timer.summary() if timer is not None else {})
         return res
@@ -598,6 +653,7 @@ def main():
             par = None
             if n_par > 0:
                 n = min(n_par, r["B"])
+                progress("parity: %d rows vs the CPU oracle" % n)
                 par = parity(args.workload, sd_cpu, r["x"][:n].cpu(), r["lp"][:n].cpu())
             return value, rl, par
 

@@ -320,6 +320,7 @@ int64_t pack_floats(int n_lo, int n_up, int H, int K) {
 
 uint32_t* g_trace = nullptr;  // diagnostic timeline buffer (NFK_TRACE builds)
 int g_form = -1;            // nfk_debug_fused_form
+int g_chain_form = -1;      // nfk_debug_chain_form
 
 int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_t st) {
     WideArgs a;
@@ -367,6 +368,15 @@ extern "C" int nfk_debug_trace(void* buf) {
 extern "C" int nfk_debug_fused_form(int form) {
     const int prev = g_form;
     g_form = form < 0 ? -1 : (form ? 1 : 0);
+    return prev;
+}
+
+// Diagnostic: kernel of nfk_fused_nsf_chain: -1 = automatic (NFK_CHAIN2 in the
+// environment), 0 = one 16-sample tile per wave, 1 = two tiles per wave where
+// instanced.  Returns the previous setting.  Not part of include/nfk.h.
+extern "C" int nfk_debug_chain_form(int form) {
+    const int prev = g_chain_form;
+    g_chain_form = form < 0 ? -1 : (form ? 1 : 0);
     return prev;
 }
 
@@ -609,9 +619,19 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
         a.prior_c2pi = (float)((n_lo + n_up) * std::log(2.0 * M_PI));
         a.prior_hld = prior_half_log_det;
     }
-    const size_t lds = lds_bytes_chain(L, nlayers);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
+    // two sample tiles per wave (nfk_fused_chain2.hip) where instanced:
+    // NFK_CHAIN2=0 / nfk_debug_chain_form(0) selects the one-tile kernel
+    static const bool c2_env = [] {
+        const char* e = std::getenv("NFK_CHAIN2");
+        return e != nullptr && e[0] == '1';
+    }();
+    if ((g_chain_form < 0 ? c2_env : g_chain_form == 1) && chain2_ok(L, K, nlayers)) {
+        const int rc = launch_chain2(a, L, K, inv, st);
+        if (rc >= 0) return rc;
+    }
+    const size_t lds = lds_bytes_chain(L, nlayers);
 #define DISPATCH(h, t, k) \
     if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, true, true, st);
 #define DISPATCH_KB(h, t) NFK_FUSED_K(DISPATCH, h, t)

@@ -1404,6 +1404,10 @@ inline bool vjp_ok(int n_lo, int n_up, int H, int K) {
     return inst && 2 * lds_alloc(vjp_lds_bytes(vjp_dims(L.KBH, L.T1, K), n_lo + n_up)) <= (size_t)kLdsBytes;
 }
 
+// the two-tile chain (nfk_fused_chain2.hip): c3-class shapes
+int launch_chain2(const FusedArgs& a, const Layout& L, int K, bool inv, hipStream_t st);
+bool chain2_ok(const Layout& L, int K, int nl);
+
 // hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f16 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132
 #define NFK_FUSED_KB(X) X(1, 0) X(1, 1) X(2, 0) X(2, 1) X(3, 0) X(3, 1) X(4, 0) X(4, 1)

@@ -161,3 +161,33 @@ def test_chain_sample_vs_oracle(hip_device):
     torch.testing.assert_close(log_px.cpu(), lpr, rtol=1e-5, atol=1e-4)
     counts = _count_chain_launches(lambda: model.sample(64))
     assert counts.get("nfk_fused_nsf_chain") == 1 and "nfk_fused_nsf" not in counts
+
+
+def test_chain_max_layers_with_scattered_packs(hip_device):
+    """VERDICT r2 #3 (the reverted spill-removal variant faulted on the chain's
+    sub-record LDS-DMA).  A chain launch at its largest layer count whose
+    layer packs lie in DESCENDING address order, each more than 2^31 bytes
+    from the next (spacer allocations between the pack builds): every DMA
+    source must be formed from that layer's own 64-bit pack pointer (a 32-bit
+    offset from one shared base, as a saddr-form DMA would use, wraps here).
+    Bitwise equal to per-layer launches, and on par with the oracle."""
+    nmax = K_.fused_nsf_chain_max(32, 32, 100, 8)
+    model, sd = _model(nmax, 32, 2, 8, 100, [[0], [1]], hip_device)
+    spacers = []
+    for f in reversed(list(model.flows)):
+        spacers.append(torch.empty(2200 * 1024 * 1024, dtype=torch.uint8, device=hip_device))
+        assert f._fused_pack(hip_device) is not None
+    ptrs = [f._pack_cache[1].data_ptr() for f in model.flows]
+    assert all(a > b + (1 << 31) for a, b in zip(ptrs, ptrs[1:])), "packs not scattered as intended"
+    x = torch.randn(3000, 64, generator=torch.Generator().manual_seed(9)) * 1.2
+    xd = x.to(hip_device)
+    counts = _count_chain_launches(lambda: model.log_prob(xd))
+    assert counts == {"nfk_fused_nsf_chain": 1}, counts
+    with torch.no_grad():
+        (zc, plc, ldc), (zs, pls, lds) = _both(lambda: model(xd))
+        (xic, ldic), (xis, ldis) = _both(lambda: model.inverse(xd))
+    for a, b in ((zc, zs), (ldc, lds), (xic, xis), (ldic, ldis)):
+        assert torch.equal(a, b)
+    specs = orc.nsf_cl_specs(nmax, 32, 2, 8, 3, [[0], [1]])
+    torch.testing.assert_close(model.log_prob(xd).cpu(), orc.model_log_prob(specs, sd, x), rtol=1e-5, atol=1e-4)
+    del spacers

@@ -8,8 +8,8 @@ run() {  # name timeout cmd...
   echo "$n rc=$rc"; tail -4 $O/$n.log
   [ $rc -eq 0 ] || exit $rc
 }
-run ar_tests 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_nsfar_fused.py
-run bench_ar 300 python bench.py --workload ar --steps 10 --warmup 2
+#run ar_tests 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_nsfar_fused.py
+#run bench_ar 300 python bench.py --workload ar --steps 10 --warmup 2
 run bench_ar_unfused 400 python bench.py --workload ar --unfused --steps 2 --warmup 1 --no-cpu-baseline --parity-rows 2048
 run bench_c3 300 python bench.py
 run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
