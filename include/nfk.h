@@ -416,20 +416,6 @@ int nfk_fcnn_dh_pack(const float* W, int32_t P, int32_t H, float* pack, nfk_stre
 int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh,
                 int32_t H, float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate,
                 int64_t batch, nfk_stream_t stream);
-/* ---------------------------------------------------------------------------
- * Weight-gradient GEMMs of the FCNN conditioner's backward (nfk_wgrad.hip;
- * the nn.Linear weight/bias gradients of flows.py:20-35 under train.py:26's
- * loss.backward(), which torch forms as g^T [h | 1]):
- *   partial[s, i, j] = sum over rows b of slice s of g[b, i] h[b, j]
- * g [batch, M] and h [batch, N] row-major with unit column stride; slice s
- * holds rows [s rows_per_slice, (s + 1) rows_per_slice) (rows_per_slice a
- * multiple of 32, nslices slices covering the batch); the caller sums
- * partial [nslices, M, N] over s.  bf16 three-way split on the matrix cores,
- * fp32 accumulation (fp32-level products, no scaling).  M <= 4096, N <= 128.
- * ------------------------------------------------------------------------- */
-int nfk_wgrad_supported(int32_t M, int32_t N);
-int nfk_wgrad(const float* g, int64_t ldg, const float* h, int64_t ldh, int64_t batch, int32_t M, int32_t N,
-              int64_t rows_per_slice, int32_t nslices, float* partial, nfk_stream_t stream);
 /* The same kernel in forward form, for the training recompute of one FCNN
  * Linear (flows.py:26-31, nn.Linear + optional nn.Tanh):
  *   out[b, j] = act(sum_p x[b, p] W[p, j] + bias[j])   act = tanh if tanh_out

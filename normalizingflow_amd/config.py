@@ -25,12 +25,6 @@ USE_FCNN_DH    training: the stock FCNN backward's input-gradient GEMMs (g W,
 USE_FCNN_FWD   training: the stock FCNN's recompute forward (Linear + bias +
                Tanh) on nfk_fcnn_linear, the same kernel in forward form;
                off: library GEMMs (addmm) + tanh.
-USE_WGRAD_MFMA training: the stock FCNN backward's weight-gradient GEMMs (g^T [h | 1],
-               the batch as the reduction) on nfk_wgrad (bf16 three-way split
-               MFMA, deterministic batch slices) where the shape is supported;
-               off (the default): split-K fp32 library GEMMs (fcnn_grad.wgrad).
-               Measured: 1.49 vs 1.70 ms for c3's 736 x 101 product at 2^20
-               rows, but the c3 train step 56.2-56.5 vs 55.5-56.1 ms with it.
 """
 STRICT_CHECKS = True
 USE_FUSED = True
@@ -38,4 +32,3 @@ USE_CHAIN = True
 USE_FUSED_VJP = True
 USE_FCNN_DH = True
 USE_FCNN_FWD = True
-USE_WGRAD_MFMA = False

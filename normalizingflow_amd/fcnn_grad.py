@@ -26,8 +26,6 @@ from . import kernels as K_
 
 _WG_ROWS = 8192   # rows per split-K slice of the weight-gradient GEMMs
 _WG_SLICES = 64   # at most this many slices
-_WG_ROWS_MFMA = 2048  # rows per batch slice of nfk_wgrad
-_WG_MFMA_MIN_M = 512  # nfk_wgrad for g with at least this many columns
 
 
 def linears(p, pre):
@@ -56,16 +54,9 @@ def forward_saved(p, pre, x):
 
 
 def wgrad(g, h):
-    """g^T h for g [B, M], h [B, N]: split over the batch (see module doc); on
-    nfk_wgrad (bf16 three-way split MFMA) where the shape allows
-    (config.USE_WGRAD_MFMA), else split-K fp32 library GEMMs."""
+    """g^T h for g [B, M], h [B, N]: split-K fp32 library GEMMs over batch
+    slices (see module doc), summed in slice order."""
     B = g.shape[0]
-    # the kernel gathers its operands by 4-byte loads; it beats the library
-    # GEMMs only for wide outputs (c3's 736-column output layer: 1.49 vs
-    # 1.70 ms at 2^20 rows; 0.51 vs 0.27 ms at 100 x 101, tools/ubench_wgrad_mfma.py)
-    if config.USE_WGRAD_MFMA and B >= _WG_ROWS and g.shape[1] >= _WG_MFMA_MIN_M and _wgrad_ok(g) \
-            and _wgrad_ok(h) and K_.wgrad_supported(g.shape[1], h.shape[1]):
-        return K_.wgrad(g, h, rows_per_slice=_WG_ROWS_MFMA)
     S = min(_WG_SLICES, B // _WG_ROWS)
     if S <= 1:
         return g.t() @ h
@@ -76,11 +67,6 @@ def wgrad(g, h):
     if S * R < B:
         out += g[S * R:].t() @ h[S * R:]
     return out
-
-
-def _wgrad_ok(a):
-    """a can feed nfk_wgrad: HIP fp32, 2-D, unit column stride."""
-    return a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and (a.shape[1] == 1 or a.stride(1) == 1)
 
 
 def _kernel_ok(a):

@@ -335,29 +335,6 @@ def fcnn_dh(g, pack, W_shape, h, out, *, accumulate=False):
            cso, 1 if accumulate else 0, B, _stream(dev))
 
 
-def wgrad_supported(M, N):
-    return bool(_lib.load().nfk_wgrad_supported(M, N))
-
-
-def wgrad(g, h, rows_per_slice=8192):
-    """g^T h for g [B, M], h [B, N] (nfk_wgrad): bf16 three-way split MFMA over
-    batch slices of rows_per_slice rows, summed here in slice order."""
-    dev = _require_hip(g, h)
-    B, M = g.shape
-    N = h.shape[1]
-    if h.shape[0] != B:
-        raise ValueError("wgrad: g and h must have the same number of rows")
-    gp_, ldg = _mat(g, "g")
-    hp_, ldh = _mat(h, "h")
-    rows = max(32, (int(rows_per_slice) + 31) // 32 * 32)
-    ns = max(1, (B + rows - 1) // rows)
-    part = torch.empty(ns, M, N, dtype=F32, device=dev)
-    if B == 0:
-        return torch.zeros(M, N, dtype=F32, device=dev)
-    _timed("nfk_wgrad", dev, "nfk_wgrad", gp_, ldg, hp_, ldh, B, M, N, rows, ns, part.data_ptr(), _stream(dev))
-    return part.sum(0)
-
-
 def fcnn_linear(x, pack, W_shape, bias, out, *, tanh=False):
     """out = x @ W + bias (tanh'd when ``tanh``), W [P, H] packed by fcnn_dh_pack
     (an nn.Linear's weight transposed): the FCNN forward on the same kernel."""

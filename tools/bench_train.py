@@ -65,13 +65,10 @@ def main():
                     help="recompute forward of FCNN conditioners on library GEMMs")
     ap.add_argument("--no-fcnn-dh", action="store_true",
                     help="library GEMMs + tanh_backward for the FCNN input gradients (config.USE_FCNN_DH off)")
-    ap.add_argument("--no-wgrad-mfma", action="store_true",
-                    help="split-K fp32 library GEMMs for the FCNN weight gradients (config.USE_WGRAD_MFMA off)")
     args = ap.parse_args()
     from normalizingflow_amd import config
     config.USE_FCNN_DH = not args.no_fcnn_dh
     config.USE_FCNN_FWD = not args.no_fcnn_fwd
-    config.USE_WGRAD_MFMA = not args.no_wgrad_mfma
     dev = torch.device("cuda", 0)
     model, sd, _ = bench.build_model(args.workload, dev)
     x = torch.randn(args.batch, bench.WORKLOADS[args.workload][3], device=dev)
@@ -83,8 +80,7 @@ def main():
 
     res = {"metric": "samples/sec train step (NLL fwd + bwd + Adam)", "workload": args.workload,
            "batch": args.batch, "steps": args.steps,
-           "fcnn_dh": config.USE_FCNN_DH, "fcnn_fwd": config.USE_FCNN_FWD,
-           "wgrad_mfma": config.USE_WGRAD_MFMA}
+           "fcnn_dh": config.USE_FCNN_DH, "fcnn_fwd": config.USE_FCNN_FWD}
     t = timed(ours, opt, x, args.steps, args.warmup)
     res["hip"] = {"ms_per_step": round(t * 1e3, 3), "samples_per_s": round(args.batch / t, 1)}
     if not args.no_torch:
