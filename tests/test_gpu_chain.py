@@ -173,10 +173,17 @@ def test_chain_max_layers_with_scattered_packs(hip_device):
     Bitwise equal to per-layer launches, and on par with the oracle."""
     nmax = K_.fused_nsf_chain_max(32, 32, 100, 8)
     model, sd = _model(nmax, 32, 2, 8, 100, [[0], [1]], hip_device)
-    spacers = []
-    for f in reversed(list(model.flows)):
-        spacers.append(torch.empty(2200 * 1024 * 1024, dtype=torch.uint8, device=hip_device))
-        assert f._fused_pack(hip_device) is not None
+    # every layer's pack copied into one large buffer at DESCENDING offsets
+    # 2.2 GiB apart, and the layers' pack caches pointed at those copies
+    packs = [f._fused_pack(hip_device) for f in model.flows]
+    step = (2200 << 20) // 4  # floats
+    big = torch.empty(step * nmax + packs[0].numel(), dtype=torch.float32, device=hip_device)
+    for l, f in enumerate(model.flows):
+        off = (nmax - 1 - l) * step
+        view = big[off:off + packs[l].numel()]
+        view.copy_(packs[l])
+        key, _, hidden = f._pack_cache
+        f._pack_cache = (key, view, hidden)
     ptrs = [f._pack_cache[1].data_ptr() for f in model.flows]
     assert all(a > b + (1 << 31) for a, b in zip(ptrs, ptrs[1:])), "packs not scattered as intended"
     x = torch.randn(3000, 64, generator=torch.Generator().manual_seed(9)) * 1.2
@@ -190,4 +197,4 @@ def test_chain_max_layers_with_scattered_packs(hip_device):
         assert torch.equal(a, b)
     specs = orc.nsf_cl_specs(nmax, 32, 2, 8, 3, [[0], [1]])
     torch.testing.assert_close(model.log_prob(xd).cpu(), orc.model_log_prob(specs, sd, x), rtol=1e-5, atol=1e-4)
-    del spacers
+    del big

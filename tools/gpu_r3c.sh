@@ -8,7 +8,7 @@ run() {  # name timeout cmd...
   echo "$n rc=$rc"; tail -3 $O/$n.log
   [ $rc -eq 0 ] || exit $rc
 }
-run bench_ar_unfused 400 python bench.py --workload ar --unfused --steps 2 --warmup 1 --no-cpu-baseline --parity-rows 2048
+#run bench_ar_unfused 400 python bench.py --workload ar --unfused --steps 2 --warmup 1 --no-cpu-baseline --parity-rows 2048
 NFK_CHAIN2=1 run chain2_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_chain.py tests/test_gpu_parity.py -k "chain or c3"
 for r in 1 2; do
   NFK_CHAIN2=0 run c3_one_$r 300 python bench.py --no-cpu-baseline --parity-rows 16384
