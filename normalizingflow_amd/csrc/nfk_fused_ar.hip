@@ -8,7 +8,7 @@
 // init_param.  The reference runs dim host iterations of torch ops per layer;
 // the unfused path here ran ~8 launches per coordinate.
 //
-// Work decomposition: a workgroup = kArWaves waves x 16 samples.  The rows
+// Work decomposition: a workgroup = NW waves x 16 samples.  The rows
 // stay with the workgroup for the whole layer and the conditioners of the dim
 // coordinates stream through it in order, so the inverse's sequential column
 // loop and the forward share one structure:
@@ -41,6 +41,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -56,7 +57,11 @@ using namespace nfk_fused;
 namespace {
 
 constexpr int kArNS = 2;     // output tiles per sub-record
-constexpr int kArWaves = 8;  // waves per workgroup (two per SIMD), 16 samples each
+// waves per workgroup, 16 samples each: 4 (one per SIMD; two independent
+// workgroups share a CU, so the two waves on a SIMD run unsynchronised phases)
+// or 8 (one workgroup per CU; half the weight stream per sample, but its two
+// waves per SIMD run every phase in lockstep); NFK_AR_WAVES selects
+constexpr int kArWavesMax = 8;
 constexpr int kArMaxDim = 128;
 
 struct ArDims {
@@ -87,8 +92,8 @@ __host__ __device__ inline int64_t ar_pack_floats(const ArDims& d, int dim) { re
 // columns splined per spline pass: in forward 4 (one per lane group; 2 when
 // the slab row is long, K > 16), in inverse 1
 __host__ __device__ constexpr int ar_group(bool inv, int ps) { return inv ? 1 : (ps <= 52 ? 4 : 2); }
-inline size_t ar_lds_bytes(const ArDims& d, int dim, bool inv) {
-    return (size_t)2 * d.SB * 1024 + (size_t)kArWaves * ar_group(inv, d.PS) * 16 * d.PS * sizeof(float) +
+inline size_t ar_lds_bytes(const ArDims& d, int dim, bool inv, int nw = kArWavesMax) {
+    return (size_t)2 * d.SB * 1024 + (size_t)nw * ar_group(inv, d.PS) * 16 * d.PS * sizeof(float) +
            (size_t)(dim + 3) / 4 * 16;
 }
 
@@ -307,8 +312,9 @@ __device__ __forceinline__ void trig_split(float v, float pi, float bnd, _Float1
     sl = (_Float16)(s - (float)sh);
 }
 
-template <int KBH, bool T1, int K, int KBX, bool INV>
-__global__ __launch_bounds__(64 * kArWaves, 2) void k_fused_ar(ArArgs a) {
+template <int KBH, bool T1, int K, int KBX, bool INV, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
+    constexpr int kArWaves = NW;
     constexpr int HT = 2 * KBH + (T1 ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
     constexpr int NH = (HT + kArNS - 1) / kArNS, N3 = (NO + kArNS - 1) / kArNS, SPC = 2 * NH + N3;
     constexpr int NTG = T1 ? (kArNS + 1) / 2 : 0;
@@ -508,13 +514,26 @@ __global__ __launch_bounds__(64 * kArWaves, 2) void k_fused_ar(ArArgs a) {
 }
 
 template <int KBH, int T1, int K, int KBX>
-int launch_ar(const ArArgs& a, size_t lds, bool inv, hipStream_t st) {
-    const int64_t per = (int64_t)kArWaves * 16;
-    const dim3 g((unsigned)((a.batch + per - 1) / per)), b(64 * kArWaves);
-    if (inv)
-        hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, true>), g, b, lds, st, a);
-    else
-        hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, false>), g, b, lds, st, a);
+int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
+    static const int nw_env = [] {
+        const char* e = std::getenv("NFK_AR_WAVES");
+        return (e != nullptr && e[0] == '8') ? 8 : 4;
+    }();
+    const int nw = nw_env;
+    const size_t lds = ar_lds_bytes(d, a.dim, inv, nw);
+    const int64_t per = (int64_t)nw * 16;
+    const dim3 g((unsigned)((a.batch + per - 1) / per)), b(64 * nw);
+    if (nw == 8) {
+        if (inv)
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, true, 8>), g, b, lds, st, a);
+        else
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, false, 8>), g, b, lds, st, a);
+    } else {
+        if (inv)
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, true, 4>), g, b, lds, st, a);
+        else
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, false, 4>), g, b, lds, st, a);
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -573,12 +592,11 @@ extern "C" int nfk_fused_ar(const float* x, int64_t ldx, const float* pack, int3
     // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:186-187)
     a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
     const bool inv = inverse != 0;
-    const size_t lds = ar_lds_bytes(d, dim, inv);
     hipStream_t st = (hipStream_t)stream;
     int kbx = 0;
     ar_instance(d, K, &kbx);
 #define NFK_AR_LAUNCH(h, t, k, xx) \
-    if (d.KBH == h && d.T1 == t && K == k && kbx == xx) return launch_ar<h, t, k, xx>(a, lds, inv, st);
+    if (d.KBH == h && d.T1 == t && K == k && kbx == xx) return launch_ar<h, t, k, xx>(a, d, inv, st);
     NFK_AR_SHAPES(NFK_AR_LAUNCH)
 #undef NFK_AR_LAUNCH
     return nfk_set_error("nfk_fused_ar: no kernel instance");
