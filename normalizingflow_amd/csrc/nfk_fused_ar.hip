@@ -28,7 +28,7 @@
 //     column): in forward G = 4 coordinates at once (lane group q takes
 //     column i0 + q), in inverse one coordinate (every lane group computes
 //     it; the result feeds the next conditioners' trig features);
-//   * weights stream as uniform sub-records (SB 1-KiB blocks: NS = 2 output
+//   * weights stream as uniform sub-records (SB 1-KiB blocks: NS = 3 output
 //     tiles x all k-blocks x {hi, lo}, the tail step's blocks, the record's
 //     bias block) through two LDS slots: the copy of sub-record s + 2 is issued
 //     right after the barrier that ends the GEMM of s (one barrier per
@@ -56,7 +56,10 @@ using namespace nfk_fused;
 
 namespace {
 
-constexpr int kArNS = 2;     // output tiles per sub-record
+#ifndef NFK_AR_NS
+#define NFK_AR_NS 3
+#endif
+constexpr int kArNS = NFK_AR_NS;  // output tiles per sub-record
 // waves per workgroup, 16 samples each: 4 (one per SIMD; two independent
 // workgroups share a CU, so the two waves on a SIMD run unsynchronised phases)
 // or 8 (one workgroup per CU; half the weight stream per sample, but its two
@@ -189,9 +192,8 @@ __device__ uint32_t ar_sub_word(int blk, int wl, int kbn, int t1, int nt, int T0
         const int lane = wl >> 2, j = 2 * (wl & 3), k0 = 32 * kb + 8 * (lane >> 4) + j;
         return nfk_f16_part_pair(val(t, lane & 15, k0) * sc, val(t, lane & 15, k0 + 1) * sc, part);
     }
-    if (blk < nf + ntg) {  // tail: (hi, hi, lo, 0) of tiles 2g, 2g + 1 (tail_word's layout)
-        const int g = T0 / 2 + (blk - nf);
-        const int t = 2 * g + ((wl & 3) >> 1), lane = wl >> 2, j = 2 * (wl & 1), qq = lane >> 4;
+    if (blk < nf + ntg) {  // tail: (hi, hi, lo, 0) of the sub-record's tile pair (tail_word's layout)
+        const int t = T0 + 2 * (blk - nf) + ((wl & 3) >> 1), lane = wl >> 2, j = 2 * (wl & 1), qq = lane >> 4;
         if (t >= nt || qq == 3) return 0u;
         const int kb0 = 32 * kbn;
         return nfk_f16_part_pair(val(t, lane & 15, kb0 + j) * sc, val(t, lane & 15, kb0 + j + 1) * sc,

@@ -79,11 +79,13 @@ def _c5_model(n_layers):
 
 
 def test_c5_log_prob_vs_oracle(hip_device):
+    """The 16-layer c5 model (BASELINE config 5) on 16,384 rows vs the oracle."""
     model = _c5_model(16)
     sd = cpu_sd(model)
     specs = orc.nsf_cl_specs(16, 128, 2, 16, 3, [[i % 2] for i in range(16)])
-    x = torch.randn(1536, 256, generator=torch.Generator().manual_seed(0))
-    ref = orc.model_log_prob(specs, sd, x)
+    x = torch.randn(16384, 256, generator=torch.Generator().manual_seed(0))
+    with torch.inference_mode():
+        ref = torch.cat([orc.model_log_prob(specs, sd, xc) for xc in x.split(4096)])
     model = model.to(hip_device)
     model.prior = torch.distributions.MultivariateNormal(torch.zeros(256, device=hip_device),
                                                         torch.eye(256, device=hip_device))

@@ -14,14 +14,5 @@ for r in 1 2; do
   NFK_CHAIN2=0 run c3_one_$r 300 python bench.py --no-cpu-baseline --parity-rows 16384
   NFK_CHAIN2=1 run c3_two_$r 300 python bench.py --no-cpu-baseline --parity-rows 16384
 done
-run ar_tests 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_nsfar_fused.py
-for r in 1 2; do
-  NFK_AR_WAVES=4 run ar_w4_$r 300 python bench.py --workload ar --no-cpu-baseline --parity-rows 4096
-  NFK_AR_WAVES=8 run ar_w8_$r 300 python bench.py --workload ar --no-cpu-baseline --parity-rows 4096
-done
 NFK_CHAIN2=0 run c3_one_2e17 300 python bench.py --no-cpu-baseline --batch 131072 --steps 50
 NFK_CHAIN2=1 run c3_two_2e17 300 python bench.py --no-cpu-baseline --batch 131072 --steps 50
-run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-export TMPDIR=/tmp
-run prof_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o trace -- python3 bench.py --no-cpu-baseline
-run prof_ar 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_ar -o trace -- python3 bench.py --workload ar --no-cpu-baseline
