@@ -371,9 +371,9 @@ extern "C" int nfk_debug_fused_form(int form) {
     return prev;
 }
 
-// Diagnostic: kernel of nfk_fused_nsf_chain: -1 = automatic (NFK_CHAIN2 in the
-// environment), 0 = one 16-sample tile per wave, 1 = two tiles per wave where
-// instanced.  Returns the previous setting.  Not part of include/nfk.h.
+// Diagnostic: kernel of nfk_fused_nsf_chain: -1 = automatic (two tiles per wave
+// where instanced unless NFK_CHAIN2=0), 0 = one 16-sample tile per wave, 1 = two
+// tiles per wave where instanced.  Returns the previous setting.  Not part of include/nfk.h.
 extern "C" int nfk_debug_chain_form(int form) {
     const int prev = g_chain_form;
     g_chain_form = form < 0 ? -1 : (form ? 1 : 0);
@@ -621,11 +621,13 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
     }
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
-    // two sample tiles per wave (nfk_fused_chain2.hip) where instanced:
-    // NFK_CHAIN2=0 / nfk_debug_chain_form(0) selects the one-tile kernel
+    // two sample tiles per wave (nfk_fused_chain2.hip) where instanced (c3:
+    // 5.83-5.84 vs 6.02 ms per 2^20 log_prob, 0.805 vs 0.832 ms at 2^17, A/B on
+    // one box, profiles/r3c_chain2_ab.txt): NFK_CHAIN2=0 /
+    // nfk_debug_chain_form(0) selects the one-tile kernel
     static const bool c2_env = [] {
         const char* e = std::getenv("NFK_CHAIN2");
-        return e != nullptr && e[0] == '1';
+        return !(e != nullptr && e[0] == '0');
     }();
     if ((g_chain_form < 0 ? c2_env : g_chain_form == 1) && chain2_ok(L, K, nlayers)) {
         const int rc = launch_chain2(a, L, K, inv, st);
