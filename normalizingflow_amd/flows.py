@@ -207,10 +207,12 @@ def check_status(status, n_slots=None, prior=None):
     if not mode or status is None or (n_slots == 0 and not _validates(prior)):
         return
     if mode == "deferred":
-        # queue this call's words first: an earlier call's error raised by the
-        # poll must not drop them
-        _STATUS_QUEUE.push(status, n_slots, prior)
-        _STATUS_QUEUE.poll()
+        # an earlier call's error raised by the poll must not drop this call's
+        # words: they are queued either way (and checked by a later call)
+        try:
+            _STATUS_QUEUE.poll()
+        finally:
+            _STATUS_QUEUE.push(status, n_slots, prior)
     else:
         raise_on_status(status, n_slots, prior)
 
