@@ -3,7 +3,7 @@
 # HEAD build's c3 chain, fused NSF_AR and c5 wide kernels; small-batch AR A/B.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-bash tools/pmc_passes.sh r3e_c3 "k_fused_nsf|k_nsf_chain2" --workload c3 || exit $?
+bash tools/pmc_passes.sh r3e_c3 "k_nsf_chain2" --workload c3 || exit $?
 bash tools/pmc_passes.sh r3e_ar "k_fused_ar" --workload ar || exit $?
 bash tools/pmc_passes.sh r3e_c5 "k_fused_nsf_wide" --workload c5 || exit $?
 O=gpurun_out/r3e; mkdir -p $O
