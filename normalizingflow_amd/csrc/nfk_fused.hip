@@ -321,6 +321,8 @@ int64_t pack_floats(int n_lo, int n_up, int H, int K) {
 uint32_t* g_trace = nullptr;  // diagnostic timeline buffer (NFK_TRACE builds)
 int g_form = -1;            // nfk_debug_fused_form
 int g_chain_form = -1;      // nfk_debug_chain_form
+constexpr int kChainFormDefault = 1;  // nfk_fused_nsf_chain's kernel form
+int g_last_chain_form = -1;           // nfk_debug_last_chain_form
 
 int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_t st) {
     WideArgs a;
@@ -371,14 +373,19 @@ extern "C" int nfk_debug_fused_form(int form) {
     return prev;
 }
 
-// Diagnostic: kernel of nfk_fused_nsf_chain: -1 = automatic (two tiles per wave
-// where instanced unless NFK_CHAIN2=0), 0 = one 16-sample tile per wave, 1 = two
-// tiles per wave where instanced.  Returns the previous setting.  Not part of include/nfk.h.
+// Diagnostic: kernel of nfk_fused_nsf_chain: -1 = automatic (NFK_CHAIN_FORM in
+// the environment, else the default of nfk_fused_nsf_chain), 0 = one
+// 16-sample tile per wave, 1 = two tiles per wave, 2 = the 32x32x16 kernel
+// (where instanced; else the next lower form).  Returns the previous setting.
+// Not part of include/nfk.h.
 extern "C" int nfk_debug_chain_form(int form) {
     const int prev = g_chain_form;
-    g_chain_form = form < 0 ? -1 : (form ? 1 : 0);
+    g_chain_form = form < 0 ? -1 : (form > 2 ? 2 : form);
     return prev;
 }
+
+// Diagnostic: the kernel form the last nfk_fused_nsf_chain call launched (-1: none yet).
+extern "C" int nfk_debug_last_chain_form() { return g_last_chain_form; }
 
 // ---- the VJP pack (nfk_fused_vjp.hip): records in the 8-coordinate layout,
 // then the stream of SB-block sub-records re-cut from them (vjp_dims)
@@ -451,9 +458,10 @@ extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidde
     return pack_ok(n_lo, n_up, hidden, K) ? 1 : 0;
 }
 
+// the 16x16 pack, then (c3-class shapes) the 32x32 chain's pack32
 extern "C" int64_t nfk_fused_nsf_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
     if (!pack_ok(n_lo, n_up, hidden, K)) return 0;
-    return pack_floats(n_lo, n_up, hidden, K);
+    return pack_floats(n_lo, n_up, hidden, K) + chain32_pack_floats(n_lo, n_up, hidden, K);
 }
 
 extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float* w2, const float* b2,
@@ -478,7 +486,11 @@ extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float*
         hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, st, a);
     }
     e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
+    if (e != hipSuccess) return (int)e;
+    if (chain32_shape_ok(n_lo, n_up, hidden, K))
+        return chain32_pack(w0, b0, w2, b2, w4, b4, n_lo, n_up, hidden, K,
+                            wpack + pack_floats(n_lo, n_up, hidden, K), st);
+    return 0;
 }
 
 namespace {
@@ -621,18 +633,28 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
     }
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
-    // two sample tiles per wave (nfk_fused_chain2.hip) where instanced (c3:
-    // 5.83-5.84 vs 6.02 ms per 2^20 log_prob, 0.805 vs 0.832 ms at 2^17, A/B on
-    // one box, profiles/r3c_chain2_ab.txt): NFK_CHAIN2=0 /
-    // nfk_debug_chain_form(0) selects the one-tile kernel
-    static const bool c2_env = [] {
-        const char* e = std::getenv("NFK_CHAIN2");
-        return !(e != nullptr && e[0] == '0');
+    // kernel forms: 2 = 32x32x16 MFMAs, 32 samples per wave
+    // (nfk_fused_chain32.hip); 1 = two 16-sample tiles per wave
+    // (nfk_fused_chain2.hip; c3: 5.83-5.84 vs 6.02 ms per 2^20 log_prob, 0.805
+    // vs 0.832 ms at 2^17 against form 0, profiles/r3c_chain2_ab.txt); 0 = one
+    // tile.  Each where instanced, else the next lower; NFK_CHAIN_FORM in the
+    // environment or nfk_debug_chain_form overrides the default.
+    static const int form_env = [] {
+        const char* e = std::getenv("NFK_CHAIN_FORM");
+        return (e != nullptr && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : kChainFormDefault;
     }();
-    if ((g_chain_form < 0 ? c2_env : g_chain_form == 1) && chain2_ok(L, K, nlayers)) {
-        const int rc = launch_chain2(a, L, K, inv, st);
+    const int form = g_chain_form < 0 ? form_env : g_chain_form;
+    if (form >= 2 && chain32_ok(n_lo, n_up, hidden, K, nlayers)) {
+        const int rc = launch_chain32(a, K, inv, pack_floats(n_lo, n_up, hidden, K), st);
+        g_last_chain_form = 2;
         if (rc >= 0) return rc;
     }
+    if (form >= 1 && chain2_ok(L, K, nlayers)) {
+        const int rc = launch_chain2(a, L, K, inv, st);
+        g_last_chain_form = 1;
+        if (rc >= 0) return rc;
+    }
+    g_last_chain_form = 0;
     const size_t lds = lds_bytes_chain(L, nlayers);
 #define DISPATCH(h, t, k) \
     if (L.KBH == h && L.T1 == t && K == k) return launch_fused<h, t, k>(a, lds, inv, true, true, st);

@@ -20,6 +20,15 @@
 
 #include "nfk_fused_impl.h"
 
+// branch-free map/x reads of layer 1 (L1) and of the spline inputs (XV):
+// build switches for A/B runs
+#ifndef NFK_C2_BF_L1
+#define NFK_C2_BF_L1 1
+#endif
+#ifndef NFK_C2_BF_XV
+#define NFK_C2_BF_XV 1
+#endif
+
 namespace nfk_fused {
 
 constexpr int kC2Tiles = 2;  // sample tiles per wave
@@ -224,7 +233,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
         c_lo = cm + l * D;
         c_up = c_lo + A->n_lo;
         sr = 0;
-        const FusedConst& c = *(const FusedConst*)&A->c;
+        const FusedConst c = *(const FusedConst*)&A->c;  // by value: SGPRs for the layer
         const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
         bool any_in = false, any_nd = false;
 
@@ -241,7 +250,13 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int k = 8 * q + j;
+#if NFK_C2_BF_L1
+                    const bool ok = k < A->n_lo;  // unconditional reads, then selected
+                    const float v = xr[c_lo[ok ? k : 0]];
+                    e[j] = ok ? v : 0.0f;
+#else
                     e[j] = k < A->n_lo ? xr[c_lo[k]] : 0.0f;
+#endif
                 }
                 float mx = 0.0f;
 #pragma unroll
@@ -302,6 +317,24 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
             {
                 f32x4 acc[NTL][K];
                 gemm_rec(acc);
+#if NFK_C2_BF_XV
+                // map reads and x reads unconditional (a guarded read became a
+                // branch with its own LDS round trip per coordinate)
+                int tc4[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    jj4[r] = jbase + 4 * q + r;
+                    const bool ok = jj4[r] < A->n_up;
+                    tc4[r] = ok ? (int)c_up[ok ? jj4[r] : 0] : D;
+                }
+#pragma unroll
+                for (int s = 0; s < NTL; ++s) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float v = xt[(16 * s + sl) * XS + tc4[r]];
+                        xv[s][r] = (jj4[r] < A->n_up) ? v : 0.0f;
+                    }
+#else
 #pragma unroll
                 for (int r = 0; r < 4; ++r) jj4[r] = jbase + 4 * q + r;
 #pragma unroll
@@ -309,6 +342,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         xv[s][r] = (jj4[r] < A->n_up) ? xt[(16 * s + sl) * XS + c_up[jj4[r]]] : 0.0f;
+#endif
                     knot_phase<K, true, 0, 4, true>(acc[s], xv[s], c, l2e3, kb[s], INV ? ch_k[s] : cw_k[s],
                                                    INV ? h_k[s] : w_k[s], scr + s * K * 64, lane);
                 }
@@ -375,7 +409,15 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                         const bool inside = (x >= c.lo) && (x <= c.hi);
                         const bool live = jj4[r] < A->n_up && row_ok[s];
                         out = inside ? out : x;
+#if NFK_C2_BF_XV
+                        // past n_up: the padding column (the map re-read: the
+                        // columns held in registers across the epilogues spilled)
+                        const bool okc = jj4[r] < A->n_up;
+                        const int tcol = okc ? (int)c_up[okc ? jj4[r] : 0] : D;
+                        xt[(16 * s + sl) * XS + tcol] = out;
+#else
                         if (jj4[r] < A->n_up) xt[(16 * s + sl) * XS + c_up[jj4[r]]] = out;
+#endif
                         ldsum[s] += (inside && live) ? lad : 0.0f;
                         any_in |= inside && live;
                         any_nd |= nd && inside && live;

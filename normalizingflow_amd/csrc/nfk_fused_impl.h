@@ -564,6 +564,13 @@ __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[
 #ifndef NFK_LUT
 #define NFK_LUT 1
 #endif
+#ifndef NFK_E1_SEL
+#define NFK_E1_SEL 1
+#endif
+#ifndef NFK_KP_SERIAL
+// knot_phase: one coordinate at a time (a scheduling barrier between them)
+#define NFK_KP_SERIAL 0
+#endif
 #ifndef NFK_PK2
 // knot prefixes of coordinate pairs in packed fp32: 7 % fewer VALU
 // instructions per layer, yet c3 measured 1 % slower (6.37 vs 6.30 ms per
@@ -641,12 +648,18 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
             }
         }
         const float e = __builtin_fmaf(c.sp30, (float)p0, lo);
-        const float e1 = (kk == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, lo);
+        float e1 = __builtin_fmaf(c.sp30, (float)p1, lo);
+        // computed for every lane, then selected: as a conditional the compiler
+        // sank the LUT read into a branch with its own LDS wait
+#if NFK_E1_SEL
+        asm volatile("" : "+v"(e1));
+#endif
+        e1 = (kk == K - 1) ? c.hi : e1;
         ek[r] = e;
         sk[r] = e1 - e;
         // wide layers (K = 16): one coordinate at a time, or the scheduler
         // interleaves the four and runs out of registers
-        if constexpr (K > 8) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (K > 8 || NFK_KP_SERIAL) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -988,7 +1001,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
         c_up = c_lo + A->n_lo;
         sr = 0;
     }
-    const FusedConst& c = *(const FusedConst*)&A->c;  // (per layer: see A)
+    const FusedConst c = *(const FusedConst*)&A->c;  // by value (SGPRs); per layer: see A
     const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
         bool any_in = false, any_nd = false;
 
@@ -1001,8 +1014,13 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int k = 32 * kb + 8 * q + j;
-                    const int col = (kb == 0 && !CHAIN) ? lo_c0[j] : (k < A->n_lo ? lo_map(k) : -1);
-                    e[j] = col >= 0 ? xlo[sl * XS + col] : 0.0f;
+                    // map and x reads unconditional (clamped), then selected: a
+                    // guarded read became a branch with its own LDS wait
+                    const bool ok = k < A->n_lo;
+                    const int m = lo_map(ok ? k : 0);
+                    const int col = (kb == 0 && !CHAIN) ? lo_c0[j] : (ok ? m : -1);
+                    const float xv0 = xlo[sl * XS + (col >= 0 ? col : 0)];
+                    e[j] = col >= 0 ? xv0 : 0.0f;
                 }
                 u = make_float4(e[0], e[1], e[2], e[3]);
                 v = make_float4(e[4], e[5], e[6], e[7]);
@@ -1084,6 +1102,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
         // per-coordinate state of the chunk: lane group q holds coordinates
         // jbase + 4q + r, r = 0..3, of sample sl
         int jj4[4];
+        int pos4[4];  // tile position of each coordinate (clamped past n_up)
         float xv[4];
         int kb[4];
         float cw_k[4], w_k[4], ch_k[4], h_k[4];
@@ -1093,7 +1112,10 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
     #pragma unroll
             for (int r = R0; r < R1; ++r) {
                 jj4[r] = jbase + 4 * q + r;
-                xv[r] = (jj4[r] < A->n_up) ? (SPLIT ? xlo : xup)[up_pos(jj4[r])] : 0.0f;
+                const bool ok = jj4[r] < A->n_up;
+                pos4[r] = up_pos(ok ? jj4[r] : 0);
+                const float v = (SPLIT ? xlo : xup)[pos4[r]];
+                xv[r] = ok ? v : 0.0f;
             }
             knot_phase<K, true, R0, R1, PK2>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k, scr, lane);
         };
@@ -1111,7 +1133,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                 float v = cw_k[r] + w_k[r] + ch_k[r] + h_k[r];
     #pragma unroll
                 for (int t = 0; t < DN; ++t) v += accd[t][r];
-                if (jj4[r] < A->n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = v;
+                if (jj4[r] < A->n_up) (SPLIT ? xlo : xup)[pos4[r]] = v;
                 ldsum += v;
                 any_in = true;
             }
@@ -1179,7 +1201,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                 const bool inside = (x >= c.lo) && (x <= c.hi);
                 const bool live = jj4[r] < A->n_up && row_ok;
                 out = inside ? out : x;
-                if (jj4[r] < A->n_up) (SPLIT ? xlo : xup)[up_pos(jj4[r])] = out;  // z collected in the tile
+                if (jj4[r] < A->n_up) (SPLIT ? xlo : xup)[pos4[r]] = out;  // z collected in the tile
                 ldsum += (inside && live) ? lad : 0.0f;
                 any_in |= inside && live;
                 any_nd |= nd && inside && live;
@@ -1407,6 +1429,14 @@ inline bool vjp_ok(int n_lo, int n_up, int H, int K) {
 // the two-tile chain (nfk_fused_chain2.hip): c3-class shapes
 int launch_chain2(const FusedArgs& a, const Layout& L, int K, bool inv, hipStream_t st);
 bool chain2_ok(const Layout& L, int K, int nl);
+// the 32x32x16 chain (nfk_fused_chain32.hip) and its pack, appended to a
+// layer's 16x16 pack where chain32_shape_ok
+bool chain32_shape_ok(int n_lo, int n_up, int H, int K);
+int64_t chain32_pack_floats(int n_lo, int n_up, int H, int K);
+int chain32_pack(const float* w0, const float* b0, const float* w2, const float* b2, const float* w4,
+                 const float* b4, int n_lo, int n_up, int H, int K, float* pack, hipStream_t st);
+int launch_chain32(FusedArgs a, int K, bool inv, int64_t base, hipStream_t st);
+bool chain32_ok(int n_lo, int n_up, int H, int K, int nl);
 
 // hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f16 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132

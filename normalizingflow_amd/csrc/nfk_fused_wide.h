@@ -21,12 +21,15 @@
 //   * layer-1 operands (x at the lower coordinates) are read once per wave
 //     into registers by plain loads in the prologue, before any copy is
 //     waited on, and split there (per-wave power-of-two scale as before);
-//   * the lower coordinates pass through to z (flows.py:239) from those
-//     prologue registers, so x's lower half is read from HBM once;
-//   * per chunk pair, each wave stages the 16 upper coordinates of its 16
-//     rows by LDS-DMA gathers into the odd columns of a 16 x 32 tile; the
-//     spline reads x there, writes z back in place, and the odd columns are
-//     stored after the pair (the even ones are never fetched);
+//   * per chunk pair, each wave stages the 32 coordinates (16 upper, 16
+//     lower) of its 16 rows by LDS-DMA gathers into a 16 x 32 tile; the
+//     spline reads x there, writes z back in place (the lower coordinates
+//     pass through, flows.py:239), and the tile is stored after the pair as
+//     whole 128-B row segments.  Writing the lower half of z from the
+//     prologue registers instead (x's lower half read once) was measured
+//     worse: the two halves of every z line then reach HBM as separate
+//     partial-line writes, 2.15 GB written and 4.56 GB read per c5 launch
+//     against 1.2 / 3.7 GB (profiles/r3e_pmc_c5.txt);
 //   * LDS: two 65-KiB slots + 2 KiB x tile per wave + index maps (152 KiB at
 //     c5), one 8-wave workgroup (128 samples) per CU.
 // Copies follow the invariant of nfk_fused_impl.h: a copy is waited for
@@ -297,10 +300,7 @@ __device__ __forceinline__ int wide_col(const int32_t* m_lo, const int32_t* m_up
     return m_lo[valid ? j : 0];
 }
 
-// LDS-DMA gather of pair g's x tile: element e = 64 i + lane is (e >> 5, e & 31);
-// only the odd (upper-coordinate) columns are fetched (the lanes of the even
-// ones are masked off): the lower coordinates pass through to z from the
-// layer-1 operand loads of the prologue, so x's lower half is read once
+// LDS-DMA gather of pair g's x tile: element e = 64 i + lane is (e >> 5, e & 31)
 __device__ __forceinline__ void wide_gather(const WideArgs& a, const int32_t* m_lo_in, const int32_t* m_up_in,
                                             int64_t b0, int g, float* tile, int lane) {
     const uint32_t base = lds_addr(tile);
@@ -311,12 +311,11 @@ __device__ __forceinline__ void wide_gather(const WideArgs& a, const int32_t* m_
         const int col = wide_col(m_lo_in, m_up_in, a.n_lo, a.n_up, g, t, ok);
         int64_t row = b0 + r;
         if (row >= a.batch) row = a.batch - 1;
-        if (t & 1) dma4(a.x + row * a.ldx + col, base + i * 256);
+        dma4(a.x + row * a.ldx + col, base + i * 256);
     }
 }
 
-// z of pair g from the tile: its upper coordinates (odd columns; the lower
-// ones were written in the prologue)
+// z of pair g from the tile (upper coordinates transformed, lower ones passed through)
 __device__ __forceinline__ void wide_store(const WideArgs& a, const int32_t* m_lo_out, const int32_t* m_up_out,
                                            int64_t b0, int nrows, int g, const float* tile, int lane) {
     float v[8];
@@ -327,7 +326,7 @@ __device__ __forceinline__ void wide_store(const WideArgs& a, const int32_t* m_l
         const int e = 64 * i + lane, r = e >> 5, t = e & 31;
         bool ok;
         const int col = wide_col(m_lo_out, m_up_out, a.n_lo, a.n_up, g, t, ok);
-        if ((t & 1) && ok && r < nrows) a.z[(b0 + r) * a.ldz + col] = v[i];
+        if (ok && r < nrows) a.z[(b0 + r) * a.ldz + col] = v[i];
     }
 }
 
@@ -354,7 +353,7 @@ __global__ __launch_bounds__(64 * kWideWaves, kWideWGs) void k_fused_nsf_wide(Wi
     const int64_t rem = a.batch - b0;
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const bool row_ok = sl < nrows;
-    const FusedConst& c = a.c;
+    const FusedConst c = a.c;  // by value: SGPRs
     const float* pk = a.pack;
     NfkTrace tr;
     NFK_MARK(tr);  // start
@@ -392,18 +391,6 @@ __global__ __launch_bounds__(64 * kWideWaves, kWideWGs) void k_fused_nsf_wide(Wi
                 xv[kb][j] = (kb < a.KB1 && k < a.n_lo) ? xr[m_lo_in[k]] : 0.0f;
                 mx = fmaxf(mx, fabsf(xv[kb][j]));
             }
-        // the pass-through half of z (flows.py:239: the lower coordinates,
-        // unchanged) straight from these registers
-        if (row_ok) {
-            float* zr = a.z + (b0 + sl) * a.ldz;
-#pragma unroll
-            for (int kb = 0; kb < KBH; ++kb)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int k = 32 * kb + 8 * q + j;
-                    if (kb < a.KB1 && k < a.n_lo) zr[m_lo_out[k]] = xv[kb][j];
-                }
-        }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
         int ex = 0;
