@@ -375,12 +375,11 @@ extern "C" int nfk_debug_fused_form(int form) {
 
 // Diagnostic: kernel of nfk_fused_nsf_chain: -1 = automatic (NFK_CHAIN_FORM in
 // the environment, else the default of nfk_fused_nsf_chain), 0 = one
-// 16-sample tile per wave, 1 = two tiles per wave, 2 = the 32x32x16 kernel
-// (where instanced; else the next lower form).  Returns the previous setting.
-// Not part of include/nfk.h.
+// 16-sample tile per wave, 1 = two tiles per wave (where instanced; else
+// form 0).  Returns the previous setting.  Not part of include/nfk.h.
 extern "C" int nfk_debug_chain_form(int form) {
     const int prev = g_chain_form;
-    g_chain_form = form < 0 ? -1 : (form > 2 ? 2 : form);
+    g_chain_form = form < 0 ? -1 : (form > 1 ? 1 : form);
     return prev;
 }
 
@@ -458,10 +457,9 @@ extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidde
     return pack_ok(n_lo, n_up, hidden, K) ? 1 : 0;
 }
 
-// the 16x16 pack, then (c3-class shapes) the 32x32 chain's pack32
 extern "C" int64_t nfk_fused_nsf_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
     if (!pack_ok(n_lo, n_up, hidden, K)) return 0;
-    return pack_floats(n_lo, n_up, hidden, K) + chain32_pack_floats(n_lo, n_up, hidden, K);
+    return pack_floats(n_lo, n_up, hidden, K);
 }
 
 extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float* w2, const float* b2,
@@ -486,11 +484,7 @@ extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float*
         hipLaunchKernelGGL(k_pack, dim3((unsigned)g), dim3(256), 0, st, a);
     }
     e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
-    if (chain32_shape_ok(n_lo, n_up, hidden, K))
-        return chain32_pack(w0, b0, w2, b2, w4, b4, n_lo, n_up, hidden, K,
-                            wpack + pack_floats(n_lo, n_up, hidden, K), st);
-    return 0;
+    return e == hipSuccess ? 0 : (int)e;
 }
 
 namespace {
@@ -633,22 +627,17 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
     }
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
-    // kernel forms: 2 = 32x32x16 MFMAs, 32 samples per wave
-    // (nfk_fused_chain32.hip); 1 = two 16-sample tiles per wave
-    // (nfk_fused_chain2.hip; c3: 5.83-5.84 vs 6.02 ms per 2^20 log_prob, 0.805
-    // vs 0.832 ms at 2^17 against form 0, profiles/r3c_chain2_ab.txt); 0 = one
-    // tile.  Each where instanced, else the next lower; NFK_CHAIN_FORM in the
-    // environment or nfk_debug_chain_form overrides the default.
+    // kernel forms: 1 = two 16-sample tiles per wave (nfk_fused_chain2.hip;
+    // c3: 5.83-5.84 vs 6.02 ms per 2^20 log_prob, 0.805 vs 0.832 ms at 2^17
+    // against form 0, profiles/r3c_chain2_ab.txt) where instanced; 0 = one
+    // tile.  NFK_CHAIN_FORM in the environment or nfk_debug_chain_form
+    // overrides the default.  (A 32x32x16 form measured 1-4 % slower once
+    // both had branch-free epilogue reads: DESIGN.md section 6.)
     static const int form_env = [] {
         const char* e = std::getenv("NFK_CHAIN_FORM");
-        return (e != nullptr && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : kChainFormDefault;
+        return (e != nullptr && e[0] >= '0' && e[0] <= '1') ? e[0] - '0' : kChainFormDefault;
     }();
     const int form = g_chain_form < 0 ? form_env : g_chain_form;
-    if (form >= 2 && chain32_ok(n_lo, n_up, hidden, K, nlayers)) {
-        const int rc = launch_chain32(a, K, inv, pack_floats(n_lo, n_up, hidden, K), st);
-        g_last_chain_form = 2;
-        if (rc >= 0) return rc;
-    }
     if (form >= 1 && chain2_ok(L, K, nlayers)) {
         const int rc = launch_chain2(a, L, K, inv, st);
         g_last_chain_form = 1;

@@ -334,12 +334,21 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
     const bool row_ok = b0 + sl < a.batch;
     const int64_t brow = row_ok ? b0 + sl : a.batch - 1;  // rows past the batch re-read the last one
 
-    // sub-record s into slot s & 1: layer-1 sub-records hold ceil(2i / 32) k-blocks
-    auto stage = [&](int64_t s) {
-        if (s >= a.nsr) return;
-        const int i = 1 + (int)(s / SPC), u = (int)(s - (int64_t)(i - 1) * SPC);
-        const int nblk = u < NH ? ((2 * i + 31) / 32) * kArNS * 2 + 1 : KBH * kArNS * 2 + NTG + 1;
-        stage_record<kArWaves>(a.pack + 256 + s * a.sb * 256, nblk, (s & 1) ? slot1 : slot0, wid, lane);
+    // the next sub-record st_s (conditioner st_i, part st_u) into slot st_s & 1;
+    // layer-1 sub-records hold ceil(2i / 32) k-blocks.  Called once per
+    // sub-record in stream order, so a cursor replaces the 64-bit division
+    // s / SPC (a long SALU sequence per call: 15k SALU instructions a wave)
+    int st_s = 0, st_i = 1, st_u = 0;
+    auto stage_next = [&]() {
+        if (st_s >= a.nsr) return;
+        const int nblk = st_u < NH ? ((2 * st_i + 31) / 32) * kArNS * 2 + 1 : KBH * kArNS * 2 + NTG + 1;
+        stage_record<kArWaves>(a.pack + 256 + (int64_t)st_s * a.sb * 256, nblk, (st_s & 1) ? slot1 : slot0, wid,
+                               lane);
+        ++st_s;
+        if (++st_u == SPC) {
+            st_u = 0;
+            ++st_i;
+        }
     };
 
     // ---- prologue: status words, the first two sub-records, the trig operands
@@ -366,8 +375,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
             }
         }
     }
-    stage(0);
-    stage(1);
+    stage_next();
+    stage_next();
     dma_barrier();
 
     int64_t s = 0;  // the sub-record the next GEMM reads
@@ -376,7 +385,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        stage(s + 2);
+        stage_next();  // sub-record s + 2
         ++s;
     };
     const float c21 = -2.0f * kL2E * un1, c22 = -2.0f * kL2E * un2;

@@ -28,6 +28,10 @@
 #ifndef NFK_C2_BF_XV
 #define NFK_C2_BF_XV 1
 #endif
+// epilogue C: the bin's two derivative logits by selects instead of the LDS table
+#ifndef NFK_C2_DSEL
+#define NFK_C2_DSEL 0
+#endif
 
 namespace nfk_fused {
 
@@ -368,10 +372,19 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                         // epilogue C of k_fused_nsf, op for op
                         const int k = kb[s][r];
                         float raw_k = accd[s][0][r], raw_k1 = accd[s][0][r];
+#if NFK_C2_DSEL
+                        // logits k-1 and k by running selects (no LDS round trip)
+#pragma unroll
+                        for (int j = 1; j < K - 1; ++j) {
+                            raw_k = (k >= j + 1) ? accd[s][j][r] : raw_k;
+                            raw_k1 = (k >= j) ? accd[s][j][r] : raw_k1;
+                        }
+#else
 #pragma unroll
                         for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[s][j][r];
                         raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
                         raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
+#endif
                         const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
                         const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
                         const float d_k = (k == 0) ? c.d_edge : dv_k;

@@ -565,11 +565,8 @@ __device__ __forceinline__ void act_operands(f32x4 (&h)[HT], float c2, h8 (&bh)[
 #define NFK_LUT 1
 #endif
 #ifndef NFK_E1_SEL
+// knot_phase: the bin's right edge computed for every lane, then selected
 #define NFK_E1_SEL 1
-#endif
-#ifndef NFK_KP_SERIAL
-// knot_phase: one coordinate at a time (a scheduling barrier between them)
-#define NFK_KP_SERIAL 0
 #endif
 #ifndef NFK_PK2
 // knot prefixes of coordinate pairs in packed fp32: 7 % fewer VALU
@@ -659,7 +656,7 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
         sk[r] = e1 - e;
         // wide layers (K = 16): one coordinate at a time, or the scheduler
         // interleaves the four and runs out of registers
-        if constexpr (K > 8 || NFK_KP_SERIAL) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (K > 8) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -1429,14 +1426,6 @@ inline bool vjp_ok(int n_lo, int n_up, int H, int K) {
 // the two-tile chain (nfk_fused_chain2.hip): c3-class shapes
 int launch_chain2(const FusedArgs& a, const Layout& L, int K, bool inv, hipStream_t st);
 bool chain2_ok(const Layout& L, int K, int nl);
-// the 32x32x16 chain (nfk_fused_chain32.hip) and its pack, appended to a
-// layer's 16x16 pack where chain32_shape_ok
-bool chain32_shape_ok(int n_lo, int n_up, int H, int K);
-int64_t chain32_pack_floats(int n_lo, int n_up, int H, int K);
-int chain32_pack(const float* w0, const float* b0, const float* w2, const float* b2, const float* w4,
-                 const float* b4, int n_lo, int n_up, int H, int K, float* pack, hipStream_t st);
-int launch_chain32(FusedArgs a, int K, bool inv, int64_t base, hipStream_t st);
-bool chain32_ok(int n_lo, int n_up, int H, int K, int nl);
 
 // hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f16 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132

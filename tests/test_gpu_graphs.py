@@ -142,3 +142,22 @@ def test_graphed_sample_consistent_with_eager_kernels(hip_device):
     prior_lp = model.prior.log_prob(z2)
     torch.testing.assert_close(lp2, prior_lp - ldi, rtol=1e-5, atol=1e-4)
     flush_status_checks()
+
+
+@pytest.mark.parametrize("workload", ["c2", "c3", "c5", "ar"])
+def test_graphed_bench_workloads_bitwise(workload, hip_device):
+    """bench.py replays log_prob as a graph for per-rank batches <= 2^17 (the
+    8-GPU strong-scaling shard): the replay of every bench workload's model is
+    bitwise its eager call (c5 at 512 rows: the wide kernel's shape, not its
+    batch, is what the graph must carry)."""
+    import bench
+    model, _, _ = bench.build_model(workload, hip_device)
+    D = bench.WORKLOADS[workload][3]
+    rows = 512 if workload == "c5" else 3000
+    x = torch.randn(rows, D, generator=torch.Generator(device=hip_device).manual_seed(5), device=hip_device)
+    gl = GraphedLogProb(model, x)
+    out = gl().clone()
+    ref = model.log_prob(x)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    flush_status_checks()

@@ -15,3 +15,12 @@ done
 for f in $O/v*.log $O/tree*.log; do echo -n "$f "; grep -h '"value"' $f | python -c "
 import sys,json
 d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['parity']['pass'])"; done
+# fused AR: the staging cursor (no 64-bit division per sub-record) vs HEAD
+run ar_tests 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_nsfar_fused.py || exit $?
+for r in 1 2; do
+  NFK_LIBRARY=build_ab/head/libnfk.so run ar_head_$r 300 python bench.py --workload ar --no-cpu-baseline --parity-rows 2048 || exit $?
+  run ar_tree_$r 300 python bench.py --workload ar --no-cpu-baseline --parity-rows 2048 || exit $?
+done
+for f in $O/ar_*.log; do echo -n "$f "; grep -h '"value"' $f | python -c "
+import sys,json
+d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['parity']['pass'])"; done
