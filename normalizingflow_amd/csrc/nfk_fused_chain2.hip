@@ -20,18 +20,6 @@
 
 #include "nfk_fused_impl.h"
 
-// branch-free map/x reads of layer 1 (L1) and of the spline inputs (XV):
-// build switches for A/B runs
-#ifndef NFK_C2_BF_L1
-#define NFK_C2_BF_L1 1
-#endif
-#ifndef NFK_C2_BF_XV
-#define NFK_C2_BF_XV 1
-#endif
-// epilogue C: the bin's two derivative logits by selects instead of the LDS table
-#ifndef NFK_C2_DSEL
-#define NFK_C2_DSEL 0
-#endif
 
 namespace nfk_fused {
 
@@ -254,13 +242,9 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int k = 8 * q + j;
-#if NFK_C2_BF_L1
                     const bool ok = k < A->n_lo;  // unconditional reads, then selected
                     const float v = xr[c_lo[ok ? k : 0]];
                     e[j] = ok ? v : 0.0f;
-#else
-                    e[j] = k < A->n_lo ? xr[c_lo[k]] : 0.0f;
-#endif
                 }
                 float mx = 0.0f;
 #pragma unroll
@@ -321,7 +305,6 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
             {
                 f32x4 acc[NTL][K];
                 gemm_rec(acc);
-#if NFK_C2_BF_XV
                 // map reads and x reads unconditional (a guarded read became a
                 // branch with its own LDS round trip per coordinate)
                 int tc4[4];
@@ -338,15 +321,6 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                         const float v = xt[(16 * s + sl) * XS + tc4[r]];
                         xv[s][r] = (jj4[r] < A->n_up) ? v : 0.0f;
                     }
-#else
-#pragma unroll
-                for (int r = 0; r < 4; ++r) jj4[r] = jbase + 4 * q + r;
-#pragma unroll
-                for (int s = 0; s < NTL; ++s) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        xv[s][r] = (jj4[r] < A->n_up) ? xt[(16 * s + sl) * XS + c_up[jj4[r]]] : 0.0f;
-#endif
                     knot_phase<K, true, 0, 4, true>(acc[s], xv[s], c, l2e3, kb[s], INV ? ch_k[s] : cw_k[s],
                                                    INV ? h_k[s] : w_k[s], scr + s * K * 64, lane);
                 }
@@ -372,19 +346,10 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                         // epilogue C of k_fused_nsf, op for op
                         const int k = kb[s][r];
                         float raw_k = accd[s][0][r], raw_k1 = accd[s][0][r];
-#if NFK_C2_DSEL
-                        // logits k-1 and k by running selects (no LDS round trip)
-#pragma unroll
-                        for (int j = 1; j < K - 1; ++j) {
-                            raw_k = (k >= j + 1) ? accd[s][j][r] : raw_k;
-                            raw_k1 = (k >= j) ? accd[s][j][r] : raw_k1;
-                        }
-#else
 #pragma unroll
                         for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[s][j][r];
                         raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
                         raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
-#endif
                         const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
                         const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
                         const float d_k = (k == 0) ? c.d_edge : dv_k;
@@ -422,15 +387,11 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                         const bool inside = (x >= c.lo) && (x <= c.hi);
                         const bool live = jj4[r] < A->n_up && row_ok[s];
                         out = inside ? out : x;
-#if NFK_C2_BF_XV
                         // past n_up: the padding column (the map re-read: the
                         // columns held in registers across the epilogues spilled)
                         const bool okc = jj4[r] < A->n_up;
                         const int tcol = okc ? (int)c_up[okc ? jj4[r] : 0] : D;
                         xt[(16 * s + sl) * XS + tcol] = out;
-#else
-                        if (jj4[r] < A->n_up) xt[(16 * s + sl) * XS + c_up[jj4[r]]] = out;
-#endif
                         ldsum[s] += (inside && live) ? lad : 0.0f;
                         any_in |= inside && live;
                         any_nd |= nd && inside && live;
