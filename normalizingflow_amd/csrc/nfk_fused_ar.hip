@@ -67,6 +67,9 @@ constexpr int kArNS = NFK_AR_NS;  // output tiles per sub-record
 constexpr int kArWavesMax = 8;
 constexpr int kArMaxDim = 128;
 
+// T1 = the hidden width's tail kind: 0 none (H = 32 KBH), 1 = 1..4 features
+// (the NSF_CL kernels' f16 tail step), 2 = 5..16 features (a 16-row half tile:
+// two 16x16x32 MFMAs per output tile instead of a padded 32-feature k-block)
 struct ArDims {
     int KBH, T1, HT, P, NO, NH, N3, SPC, NTG, KB1M, SB, PS;
 };
@@ -74,15 +77,15 @@ struct ArDims {
 __host__ __device__ inline ArDims ar_dims(int hidden, int K, int dim) {
     ArDims d{};
     const int kbf = hidden / 32, rem = hidden - 32 * kbf;
-    d.KBH = rem == 0 ? kbf : (rem <= 4 && kbf >= 1 ? kbf : kbf + 1);
-    d.T1 = (rem != 0 && rem <= 4 && kbf >= 1) ? 1 : 0;
-    d.HT = 2 * d.KBH + d.T1;
+    d.T1 = (rem == 0 || kbf < 1) ? 0 : (rem <= 4 ? 1 : (rem <= 16 ? 2 : 0));
+    d.KBH = (rem == 0 || d.T1 != 0) ? kbf : kbf + 1;
+    d.HT = 2 * d.KBH + (d.T1 ? 1 : 0);
     d.P = 3 * K - 1;
     d.NO = (d.P + 15) / 16;
     d.NH = (d.HT + kArNS - 1) / kArNS;
     d.N3 = (d.NO + kArNS - 1) / kArNS;
     d.SPC = 2 * d.NH + d.N3;
-    d.NTG = d.T1 ? (kArNS + 1) / 2 : 0;
+    d.NTG = d.T1 == 1 ? (kArNS + 1) / 2 : (d.T1 == 2 ? 2 * kArNS : 0);
     d.KB1M = dim > 1 ? (2 * (dim - 1) + 31) / 32 : 1;
     const int s1 = d.KB1M * kArNS * 2 + 1, s2 = d.KBH * kArNS * 2 + d.NTG + 1;
     d.SB = s1 > s2 ? s1 : s2;
@@ -104,7 +107,7 @@ inline size_t ar_lds_bytes(const ArDims& d, int dim, bool inv, int nw = kArWaves
 #define NFK_AR_SHAPES(X)                                                                        \
     X(1, 0, 4, 2)   /* golden nsfar_d4_k4 (H = 16) */                                            \
     X(1, 0, 8, 2)   /* small test shapes (H <= 32) */                                           \
-    X(3, 0, 10, 4)  /* applications/input/Gaussian.yaml: dim 40, K 10, H 80 */                  \
+    X(2, 2, 10, 4)  /* applications/input/Gaussian.yaml: dim 40, K 10, H 80 (64 + a 16 tail) */ \
     X(3, 1, 8, 4)   /* H = 100 (config.py:40), K 8, dim <= 64 */                                 \
     X(3, 1, 10, 4)  /* H = 100, K 10 */                                                           \
     X(3, 1, 32, 4)  /* config.py defaults: H = 100, K 32 (nsplines), dim <= 64 */
@@ -185,7 +188,34 @@ __device__ int ar_scale_exp(float maxw) {  // 2^s max|W| in [2^14, 2^15)
 template <class ValF, class BiasF>
 __device__ uint32_t ar_sub_word(int blk, int wl, int kbn, int t1, int nt, int T0, float sc, float bsc, ValF val,
                                 BiasF bias) {
-    const int nf = kbn * kArNS * 2, ntg = t1 ? (kArNS + 1) / 2 : 0;
+    const int nf = kbn * kArNS * 2, ntg = t1 == 1 ? (kArNS + 1) / 2 : 0;
+    if (t1 == 2 && blk >= nf) {
+        // 16-feature tail: the bias block first, then per tile {A1, A2}: lane l
+        // (row l & 15, lane group g = l >> 4) element j of A1 = lo (j < 4) / hi
+        // (j >= 4) weight of feature 32 kbn + 4 g + (j & 3), of A2 = hi (j < 4) / 0;
+        // against B1 = {hi, lo} and B2 = {hi, 0} of the half tile's 4 rows
+        if (blk == nf) {
+            const int t = wl >> 4, r = wl & 15;
+            return __float_as_uint(t < nt ? bias(t, r) * bsc : 0.0f);
+        }
+        const int tt = blk - nf - 1;
+        if (tt >= 2 * kArNS) return 0u;
+        const int t = T0 + (tt >> 1), which = tt & 1;
+        if (t >= nt) return 0u;
+        const int lane = wl >> 2, g = lane >> 4, row = lane & 15, jp = 2 * (wl & 3);
+        _Float16 hv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int j = jp + e;
+            const float w = val(t, row, 32 * kbn + 4 * g + (j & 3)) * sc;
+            const _Float16 wh = (_Float16)w;
+            if (which == 0)
+                hv[e] = j < 4 ? (_Float16)(w - (float)wh) : wh;
+            else
+                hv[e] = j < 4 ? wh : (_Float16)0.0f;
+        }
+        return (uint32_t)__builtin_bit_cast(uint16_t, hv[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, hv[1]) << 16);
+    }
     if (blk < nf) {
         const int part = blk & 1, idx = blk >> 1, kb = idx / kArNS, t = T0 + (idx - kb * kArNS);
         if (t >= nt) return 0u;
@@ -214,6 +244,8 @@ __global__ __launch_bounds__(256) void k_ar_pack(ArPackArgs a) {
               s3 = ar_scale_exp(__uint_as_float(hdr[2]));
     const int64_t total = ar_pack_floats(d, a.dim);
     const int H = a.H, kbh = d.KBH;
+    // hidden feature of row r of hidden tile t (the 16-feature half tile: 32 KBH + r)
+    auto hid = [&](int t, int r) { return (d.T1 == 2 && t == 2 * kbh) ? 32 * kbh + r : hid_feature(t, r, kbh); };
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (int64_t)gridDim.x * blockDim.x) {
         if (g < 256) {
@@ -237,12 +269,12 @@ __global__ __launch_bounds__(256) void k_ar_pack(ArPackArgs a) {
             v = ar_sub_word(
                 blk, wl, kb1, 0, d.HT, kArNS * u, ldexpf(1.0f, s1), ldexpf(1.0f, s1 + 14),
                 [&](int t, int r, int k) -> float {
-                    const int f = hid_feature(t, r, kbh);
+                    const int f = hid(t, r);
                     if (f >= H || k >= 2 * i) return 0.0f;
                     return W1[(int64_t)f * 2 * i + (k & 1) * i + (k >> 1)];  // cat(cos, sin) columns
                 },
                 [&](int t, int r) -> float {
-                    const int f = hid_feature(t, r, kbh);
+                    const int f = hid(t, r);
                     return f < H ? b1[f] : 0.0f;
                 });
         } else if (u < 2 * d.NH) {  // layer 2: Linear(H, H)
@@ -251,11 +283,11 @@ __global__ __launch_bounds__(256) void k_ar_pack(ArPackArgs a) {
             v = ar_sub_word(
                 blk, wl, kbh, d.T1, d.HT, kArNS * (u - d.NH), ldexpf(1.0f, s2), ldexpf(1.0f, s2 + 14),
                 [&](int t, int r, int k) -> float {
-                    const int f = hid_feature(t, r, kbh);
+                    const int f = hid(t, r);
                     return (f < H && k < H) ? W2[(int64_t)f * H + k] : 0.0f;
                 },
                 [&](int t, int r) -> float {
-                    const int f = hid_feature(t, r, kbh);
+                    const int f = hid(t, r);
                     return f < H ? b2[f] : 0.0f;
                 });
         } else {  // output layer: Linear(H, 3K-1), row 16 t + r = parameter (W, H, D logits in order)
@@ -303,6 +335,46 @@ __device__ __forceinline__ void ar_parts(const h8 (&bh)[KB], const h8 (&bl)[KB],
     if constexpr (T0 + kArNS < NT) ar_parts<KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end);
 }
 
+// The same over a hidden width with a 16-feature tail (tail kind 2): the full
+// k-blocks by gemm_h (its bias block sits right after them), then per output
+// tile the tail's two MFMAs on B1 = {hi, lo}, B2 = {hi, 0} of the half tile
+template <int KB, int NT, int J, class SlotF, class EndF>
+__device__ __forceinline__ void ar_parts16(const h8 (&bh)[KB], const h8 (&bl)[KB], h8 b1, h8 b2, int lane,
+                                           f32x4 (&acc)[NT], SlotF slot, EndF end) {
+    constexpr int T0 = J * kArNS;
+    constexpr int N = (NT - T0) < kArNS ? (NT - T0) : kArNS;
+    const float4* sl = slot();
+    gemm_h<KB, false, N, kArNS, T0, NT>(bh, bl, h4{0, 0, 0, 0}, sl, lane, acc);
+    const float4* t16 = sl + (KB * kArNS * 2 + 1) * 64;
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        const h8 a1 = __builtin_bit_cast(h8, t16[(2 * t) * 64 + lane]);
+        const h8 a2 = __builtin_bit_cast(h8, t16[(2 * t + 1) * 64 + lane]);
+        acc[T0 + t] = mfma16(a1, b1, acc[T0 + t]);
+        acc[T0 + t] = mfma16(a2, b2, acc[T0 + t]);
+    }
+    end();
+    if constexpr (T0 + kArNS < NT) ar_parts16<KB, NT, J + 1>(bh, bl, b1, b2, lane, acc, slot, end);
+}
+
+// activations of a hidden layer with a 16-feature tail: the full tiles by
+// act_operands, the half tile's 4 rows per lane into B1 = {hi, lo}, B2 = {hi, 0}
+template <int KBH, int HT>
+__device__ __forceinline__ void act_operands16(f32x4 (&h)[HT], float c2, h8 (&bh)[KBH], h8 (&bl)[KBH], h8& b1,
+                                               h8& b2) {
+    h4 unused;
+    act_operands<KBH, false, HT>(h, c2, bh, bl, unused);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float v = tanh_scaled(h[HT - 1][r], c2);
+        const _Float16 hi = (_Float16)v;
+        b1[r] = hi;
+        b1[4 + r] = (_Float16)(v - (float)hi);
+        b2[r] = hi;
+        b2[4 + r] = (_Float16)0.0f;
+    }
+}
+
 // fp16 hi/lo of two trig features (x 2^14, the activations' split scale)
 __device__ __forceinline__ void trig_split(float v, float pi, float bnd, _Float16& ch, _Float16& cl, _Float16& sh,
                                            _Float16& sl) {
@@ -314,12 +386,13 @@ __device__ __forceinline__ void trig_split(float v, float pi, float bnd, _Float1
     sl = (_Float16)(s - (float)sh);
 }
 
-template <int KBH, bool T1, int K, int KBX, bool INV, int NW>
+template <int KBH, int TK, int K, int KBX, bool INV, int NW>
 __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
     constexpr int kArWaves = NW;
-    constexpr int HT = 2 * KBH + (T1 ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
+    constexpr bool T1 = TK == 1;  // the f16 4-feature tail step; TK == 2: the 16-feature tail
+    constexpr int HT = 2 * KBH + (TK ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
     constexpr int NH = (HT + kArNS - 1) / kArNS, N3 = (NO + kArNS - 1) / kArNS, SPC = 2 * NH + N3;
-    constexpr int NTG = T1 ? (kArNS + 1) / 2 : 0;
+    constexpr int NTG = TK == 1 ? (kArNS + 1) / 2 : (TK == 2 ? 2 * kArNS : 0);
     constexpr int PS = 16 * NO + 4, G = ar_group(INV, PS);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -435,14 +508,25 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
                 case 4: if constexpr (KBX >= 4) layer1(std::integral_constant<int, 4>{}); break;
                 default: break;
             }
-            act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
-            {
-                f32x4 h2[HT];
-                ar_parts<KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
-                act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
-            }
             f32x4 o[NO];
-            ar_parts<KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+            if constexpr (TK == 2) {
+                h8 b1, b2;
+                act_operands16<KBH, HT>(h, c21, bh, bl, b1, b2);
+                {
+                    f32x4 h2[HT];
+                    ar_parts16<KBH, HT, 0>(bh, bl, b1, b2, lane, h2, slot, end);
+                    act_operands16<KBH, HT>(h2, c22, bh, bl, b1, b2);
+                }
+                ar_parts16<KBH, NO, 0>(bh, bl, b1, b2, lane, o, slot, end);
+            } else {
+                act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
+                {
+                    f32x4 h2[HT];
+                    ar_parts<KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+                    act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
+                }
+                ar_parts<KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+            }
             // logits (unscaled: the exact power of two) into the slab, [sample][param]
 #pragma unroll
             for (int t = 0; t < NO; ++t) {
@@ -536,14 +620,14 @@ int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
     const dim3 g((unsigned)((a.batch + per - 1) / per)), b(64 * nw);
     if (nw == 8) {
         if (inv)
-            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, true, 8>), g, b, lds, st, a);
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, true, 8>), g, b, lds, st, a);
         else
-            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, false, 8>), g, b, lds, st, a);
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, false, 8>), g, b, lds, st, a);
     } else {
         if (inv)
-            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, true, 4>), g, b, lds, st, a);
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, true, 4>), g, b, lds, st, a);
         else
-            hipLaunchKernelGGL((k_fused_ar<KBH, T1 != 0, K, KBX, false, 4>), g, b, lds, st, a);
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, false, 4>), g, b, lds, st, a);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
