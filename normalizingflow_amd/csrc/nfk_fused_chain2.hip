@@ -239,12 +239,17 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
             for (int s = 0; s < NTL; ++s) {
                 const float* xr = xt + (16 * s + sl) * XS;
                 float e[8];
+                if (A->n_lo >= 32) {  // (uniform) every lane group's 8 inputs exist: plain reads
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int k = 8 * q + j;
-                    const bool ok = k < A->n_lo;  // unconditional reads, then selected
-                    const float v = xr[c_lo[ok ? k : 0]];
-                    e[j] = ok ? v : 0.0f;
+                    for (int j = 0; j < 8; ++j) e[j] = xr[c_lo[8 * q + j]];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = 8 * q + j;
+                        const bool ok = k < A->n_lo;  // unconditional reads, then selected
+                        const float v = xr[c_lo[ok ? k : 0]];
+                        e[j] = ok ? v : 0.0f;
+                    }
                 }
                 float mx = 0.0f;
 #pragma unroll
@@ -307,19 +312,21 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                 gemm_rec(acc);
                 // map reads and x reads unconditional (a guarded read became a
                 // branch with its own LDS round trip per coordinate)
+                // (uniform) n_up a multiple of 16: every chunk's coordinates exist
+                const bool full_up = (A->n_up & 15) == 0;
                 int tc4[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     jj4[r] = jbase + 4 * q + r;
-                    const bool ok = jj4[r] < A->n_up;
-                    tc4[r] = ok ? (int)c_up[ok ? jj4[r] : 0] : D;
+                    const bool ok = full_up || jj4[r] < A->n_up;
+                    tc4[r] = full_up ? (int)c_up[jj4[r]] : (ok ? (int)c_up[ok ? jj4[r] : 0] : D);
                 }
 #pragma unroll
                 for (int s = 0; s < NTL; ++s) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float v = xt[(16 * s + sl) * XS + tc4[r]];
-                        xv[s][r] = (jj4[r] < A->n_up) ? v : 0.0f;
+                        xv[s][r] = (full_up || jj4[r] < A->n_up) ? v : 0.0f;
                     }
                     knot_phase<K, true, 0, 4, true>(acc[s], xv[s], c, l2e3, kb[s], INV ? ch_k[s] : cw_k[s],
                                                    INV ? h_k[s] : w_k[s], scr + s * K * 64, lane);
