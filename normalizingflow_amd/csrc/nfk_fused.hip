@@ -290,8 +290,7 @@ bool wide_ok(int n_lo, int n_up, int H, int K) {
     if (n_lo < 1 || n_up < 1 || H < 1 || K < 2 || (K & 1)) return false;
     const Layout L = make_layout(n_lo, n_up, H, K, 1);
     if (L.T1 != 0 || L.KB1 > L.KBH || n_lo > 16 * ((L.NCH + 1) / 2)) return false;
-    if (wide_wgs<1>() * lds_alloc(wide_lds_bytes(n_lo, n_up, 1)) > (size_t)kLdsBytes) return false;
-    if (wide_wgs<2>() * lds_alloc(wide_lds_bytes(n_lo, n_up, 2)) > (size_t)kLdsBytes) return false;
+    if (kWideWGs * lds_alloc(wide_lds_bytes(n_lo, n_up)) > (size_t)kLdsBytes) return false;
     bool kb = false, kk = false;
 #define CHK_KB(h) kb |= (L.KBH == h);
     NFK_WIDE_KB(CHK_KB)
@@ -325,19 +324,6 @@ int g_chain_form = -1;      // nfk_debug_chain_form
 constexpr int kChainFormDefault = 1;  // nfk_fused_nsf_chain's kernel form
 int g_last_chain_form = -1;           // nfk_debug_last_chain_form
 
-int g_wide_form = -1;                 // nfk_debug_wide_form
-constexpr int kWideFormDefault = 2;   // sample tiles per wave of the wide kernel
-
-// form of the wide kernel: nfk_debug_wide_form, else NFK_WIDE_FORM, else the default
-int wide_form() {
-    if (g_wide_form > 0) return g_wide_form;
-    static const int env = [] {
-        const char* e = std::getenv("NFK_WIDE_FORM");
-        return (e != nullptr && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-    }();
-    return env > 0 ? env : kWideFormDefault;
-}
-
 int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_t st) {
     WideArgs a;
     a.trace = g_trace;
@@ -360,10 +346,9 @@ int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_
     a.mode = f.mode;
     a.NS = wide_substeps(L.KB1, L.KBH, K, L.NCH, &a.S1);
     a.c = f.c;
-    const int form = wide_form();
-    const size_t lds = wide_lds_bytes(L.n_lo, L.n_up, form);
+    const size_t lds = wide_lds_bytes(L.n_lo, L.n_up);
 #define DISPATCH(h, k) \
-    if (L.KBH == h && K == k) return launch_fused_wide<h, k>(a, lds, inv, form, st);
+    if (L.KBH == h && K == k) return launch_fused_wide<h, k>(a, lds, inv, st);
 #define DISPATCH_KB(h) NFK_WIDE_K(DISPATCH, h)
     NFK_WIDE_KB(DISPATCH_KB)
 #undef DISPATCH_KB
@@ -377,16 +362,6 @@ int launch_wide(const FusedArgs& f, const Layout& L, int K, bool inv, hipStream_
 extern "C" int nfk_debug_trace(void* buf) {
     g_trace = static_cast<uint32_t*>(buf);
     return 0;
-}
-
-// Diagnostic: form of the wide kernel (c5-class layers): -1 = automatic
-// (NFK_WIDE_FORM in the environment, else two sample tiles per wave), 1 = one
-// 16-row tile per wave (8-wave workgroups), 2 = two tiles per wave (4-wave
-// workgroups).  Returns the previous setting.  Not part of include/nfk.h.
-extern "C" int nfk_debug_wide_form(int form) {
-    const int prev = g_wide_form;
-    g_wide_form = (form == 1 || form == 2) ? form : -1;
-    return prev;
 }
 
 // Diagnostic: form of k_fused_nsf: -1 = automatic (split where it fits unless

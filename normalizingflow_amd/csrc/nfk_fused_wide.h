@@ -58,18 +58,6 @@ namespace nfk_fused {
 #ifndef NFK_WIDE_PIN
 #define NFK_WIDE_PIN 1
 #endif
-#ifndef NFK_WIDE_PIPE
-#define NFK_WIDE_PIPE 1  // two-tile form: pipelined chunk schedule
-#endif
-#ifndef NFK_WIDE_BAGPR
-#define NFK_WIDE_BAGPR 1
-#endif
-#ifndef NFK_WIDE_SGB
-#define NFK_WIDE_SGB 0  // pipelined schedule: sched_group_barrier pattern (measured: defeats interleaving)
-#endif
-#ifndef NFK_WIDE_FV
-#define NFK_WIDE_FV 2  // pipelined schedule: filler VALU instructions per MFMA
-#endif
 constexpr int kWideFB = NFK_WIDE_FB;             // f16 blocks of a frame
 constexpr int kWideSlotBlocks = kWideFB + 1;     // + the record's bias block
 constexpr int kWideWaves = NFK_WIDE_NW;          // waves per workgroup
@@ -77,20 +65,6 @@ constexpr int kWideWGs = kWideWaves == 4 ? 2 : 1;  // workgroups per CU
 constexpr int kWideTile = 16 * 32;               // floats of a wave's chunk-pair tile
 static_assert(kWideFB == 32 || kWideFB == 64, "frame of 32 or 64 blocks");
 static_assert(kWideWaves == 4 || kWideWaves == 8 || kWideWaves == 12, "4-, 8- or 12-wave workgroups");
-// Two-tile form (NU = 2): every wave owns two 16-row sample tiles, so each A
-// fragment read from the slot feeds the MFMAs of both (half the ds_read_b128
-// bytes per MFMA: the one-tile form's GEMMs ran the LDS array at its 256
-// B/clk/CU peak); one 4-wave workgroup per CU, 512 registers per lane.  The
-// rows of tile u of wave w are those of wave 2w + u of the one-tile form, so
-// both forms are bitwise equal.
-template <int NU>
-__host__ __device__ constexpr int wide_nw() {
-    return NU == 2 ? 4 : kWideWaves;
-}
-template <int NU>
-__host__ __device__ constexpr int wide_wgs() {
-    return NU == 2 ? 1 : kWideWGs;
-}
 
 // k-blocks per sub-record of a record with nt tiles
 __host__ __device__ constexpr int wide_g(int nt, int kbh) {
@@ -111,13 +85,9 @@ struct WideArgs {
     uint32_t* trace;  // diagnostic timeline buffer (NFK_TRACE builds), else unused
 };
 
-// LDS of a workgroup of the form with nu sample tiles per wave (one x tile each)
-// (two-tile form: plus a 16 x 16 buffer of the pair's upper x per tile, the
-// pipelined schedule's spline inputs)
-inline size_t wide_lds_bytes(int n_lo, int n_up, int nu = 1) {
-    const int tiles = nu == 2 ? 2 * wide_nw<2>() : kWideWaves;
+inline size_t wide_lds_bytes(int n_lo, int n_up) {
     return 2 * (size_t)kWideSlotBlocks * 1024 + (size_t)((2 * (n_lo + n_up) + 3) / 4) * 16 +
-           (size_t)tiles * kWideTile * sizeof(float) + (nu == 2 ? (size_t)tiles * 256 * sizeof(float) : 0);
+           (size_t)kWideWaves * kWideTile * sizeof(float);
 }
 
 // sub-steps of one layer: layer 1, layer 2, then per 8-coordinate chunk the
@@ -131,7 +101,7 @@ inline int wide_substeps(int kb1, int kbh, int K, int nch, int* s1) {
 // Copy the frame of sub-step s (if any) into slot s & 1.  The pack holds one
 // frame per sub-step in forward order (W, H, D records per chunk); the
 // inverse searches the heights, so it takes each chunk's H frames first.
-template <int KBH, int K, bool INV, int NW>
+template <int KBH, int K, bool INV>
 __device__ __forceinline__ void wide_stage(const WideArgs& a, int s, float4* slot0, float4* slot1, int wid,
                                            int lane) {
     if (s >= a.NS) return;
@@ -148,18 +118,15 @@ __device__ __forceinline__ void wide_stage(const WideArgs& a, int s, float4* slo
     if (s >= 2) return;  // diagnostic: no copies after the prologue
 #endif
     float4* slot = (s & 1) ? slot1 : slot0;
-    stage_record<NW>(a.pack + 256 + (int64_t)f * (kWideSlotBlocks * 256), kWideSlotBlocks, slot, wid,
+    stage_record<kWideWaves>(a.pack + 256 + (int64_t)f * (kWideSlotBlocks * 256), kWideSlotBlocks, slot, wid,
                              lane);
 }
 
 // GEMM over sub-record J (k-blocks G J .. G J + G - 1, those below nkb) of a
-// record with NT tiles, for the NU sample tiles of this wave (each A fragment
-// feeds all of them); J == 0 starts the accumulators at bias * bscale[u].
-// Per accumulator the products run in the one-tile order (lo hi, hi lo, hi hi).
-template <int KBH, int NT, int J, int NU, bool SB = true, class Mid = int>
-__device__ __forceinline__ void gemm_sub(const h8 (&bh)[NU][KBH], const h8 (&bl)[NU][KBH], const float4* slot,
-                                         int lane, f32x4 (&acc)[NU][NT], int nkb, const float (&bscale)[NU],
-                                         Mid mid = 0) {
+// record with NT tiles; J == 0 starts the accumulators at bias * bscale.
+template <int KBH, int NT, int J>
+__device__ __forceinline__ void gemm_sub(const h8 (&bh)[KBH], const h8 (&bl)[KBH], const float4* slot, int lane,
+                                         f32x4 (&acc)[NT], int nkb, float bscale) {
     constexpr int G = wide_g(NT, KBH);
     constexpr int NPR = (NT + 1) / 2;
     constexpr int N = G * NPR;
@@ -170,9 +137,7 @@ __device__ __forceinline__ void gemm_sub(const h8 (&bh)[NU][KBH], const h8 (&bl)
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const float4 b = bias[t * 4 + q];
-#pragma unroll
-            for (int u = 0; u < NU; ++u)
-                acc[u][t] = f32x4{b.x * bscale[u], b.y * bscale[u], b.z * bscale[u], b.w * bscale[u]};
+            acc[t] = f32x4{b.x * bscale, b.y * bscale, b.z * bscale, b.w * bscale};
         }
     }
     auto blk = [](int i, int j) {  // block j (0..3) of step i: tile pair pr of local k-block kl
@@ -194,42 +159,22 @@ __device__ __forceinline__ void gemm_sub(const h8 (&bh)[NU][KBH], const h8 (&bl)
             for (int j = 0; j < 4; ++j)
                 if (2 * pn + (j >> 1) < NT) ring[(i + 1) & 1][j] = slot[blk(i + 1, j) * 64 + lane];
         }
-        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!std::is_same<Mid, int>::value) {
-            // the filler's second half, in the GEMM's second half (its own
-            // scheduling region: half the epilogue's live values per region)
-            if (i == N / 2) {
-                __builtin_amdgcn_sched_barrier(0);
-                mid();
-            }
-        }
+        __builtin_amdgcn_sched_barrier(0);
         if (kl > 0 && kb >= nkb) continue;
         const float4* r = ring[i & 1];
         const h8 ahi0 = __builtin_bit_cast(h8, r[0]), alo0 = __builtin_bit_cast(h8, r[1]);
         if (two) {
             const h8 ahi1 = __builtin_bit_cast(h8, r[2]), alo1 = __builtin_bit_cast(h8, r[3]);
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                acc[u][t0] = mfma16(alo0, bh[u][kb], acc[u][t0]);
-                acc[u][t0 + 1] = mfma16(alo1, bh[u][kb], acc[u][t0 + 1]);
-            }
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                acc[u][t0] = mfma16(ahi0, bl[u][kb], acc[u][t0]);
-                acc[u][t0 + 1] = mfma16(ahi1, bl[u][kb], acc[u][t0 + 1]);
-            }
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                acc[u][t0] = mfma16(ahi0, bh[u][kb], acc[u][t0]);
-                acc[u][t0 + 1] = mfma16(ahi1, bh[u][kb], acc[u][t0 + 1]);
-            }
+            acc[t0] = mfma16(alo0, bh[kb], acc[t0]);
+            acc[t0 + 1] = mfma16(alo1, bh[kb], acc[t0 + 1]);
+            acc[t0] = mfma16(ahi0, bl[kb], acc[t0]);
+            acc[t0 + 1] = mfma16(ahi1, bl[kb], acc[t0 + 1]);
+            acc[t0] = mfma16(ahi0, bh[kb], acc[t0]);
+            acc[t0 + 1] = mfma16(ahi1, bh[kb], acc[t0 + 1]);
         } else {
-#pragma unroll
-            for (int u = 0; u < NU; ++u) acc[u][t0] = mfma16(alo0, bh[u][kb], acc[u][t0]);
-#pragma unroll
-            for (int u = 0; u < NU; ++u) acc[u][t0] = mfma16(ahi0, bl[u][kb], acc[u][t0]);
-#pragma unroll
-            for (int u = 0; u < NU; ++u) acc[u][t0] = mfma16(ahi0, bh[u][kb], acc[u][t0]);
+            acc[t0] = mfma16(alo0, bh[kb], acc[t0]);
+            acc[t0] = mfma16(ahi0, bl[kb], acc[t0]);
+            acc[t0] = mfma16(ahi0, bh[kb], acc[t0]);
         }
     }
 }
@@ -237,55 +182,22 @@ __device__ __forceinline__ void gemm_sub(const h8 (&bh)[NU][KBH], const h8 (&bl)
 // A whole phase: the GEMM of each of its sub-records (nsub of them, at most
 // KBH/G), each ended by the barrier that recycles its slot and issues the
 // copy of sub-record s + 2.
-struct NoFill {
-    __device__ void operator()(int, int) const {}
-};
-
-// fill(J, part): independent work placed in sub-step J's basic block beside
-// its MFMAs (the pipelined chunk schedule: the previous record's epilogue):
-// part 0 with the GEMM's first half, part 1 with its second half (a
-// scheduling fence between), part 2 after it (result pins, LDS stores: what
-// orders against the GEMM's LDS reads); with a filler the GEMM steps carry
-// no other scheduling barriers, so the scheduler can interleave each half
-template <int KBH, int K, bool INV, int NT, int NU, class Fill = NoFill>
-__device__ __forceinline__ void wide_phase(const WideArgs& a, int& s, int nsub, int nkb, const h8 (&bh)[NU][KBH],
-                                           const h8 (&bl)[NU][KBH], f32x4 (&acc)[NU][NT],
-                                           const float (&bscale)[NU], float4* slot0, float4* slot1, int wid,
-                                           int lane, NfkTrace& tr, Fill fill = Fill{}) {
+template <int KBH, int K, bool INV, int NT>
+__device__ __forceinline__ void wide_phase(const WideArgs& a, int& s, int nsub, int nkb, const h8 (&bh)[KBH],
+                                           const h8 (&bl)[KBH], f32x4 (&acc)[NT], float bscale, float4* slot0,
+                                           float4* slot1, int wid, int lane, NfkTrace& tr) {
     constexpr int NS = KBH / wide_g(NT, KBH);
-    constexpr bool FILL = !std::is_same<Fill, NoFill>::value;
     static_assert(NS <= 8, "at most 8 sub-records per phase");
     auto one = [&](auto Jc) {
         constexpr int J = decltype(Jc)::value;
         if (J < nsub) {
-            if constexpr (FILL) {
-                fill(J, 0);
-                gemm_sub<KBH, NT, J, NU, false>(bh, bl, (s & 1) ? slot1 : slot0, lane, acc, nkb, bscale,
-                                                [&] { fill(J, 1); });
-            } else {
-                gemm_sub<KBH, NT, J, NU>(bh, bl, (s & 1) ? slot1 : slot0, lane, acc, nkb, bscale);
-            }
-            if constexpr (FILL && NFK_WIDE_SGB) {
-                // interleave: per GEMM step its A-fragment reads, then each
-                // MFMA followed by NFK_WIDE_FV filler VALU instructions
-                constexpr int G = wide_g(NT, KBH), NPR = (NT + 1) / 2;
-#pragma unroll
-                for (int i = 0; i < G * NPR; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-                    for (int m = 0; m < 6 * NU; ++m) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x002, NFK_WIDE_FV, 0);
-                    }
-                }
-            }
-            if constexpr (FILL) fill(J, 2);
+            gemm_sub<KBH, NT, J>(bh, bl, (s & 1) ? slot1 : slot0, lane, acc, nkb, bscale);
             NFK_MARK(tr);  // GEMM issued
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             NFK_MARK(tr);  // barrier passed
-            wide_stage<KBH, K, INV, wide_nw<NU>()>(a, s + 2, slot0, slot1, wid, lane);
+            wide_stage<KBH, K, INV>(a, s + 2, slot0, slot1, wid, lane);
             ++s;
         }
     };
@@ -363,33 +275,6 @@ __device__ __forceinline__ void knot_phase_w(const f32x4 (&acc)[K / 2], const fl
     }
 }
 
-// knot_phase_w for coordinate h of this lane group alone (scalar prefixes:
-// bitwise the packed pair form), the pipelined schedule's half-epilogue
-template <int K, bool SEARCH>
-__device__ __forceinline__ void knot_one_w(const f32x4 (&acc)[K / 2], int h, float xv, const FusedConst& c, float l2e,
-                                           int& kb, float& ek, float& sk) {
-    float u[K];
-    int pre[K];
-#pragma unroll
-    for (int p = 0; p < K; ++p) u[p] = acc[p >> 1][2 * h + (p & 1)];
-    const float s2 = nfk_prefix_nsf_lean<K>(u, l2e, c.m2b, c.fb30, c.mb30, pre);
-    const float lo = __builtin_fmaf(s2, 0.0f, c.lo);  // NaN iff the logits were (knot_phase)
-    int p0 = 0, p1 = pre[1 < K ? 1 : 0], k = 0;
-    const int xi = __float2int_rd(__builtin_fmaf(xv, c.inv30, -c.lo * c.inv30));
-#pragma unroll
-    for (int j = 1; j < K; ++j) {
-        const bool ge = SEARCH ? (xi >= pre[j]) : (kb >= j);
-        p0 = ge ? pre[j] : p0;
-        if (j + 1 < K) p1 = ge ? pre[j + 1] : p1;
-        if (SEARCH) k += ge ? 1 : 0;
-    }
-    if (SEARCH) kb = k;
-    const float e = __builtin_fmaf(c.sp30, (float)p0, lo);
-    const float e1 = (kb == K - 1) ? c.hi : __builtin_fmaf(c.sp30, (float)p1, lo);
-    ek = e;
-    sk = e1 - e;
-}
-
 // Pin a knot epilogue's results at its place in the schedule: without it
 // the compiler sinks the searched-knot and other-knot epilogues below the
 // derivative record's GEMMs (only register dependences order them), so the
@@ -430,21 +315,6 @@ __device__ __forceinline__ void wide_gather(const WideArgs& a, const int32_t* m_
     }
 }
 
-// LDS-DMA gather of the upper x of pair g (16 rows x upper coordinates
-// 16 g .. 16 g + 15) into a 16 x 16 buffer: element e = 64 i + lane is (e >> 4, e & 15)
-__device__ __forceinline__ void wide_gather_up(const WideArgs& a, const int32_t* m_up_in, int64_t b0, int g,
-                                               float* xb, int lane) {
-    const uint32_t base = lds_addr(xb);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int e = 64 * i + lane, r = e >> 4, j = 16 * g + (e & 15);
-        const int col = m_up_in[j < a.n_up ? j : 0];
-        int64_t row = b0 + r;
-        if (row >= a.batch) row = a.batch - 1;
-        dma4(a.x + row * a.ldx + col, base + i * 256);
-    }
-}
-
 // z of pair g from the tile (upper coordinates transformed, lower ones passed through)
 __device__ __forceinline__ void wide_store(const WideArgs& a, const int32_t* m_lo_out, const int32_t* m_up_out,
                                            int64_t b0, int nrows, int g, const float* tile, int lane) {
@@ -460,9 +330,8 @@ __device__ __forceinline__ void wide_store(const WideArgs& a, const int32_t* m_l
     }
 }
 
-template <int KBH, int K, bool INV, int NU>
-__global__ __launch_bounds__(64 * wide_nw<NU>(), wide_wgs<NU>()) void k_fused_nsf_wide(WideArgs a) {
-    constexpr int NW = wide_nw<NU>();
+template <int KBH, int K, bool INV>
+__global__ __launch_bounds__(64 * kWideWaves, kWideWGs) void k_fused_nsf_wide(WideArgs a) {
     constexpr int HT = 2 * KBH;
     constexpr int NTC = K / 2;  // tiles of a chunk's W, H or D record
     constexpr int S2 = KBH / wide_g(HT, KBH);
@@ -478,53 +347,38 @@ __global__ __launch_bounds__(64 * wide_nw<NU>(), wide_wgs<NU>()) void k_fused_ns
     int32_t* m_up_out = m_up_in + a.n_up;
     int32_t* m_lo_in = m_up_out + a.n_up;
     int32_t* m_lo_out = m_lo_in + a.n_lo;
-    float* tiles0 = reinterpret_cast<float*>(lds4 + 2 * kWideSlotBlocks * 64 + (2 * (a.n_lo + a.n_up) + 3) / 4);
-    float* tiles = tiles0 + wid * NU * kWideTile;  // x tile of sample tile u: tiles + u * kWideTile
-    // two-tile form: upper x of the current pair, 16 x 16 per tile
-    float* xbuf = tiles0 + NW * NU * kWideTile + wid * NU * 256;
-    int64_t b0[NU];
-    int nrows[NU];
-    bool row_ok[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        b0[u] = (((int64_t)blockIdx.x * NW + wid) * NU + u) * 16;
-        const int64_t rem = a.batch - b0[u];
-        nrows[u] = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
-        row_ok[u] = sl < nrows[u];
-    }
+    float* tile = reinterpret_cast<float*>(lds4 + 2 * kWideSlotBlocks * 64 + (2 * (a.n_lo + a.n_up) + 3) / 4) +
+                  wid * kWideTile;
+    const int64_t b0 = ((int64_t)blockIdx.x * kWideWaves + wid) * 16;
+    const int64_t rem = a.batch - b0;
+    const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
+    const bool row_ok = sl < nrows;
     const FusedConst c = a.c;  // by value: SGPRs
     const float* pk = a.pack;
     NfkTrace tr;
     NFK_MARK(tr);  // start
 
     // ---- prologue: index maps (plain loads, no copy in flight yet)
-    for (int i = threadIdx.x; i < a.n_up; i += 64 * NW) {
+    for (int i = threadIdx.x; i < a.n_up; i += 64 * kWideWaves) {
         m_up_in[i] = a.up_in[i];
         m_up_out[i] = a.up_out[i];
     }
-    for (int i = threadIdx.x; i < a.n_lo; i += 64 * NW) {
+    for (int i = threadIdx.x; i < a.n_lo; i += 64 * kWideWaves) {
         m_lo_in[i] = a.lo_in[i];
         m_lo_out[i] = a.lo_out[i];
     }
     const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
     __syncthreads();
     int s = 0;
-    wide_stage<KBH, K, INV, NW>(a, 0, slot0, slot1, wid, lane);
-    wide_stage<KBH, K, INV, NW>(a, 1, slot0, slot1, wid, lane);
-#pragma unroll
-    for (int u = 0; u < NU; ++u) wide_gather(a, m_lo_in, m_up_in, b0[u], 0, tiles + u * kWideTile, lane);
-    if constexpr (NU == 2 && NFK_WIDE_PIPE)
-#pragma unroll
-        for (int u = 0; u < NU; ++u) wide_gather_up(a, m_up_in, b0[u], 0, xbuf + u * 256, lane);
+    wide_stage<KBH, K, INV>(a, 0, slot0, slot1, wid, lane);
+    wide_stage<KBH, K, INV>(a, 1, slot0, slot1, wid, lane);
+    wide_gather(a, m_lo_in, m_up_in, b0, 0, tile, lane);
 
     // layer-1 operands: x at the lower coordinates of sample sl, k = 32 kb + 8 q + j
-    // (per sample tile: its own power-of-two scale, as one wave of the one-tile form)
-    h8 bh[NU][KBH], bl[NU][KBH];
-    float unx[NU], bsc[NU], ones[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        ones[u] = 1.0f;
-        int64_t row = b0[u] + sl;
+    h8 bh[KBH], bl[KBH];
+    float unx, bsc;
+    {
+        int64_t row = b0 + sl;
         if (row >= a.batch) row = a.batch - 1;
         const float* xr = a.x + row * a.ldx;
         float xv[KBH][8];
@@ -542,360 +396,158 @@ __global__ __launch_bounds__(64 * wide_nw<NU>(), wide_wgs<NU>()) void k_fused_ns
         int ex = 0;
         if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
         const float sx = ldexpf(1.0f, 14 - ex);
-        unx[u] = ldexpf(un1, ex - 14);
-        bsc[u] = sx / un1;  // bias b1 2^(s1 + sx): the epilogue only multiplies by 2^-(s1 + sx)
+        unx = ldexpf(un1, ex - 14);
+        bsc = sx / un1;  // bias b1 2^(s1 + sx): the epilogue only multiplies by 2^-(s1 + sx)
 #pragma unroll
         for (int kb = 0; kb < KBH; ++kb)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float v = xv[kb][j] * sx;
                 const _Float16 hh = (_Float16)v;
-                bh[u][kb][j] = hh;
-                bl[u][kb][j] = (_Float16)(v - (float)hh);
+                bh[kb][j] = hh;
+                bl[kb][j] = (_Float16)(v - (float)hh);
             }
     }
-    dma_barrier();  // sub-records 0, 1 and the first x tiles landed
+    dma_barrier();  // sub-records 0, 1 and the first x tile landed
     NFK_MARK(tr);  // prologue done
 
     // ---- layer 1 (S1 sub-steps) and layer 2 (S2 sub-steps)
+    h4 btail;
     {
-        h4 btail;
-        f32x4 h[NU][HT];
-        wide_phase<KBH, K, INV, HT, NU>(a, s, a.S1, a.KB1, bh, bl, h, bsc, slot0, slot1, wid, lane, tr);
-#pragma unroll
-        for (int u = 0; u < NU; ++u) act_operands<KBH, false, HT>(h[u], -2.0f * kL2E * unx[u], bh[u], bl[u], btail);
-        wide_phase<KBH, K, INV, HT, NU>(a, s, S2, KBH, bh, bl, h, ones, slot0, slot1, wid, lane, tr);
-#pragma unroll
-        for (int u = 0; u < NU; ++u) act_operands<KBH, false, HT>(h[u], -2.0f * kL2E * un2, bh[u], bl[u], btail);
-#if NFK_WIDE_BAGPR
-        // two-tile pipelined form: the output layer's B operands live in
-        // AGPRs (MFMA sources may be AGPRs), leaving the VGPRs to the
-        // epilogue the schedule interleaves with the GEMM
-        if constexpr (NU == 2 && NFK_WIDE_PIPE)
-#pragma unroll
-            for (int u = 0; u < NU; ++u)
-#pragma unroll
-                for (int kb = 0; kb < KBH; ++kb) asm volatile("" : "+a"(bh[u][kb]), "+a"(bl[u][kb]));
-#endif
+        f32x4 h[HT];
+        wide_phase<KBH, K, INV, HT>(a, s, a.S1, a.KB1, bh, bl, h, bsc, slot0, slot1, wid, lane, tr);
+        act_operands<KBH, false, HT>(h, -2.0f * kL2E * unx, bh, bl, btail);
+        wide_phase<KBH, K, INV, HT>(a, s, S2, KBH, bh, bl, h, 1.0f, slot0, slot1, wid, lane, tr);
+        act_operands<KBH, false, HT>(h, -2.0f * kL2E * un2, bh, bl, btail);
     }
 
     const float l2e3 = kL2E * un3;
-    float ldsum[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) ldsum[u] = 0.0f;
+    float ldsum = 0.0f;
     bool any_in = false, any_nd = false;
-    if constexpr (NU == 2 && NFK_WIDE_PIPE) {
-        // Pipelined chunk schedule: a record's spline epilogue runs beside the
-        // NEXT record's GEMM (fill), tile u's in sub-step u (both in sub-step
-        // 0 of one-sub-step records): A(ch) GEMM | C(ch-1) epilogue, B(ch) |
-        // A(ch), C(ch) | B(ch).  Same arithmetic, so bitwise the other forms.
-        // The searched phase reads x from xbuf (the pair's upper x, gathered a
-        // phase ahead), so the z tile of a pair can be stored and refilled
-        // while the next pair's first epilogues run.
-        int kb[NU][2];
-        float xv[NU][2], cw_k[NU][2], w_k[NU][2], ch_k[NU][2], h_k[NU][2];
-        f32x4 accA[NU][NTC], accB[NU][NTC], accC[NU][NTC];
-        float zout[NU][2];
-        // pins: the epilogue's inputs and results pass through empty volatile
-        // asm at the start and end of its pieces, so the optimiser cannot move
-        // the (side-effect free) epilogue out of the GEMM's regions
-        auto pin_in = [](f32x4 (&v)[NTC], int h) {
-#pragma unroll
-            for (int t = 0; t < NTC; ++t)
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    float e = v[t][2 * h + r];
-                    asm volatile("" : "+v"(e));
-                    v[t][2 * h + r] = e;
-                }
-        };
-        // the pieces of sub-step J's filler: part 0 (beside the GEMM's first
-        // half) and part 1 (its second half) are (tile, coordinate) pieces,
-        // part 2 the closing pins/stores per tile.  Two-sub-step records
-        // (K = 16): tile J, coordinate = part; one-sub-step records: tile =
-        // part, both coordinates.
-        auto pieces = [&](int J, int part, auto&& f) {
-            if (SC == 1) {
-                if (part < 2) {
-                    f(part, 0, false);
-                    f(part, 1, false);
-                } else {
-                    f(0, 0, true);
-                    f(1, 0, true);
-                }
-            } else if (J < 2) {
-                f(J, part < 2 ? part : 0, part == 2);
-            }
-        };
-        auto epi_a = [&](int u, int h, bool fin) {
-            if (fin) {
-                wide_pin(kb[u], INV ? ch_k[u] : cw_k[u], INV ? h_k[u] : w_k[u]);
-                return;
-            }
-            pin_in(accA[u], h);
-            knot_one_w<K, true>(accA[u], h, xv[u][h], c, l2e3, kb[u][h], INV ? ch_k[u][h] : cw_k[u][h],
-                                INV ? h_k[u][h] : w_k[u][h]);
-        };
-        // chunk ch's spline inputs from xbuf, read at the end of its searched
-        // record's GEMM (the epilogue that needs them runs in the next phase)
-        auto read_xv = [&](int ch, int u) {
-            const float2 v = *reinterpret_cast<const float2*>(xbuf + u * 256 + sl * 16 + 8 * (ch & 1) + 2 * q);
-            xv[u][0] = 8 * ch + 2 * q < a.n_up ? v.x : 0.0f;
-            xv[u][1] = 8 * ch + 2 * q + 1 < a.n_up ? v.y : 0.0f;
-            asm volatile("" : "+v"(xv[u][0]), "+v"(xv[u][1]));
-        };
-        auto epi_b = [&](int u, int h, bool fin) {
-            if (fin) {
-                wide_pin(kb[u], INV ? cw_k[u] : ch_k[u], INV ? w_k[u] : h_k[u]);
-                return;
-            }
-            pin_in(accB[u], h);
-            knot_one_w<K, false>(accB[u], h, xv[u][h], c, l2e3, kb[u][h], INV ? cw_k[u][h] : ch_k[u][h],
-                                 INV ? w_k[u][h] : h_k[u][h]);
-        };
-        auto epi_c = [&](int ch, int u, int h, bool fin) {
-            if (fin) {
-                asm volatile("" : "+v"(ldsum[u]), "+v"(zout[u][0]), "+v"(zout[u][1]));
-                float* tw = tiles + u * kWideTile + sl * 32 + 2 * (8 * (ch & 1) + 2 * q) + 1;
-                tw[0] = zout[u][0];  // z back into the upper columns
-                tw[2] = zout[u][1];
-                return;
-            }
-            pin_in(accC[u], h);
-            const int k = kb[u][h];
-            float raw_k = accC[u][0][2 * h], raw_k1 = accC[u][0][2 * h];
-#pragma unroll
-            for (int j = 1; j < K - 1; ++j) {
-                const float v = accC[u][j >> 1][2 * h + (j & 1)];
-                raw_k = (k >= j + 1) ? v : raw_k;
-                raw_k1 = (k >= j) ? v : raw_k1;
-            }
-            const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k * un3, c.min_d);
-            const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1 * un3, c.min_d);
-            const float x = xv[u][h];
-            const float wk = w_k[u][h], hk = h_k[u][h], cwk = cw_k[u][h], chk = ch_k[u][h];
-            const float rw = nfk_rcp_fast(wk);
-            const float delta = hk * rw;
-            const float gap = (d_k + d_k1) - 2.0f * delta;
-            float out, th;
-            bool nd = false;
-            if (INV) {
-                const float y = x - chk;
-                const float qa = y * gap + hk * (delta - d_k);
-                const float qb = hk * d_k - y * gap;
-                const float qc = (-delta) * y;
-                const float disc = qb * qb - (4.0f * qa) * qc;
-                nd = !(disc >= 0.0f);
-                const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
-                out = root * wk + cwk;
-                th = root;
-            } else {
-                th = (x - cwk) * rw;
-            }
-            const float t1mt = th * (1.0f - th);
-            const float den = delta + gap * t1mt;
-            if (!INV) {
-                const float num = hk * (delta * (th * th) + d_k * t1mt);
-                out = chk + nfk_div<true>(num, den);
-            }
-            const float omt = 1.0f - th;
-            const float dnum = (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
-            float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
-            lad = INV ? -lad : lad;
-            const bool inside = (x >= c.lo) && (x <= c.hi);
-            const bool live = 8 * ch + 2 * q + h < a.n_up && row_ok[u];
-            zout[u][h] = inside ? out : x;
-            ldsum[u] += (inside && live) ? lad : 0.0f;  // coordinate order: h = 0 first, as the other forms
-            any_in |= inside && live;
-            any_nd |= nd && inside && live;
-        };
-        for (int ch = 0; ch < a.NCH; ++ch) {
-            const int g = ch >> 1;
-            if (ch == 0) {
-                wide_phase<KBH, K, INV, NTC, NU>(a, s, SC, KBH, bh, bl, accA, ones, slot0, slot1, wid, lane, tr,
-                                                 [&](int J, int part) {
-                                                     pieces(J, part, [&](int u, int, bool f) {
-                                                         if (f) read_xv(0, u);
-                                                     });
-                                                 });
-            } else {
-                wide_phase<KBH, K, INV, NTC, NU>(a, s, SC, KBH, bh, bl, accA, ones, slot0, slot1, wid, lane, tr,
-                                                 [&](int J, int part) {
-                                                     pieces(J, part, [&](int u, int h, bool f) {
-                                                         epi_c(ch - 1, u, h, f);
-                                                         if (f) read_xv(ch, u);
-                                                     });
-                                                 });
-                if (!(ch & 1)) {
-                    // pair g - 1 complete: its z out, pair g's x into the tile
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (int u = 0; u < NU; ++u)
-                        wide_store(a, m_lo_out, m_up_out, b0[u], nrows[u], g - 1, tiles + u * kWideTile, lane);
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (int u = 0; u < NU; ++u)
-                        wide_gather(a, m_lo_in, m_up_in, b0[u], g, tiles + u * kWideTile, lane);
-                }
-            }
-            wide_phase<KBH, K, INV, NTC, NU>(a, s, SC, KBH, bh, bl, accB, ones, slot0, slot1, wid, lane, tr,
-                                             [&](int J, int part) { pieces(J, part, [&](int u, int h, bool f) { epi_a(u, h, f); }); });
-            if ((ch & 1) && ch + 1 < a.NCH) {
-                // xbuf's last reader (the searched epilogue of ch) is done: pair g + 1's upper x
-#pragma unroll
-                for (int u = 0; u < NU; ++u) wide_gather_up(a, m_up_in, b0[u], g + 1, xbuf + u * 256, lane);
-            }
-            wide_phase<KBH, K, INV, NTC, NU>(a, s, SC, KBH, bh, bl, accC, ones, slot0, slot1, wid, lane, tr,
-                                             [&](int J, int part) { pieces(J, part, [&](int u, int h, bool f) { epi_b(u, h, f); }); });
-        }
-        // the last chunk's derivative epilogue, then the last pair's z
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            epi_c(a.NCH - 1, u, 0, false);
-            epi_c(a.NCH - 1, u, 1, false);
-            epi_c(a.NCH - 1, u, 0, true);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int u = 0; u < NU; ++u)
-            wide_store(a, m_lo_out, m_up_out, b0[u], nrows[u], (a.NCH - 1) >> 1, tiles + u * kWideTile, lane);
-    } else
     for (int ch = 0; ch < a.NCH; ++ch) {
         const int g = ch >> 1;
         // this lane group's coordinates 8 ch + 2 q + h; tile column of upper coordinate
         const int tcol = 2 * (8 * (ch & 1) + 2 * q) + 1;
         int jj[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) jj[h] = 8 * ch + 2 * q + h;
-        float xv[NU][2];
-        int kb[NU][2];
-        float cw_k[NU][2], w_k[NU][2], ch_k[NU][2], h_k[NU][2];
+        float xv[2];
+        int kb[2];
+        float cw_k[2], w_k[2], ch_k[2], h_k[2];
 
         // ---- searched knots (widths forward / heights inverse)
         {
-            f32x4 acc[NU][NTC];
-            wide_phase<KBH, K, INV, NTC, NU>(a, s, SC, KBH, bh, bl, acc, ones, slot0, slot1, wid, lane, tr);
+            f32x4 acc[NTC];
+            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, acc, 1.0f, slot0, slot1, wid, lane, tr);
+            const float4 u = *reinterpret_cast<const float4*>(tile + sl * 32 + tcol - 1);
+            xv[0] = u.y;
+            xv[1] = u.w;
 #pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const float4 v = *reinterpret_cast<const float4*>(tiles + u * kWideTile + sl * 32 + tcol - 1);
-                xv[u][0] = jj[0] < a.n_up ? v.y : 0.0f;
-                xv[u][1] = jj[1] < a.n_up ? v.w : 0.0f;
-                knot_phase_w<K, true>(acc[u], xv[u], c, l2e3, kb[u], INV ? ch_k[u] : cw_k[u], INV ? h_k[u] : w_k[u]);
-                wide_pin(kb[u], INV ? ch_k[u] : cw_k[u], INV ? h_k[u] : w_k[u]);
+            for (int h = 0; h < 2; ++h) {
+                jj[h] = 8 * ch + 2 * q + h;
+                if (jj[h] >= a.n_up) xv[h] = 0.0f;
             }
+            knot_phase_w<K, true>(acc, xv, c, l2e3, kb, INV ? ch_k : cw_k, INV ? h_k : w_k);
+            wide_pin(kb, INV ? ch_k : cw_k, INV ? h_k : w_k);
             NFK_MARK(tr);  // epilogue A
         }
         // ---- the other knots, selected at the bin
         {
-            f32x4 acc[NU][NTC];
-            wide_phase<KBH, K, INV, NTC, NU>(a, s, SC, KBH, bh, bl, acc, ones, slot0, slot1, wid, lane, tr);
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                knot_phase_w<K, false>(acc[u], xv[u], c, l2e3, kb[u], INV ? cw_k[u] : ch_k[u], INV ? w_k[u] : h_k[u]);
-                wide_pin(kb[u], INV ? cw_k[u] : ch_k[u], INV ? w_k[u] : h_k[u]);
-            }
+            f32x4 acc[NTC];
+            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, acc, 1.0f, slot0, slot1, wid, lane, tr);
+            knot_phase_w<K, false>(acc, xv, c, l2e3, kb, INV ? cw_k : ch_k, INV ? w_k : h_k);
+            wide_pin(kb, INV ? cw_k : ch_k, INV ? w_k : h_k);
             NFK_MARK(tr);  // epilogue B
         }
         // ---- derivatives of the bin, evaluate, log|det|
         {
-            f32x4 accd[NU][NTC];
-            wide_phase<KBH, K, INV, NTC, NU>(a, s, SC, KBH, bh, bl, accd, ones, slot0, slot1, wid, lane, tr);
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                float outv[2];
+            f32x4 accd[NTC];
+            wide_phase<KBH, K, INV, NTC>(a, s, SC, KBH, bh, bl, accd, 1.0f, slot0, slot1, wid, lane, tr);
+            float outv[2];
 #ifdef NFK_WABL_NOEPI
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    float v = cw_k[u][h] + w_k[u][h] + ch_k[u][h] + h_k[u][h];
+            for (int h = 0; h < 2; ++h) {
+                float v = cw_k[h] + w_k[h] + ch_k[h] + h_k[h];
 #pragma unroll
-                    for (int t = 0; t < NTC; ++t) v += accd[u][t][2 * h] + accd[u][t][2 * h + 1];
-                    outv[h] = v;
-                    ldsum[u] += v;
-                    any_in = true;
-                }
-                if (false)
+                for (int t = 0; t < NTC; ++t) v += accd[t][2 * h] + accd[t][2 * h + 1];
+                outv[h] = v;
+                ldsum += v;
+                any_in = true;
+            }
+            if (false)
 #endif
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    // derivative logit j in register 2h + (j & 1) of tile j >> 1;
-                    // padded index j+1 holds logit j (utils.py:36-39): raw_k = logit k-1, raw_k1 = logit k
-                    const int k = kb[u][h];
-                    float raw_k = accd[u][0][2 * h], raw_k1 = accd[u][0][2 * h];
+            for (int h = 0; h < 2; ++h) {
+                // derivative logit j in register 2h + (j & 1) of tile j >> 1;
+                // padded index j+1 holds logit j (utils.py:36-39): raw_k = logit k-1, raw_k1 = logit k
+                const int k = kb[h];
+                float raw_k = accd[0][2 * h], raw_k1 = accd[0][2 * h];
 #pragma unroll
-                    for (int j = 1; j < K - 1; ++j) {
-                        const float v = accd[u][j >> 1][2 * h + (j & 1)];
-                        raw_k = (k >= j + 1) ? v : raw_k;
-                        raw_k1 = (k >= j) ? v : raw_k1;
-                    }
-                    const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k * un3, c.min_d);
-                    const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1 * un3, c.min_d);
-                    const float x = xv[u][h];
-                    const float wk = w_k[u][h], hk = h_k[u][h], cwk = cw_k[u][h], chk = ch_k[u][h];
-                    const float rw = nfk_rcp_fast(wk);
-                    const float delta = hk * rw;
-                    const float gap = (d_k + d_k1) - 2.0f * delta;
-                    float out, th;
-                    bool nd = false;
-                    if (INV) {
-                        const float y = x - chk;
-                        const float qa = y * gap + hk * (delta - d_k);
-                        const float qb = hk * d_k - y * gap;
-                        const float qc = (-delta) * y;
-                        const float disc = qb * qb - (4.0f * qa) * qc;
-                        nd = !(disc >= 0.0f);
-                        const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
-                        out = root * wk + cwk;
-                        th = root;
-                    } else {
-                        th = (x - cwk) * rw;
-                    }
-                    const float t1mt = th * (1.0f - th);
-                    const float den = delta + gap * t1mt;
-                    if (!INV) {
-                        const float num = hk * (delta * (th * th) + d_k * t1mt);
-                        out = chk + nfk_div<true>(num, den);
-                    }
-                    const float omt = 1.0f - th;
-                    const float dnum =
-                        (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
-                    float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
-                    lad = INV ? -lad : lad;
-                    const bool inside = (x >= c.lo) && (x <= c.hi);
-                    const bool live = jj[h] < a.n_up && row_ok[u];
-                    outv[h] = inside ? out : x;
-                    ldsum[u] += (inside && live) ? lad : 0.0f;
-                    any_in |= inside && live;
-                    any_nd |= nd && inside && live;
+                for (int j = 1; j < K - 1; ++j) {
+                    const float v = accd[j >> 1][2 * h + (j & 1)];
+                    raw_k = (k >= j + 1) ? v : raw_k;
+                    raw_k1 = (k >= j) ? v : raw_k1;
                 }
-                float* tw = tiles + u * kWideTile + sl * 32 + tcol;
-                tw[0] = outv[0];  // z back into the upper columns
-                tw[2] = outv[1];
+                const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k * un3, c.min_d);
+                const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1 * un3, c.min_d);
+                const float x = xv[h];
+                const float rw = nfk_rcp_fast(w_k[h]);
+                const float delta = h_k[h] * rw;
+                const float gap = (d_k + d_k1) - 2.0f * delta;
+                float out, th;
+                bool nd = false;
+                if (INV) {
+                    const float y = x - ch_k[h];
+                    const float qa = y * gap + h_k[h] * (delta - d_k);
+                    const float qb = h_k[h] * d_k - y * gap;
+                    const float qc = (-delta) * y;
+                    const float disc = qb * qb - (4.0f * qa) * qc;
+                    nd = !(disc >= 0.0f);
+                    const float root = nfk_div<true>(2.0f * qc, -qb - sqrtf(disc));
+                    out = root * w_k[h] + cw_k[h];
+                    th = root;
+                } else {
+                    th = (x - cw_k[h]) * rw;
+                }
+                const float t1mt = th * (1.0f - th);
+                const float den = delta + gap * t1mt;
+                if (!INV) {
+                    const float num = h_k[h] * (delta * (th * th) + d_k * t1mt);
+                    out = ch_k[h] + nfk_div<true>(num, den);
+                }
+                const float omt = 1.0f - th;
+                const float dnum =
+                    (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+                float lad = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
+                lad = INV ? -lad : lad;
+                const bool inside = (x >= c.lo) && (x <= c.hi);
+                const bool live = jj[h] < a.n_up && row_ok;
+                outv[h] = inside ? out : x;
+                ldsum += (inside && live) ? lad : 0.0f;
+                any_in |= inside && live;
+                any_nd |= nd && inside && live;
             }
+            float* tw = tile + sl * 32 + tcol;
+            tw[0] = outv[0];  // z back into the upper columns
+            tw[2] = outv[1];
             NFK_MARK(tr);  // epilogue C
         }
         // after a chunk pair: its z, then the next pair's x into the same tile
         // (the stores' data left the tile before the copy is issued)
         if ((ch & 1) || ch + 1 == a.NCH) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int u = 0; u < NU; ++u)
-                wide_store(a, m_lo_out, m_up_out, b0[u], nrows[u], g, tiles + u * kWideTile, lane);
+            wide_store(a, m_lo_out, m_up_out, b0, nrows, g, tile, lane);
             if (ch + 1 < a.NCH) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int u = 0; u < NU; ++u)
-                    wide_gather(a, m_lo_in, m_up_in, b0[u], g + 1, tiles + u * kWideTile, lane);
+                wide_gather(a, m_lo_in, m_up_in, b0, g + 1, tile, lane);
             }
         }
     }
 
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        float v = ldsum[u];
+    {
+        float v = ldsum;
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        if (q == 0 && row_ok[u] && a.mode != 0) {
-            float* dst = a.logdet + b0[u] + sl;
+        if (q == 0 && row_ok && a.mode != 0) {
+            float* dst = a.logdet + b0 + sl;
             *dst = (a.mode == 2) ? (*dst + v) : v;
         }
     }
@@ -912,33 +564,23 @@ __global__ __launch_bounds__(64 * wide_nw<NU>(), wide_wgs<NU>()) void k_fused_ns
 #endif
 }
 
-// form: 1 = one sample tile per wave (kWideWaves-wave workgroups), 2 = two
 template <int KBH, int K>
-int launch_fused_wide(const WideArgs& a, size_t lds, bool inv, int form, hipStream_t st) {
-    const int nw = form == 2 ? wide_nw<2>() : wide_nw<1>();
-    const int64_t per_block = (int64_t)nw * 16 * (form == 2 ? 2 : 1);
+int launch_fused_wide(const WideArgs& a, size_t lds, bool inv, hipStream_t st) {
+    const int64_t per_block = (int64_t)kWideWaves * 16;
     const int64_t blocks = (a.batch + per_block - 1) / per_block;
     if (blocks == 0) return 0;
-    const dim3 grid((unsigned)blocks), block(64 * nw);
-    if (form == 2) {
-        if (inv)
-            hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, true, 2>), grid, block, lds, st, a);
-        else
-            hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, false, 2>), grid, block, lds, st, a);
-    } else {
-        if (inv)
-            hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, true, 1>), grid, block, lds, st, a);
-        else
-            hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, false, 1>), grid, block, lds, st, a);
-    }
+    if (inv)
+        hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, true>), dim3((unsigned)blocks), dim3(64 * kWideWaves), lds, st, a);
+    else
+        hipLaunchKernelGGL((k_fused_nsf_wide<KBH, K, false>), dim3((unsigned)blocks), dim3(64 * kWideWaves), lds, st, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 
 #define NFK_WIDE_INSTANCE(KBH, K) \
-    template int launch_fused_wide<KBH, K>(const WideArgs& a, size_t lds, bool inv, int form, hipStream_t st);
+    template int launch_fused_wide<KBH, K>(const WideArgs& a, size_t lds, bool inv, hipStream_t st);
 #define NFK_WIDE_EXTERN(KBH, K) \
-    extern template int launch_fused_wide<KBH, K>(const WideArgs& a, size_t lds, bool inv, int form, hipStream_t st);
+    extern template int launch_fused_wide<KBH, K>(const WideArgs& a, size_t lds, bool inv, hipStream_t st);
 
 // hidden widths H = 32 KBH (no f32 tail), bins K
 #define NFK_WIDE_KB(X) X(4) X(8)

@@ -12,7 +12,7 @@ import torch
 
 import nf.flows as nff
 import nf.models as nfm
-from normalizingflow_amd import _lib, config
+from normalizingflow_amd import config
 from normalizingflow_amd import kernels as K_
 from oracle import nf_oracle as orc
 
@@ -20,14 +20,6 @@ pytestmark = pytest.mark.gpu
 
 Z_RTOL, Z_ATOL = 1e-5, 5e-5
 LD_RTOL, LD_ATOL = 1e-5, 3e-4
-
-
-@pytest.fixture
-def wide_form():
-    lib = _lib.load()
-    prev = lib.nfk_debug_wide_form(-1)
-    yield lib
-    lib.nfk_debug_wide_form(prev)
 
 
 def close(a, b, rtol, atol):
@@ -120,50 +112,3 @@ def test_c5_prefix_roundtrip_and_determinism(hip_device):
     assert torch.equal(z, z2) and torch.equal(ld_f, ld_f2)
     assert float((xr - x).abs().max()) < 1e-3
     assert float((ld_f + ld_i).abs().max()) < 2e-3
-
-
-@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "s%d_d%d_k%d_h%d_m%s" % (s[0], s[1], s[2], s[3],
-                                                                                 "".join(map(str, s[4]))))
-@pytest.mark.parametrize("inverse", [False, True])
-def test_wide_forms_bitwise(shape, inverse, wide_form, hip_device):
-    """One (8-wave workgroups) and two (4-wave workgroups) 16-row sample tiles
-    per wave: same rows per tile, same products in the same order, so z and
-    log|det| agree bitwise; both against the oracle.  1,000 rows leave the
-    last workgroup of either form partly empty (ragged tiles)."""
-    size, dim, K, hidden, mask = shape
-    torch.manual_seed(size + 7 * K + hidden)
-    layer = nff.NSF_CL(size=size, dim=dim, K=K, B=3, hidden_dim=hidden, mask=mask)
-    x = torch.randn(1000, size * dim, generator=torch.Generator().manual_seed(5)) * 1.3
-    z_ref, ld_ref = orc.nsf_cl(x, cpu_sd(layer), "", size, dim, K, 3, mask, inverse=inverse)
-    dev = layer.to(hip_device)
-    xd = x.to(hip_device)
-    out = {}
-    for f in (1, 2):
-        wide_form.nfk_debug_wide_form(f)
-        with torch.no_grad():
-            z, ld = (dev.inverse(xd) if inverse else dev(xd))
-        assert dev._pack_cache is not None
-        out[f] = (z.cpu(), ld.cpu())
-        close(out[f][0], z_ref, Z_RTOL, Z_ATOL)
-        close(out[f][1], ld_ref, LD_RTOL, LD_ATOL)
-    assert torch.equal(out[1][0], out[2][0]) and torch.equal(out[1][1], out[2][1])
-
-
-def test_c5_forms_bitwise_full_model(wide_form, hip_device):
-    """The 16-layer c5 model at 2^16 + 77 rows (a ragged last workgroup):
-    log_prob, z and the inverse agree bitwise between the two wide forms."""
-    model = _c5_model(16).to(hip_device)
-    model.prior = torch.distributions.MultivariateNormal(torch.zeros(256, device=hip_device),
-                                                        torch.eye(256, device=hip_device))
-    x = torch.randn((1 << 16) + 77, 256, device=hip_device, generator=torch.Generator(hip_device).manual_seed(4))
-    out = {}
-    for f in (1, 2):
-        wide_form.nfk_debug_wide_form(f)
-        with torch.no_grad():
-            lp = model.log_prob(x)
-            z, _, ld = model(x)
-            xr, ldi = model.inverse(z)
-        out[f] = (lp, z, ld, xr, ldi)
-    for a, b in zip(out[1], out[2]):
-        assert torch.equal(a, b)
-    assert torch.isfinite(out[2][0]).all()
