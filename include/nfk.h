@@ -278,6 +278,28 @@ int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* const* wpacks,
                         float prior_half_log_det, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Training forward of a chain of fused NSF_CL layers (forward direction, the
+ * two-tile chain's shapes: nfk_fused_nsf_chain_saved_ok != 0, nlayers >= 2):
+ * nfk_fused_nsf_chain's z and log|det|, and in the same launch the INPUT of
+ * every layer l >= 1 -- what that layer's backward needs (the per-layer
+ * autograd node saves it, nf/models.py:13-20 run under autograd) -- written to
+ * saves + (l - 1) * save_stride, rows of ld_saves floats, in that layer's own
+ * column order (bitwise the z of layer l - 1).
+ *   smaps: DEVICE int32 [(nlayers - 1) * D]: for layer l >= 1 and each of its
+ *          input columns, the tile column holding it (the permutation the
+ *          chain's cmaps compose at the start of layer l).
+ * x, z, saves 16-byte aligned; ldx, ldz, ld_saves, save_stride multiples of 4;
+ * D = n_lo + n_up a multiple of 4.
+ * ------------------------------------------------------------------------- */
+int nfk_fused_nsf_chain_saved_ok(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K, int32_t nlayers);
+int nfk_fused_nsf_chain_saved(const float* x, int64_t ldx, const float* const* wpacks,
+                              const int32_t* cmaps, int32_t nlayers, int32_t n_lo, int32_t n_up,
+                              int32_t hidden, float* z, int64_t ldz, float* logdet,
+                              int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound,
+                              int32_t* status, float* saves, int64_t ld_saves, int64_t save_stride,
+                              const int32_t* smaps, nfk_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Training backward of one fused NSF_CL layer (the VJP of flows.py:227-253,
  * utils.py:58-152 at the layer input x): the conditioner recomputed on the
  * matrix cores as nfk_fused_nsf computes it, and the spline VJP of every

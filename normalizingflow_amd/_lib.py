@@ -84,6 +84,13 @@ SIGNATURES = {
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
         I64, I32, F64, I32, P,          # batch, K, tail_bound, inverse, status
         P, F32, F32, P]),               # log_prob, prior_scale, prior_half_log_det, stream
+    "nfk_fused_nsf_chain_saved_ok": (ctypes.c_int, [I32, I32, I32, I32, I32]),
+    "nfk_fused_nsf_chain_saved": (ctypes.c_int, [
+        P, I64, P, P, I32,              # x, ldx, wpacks, cmaps, nlayers
+        I32, I32, I32,                  # n_lo, n_up, hidden
+        P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
+        I64, I32, F64, P,               # batch, K, tail_bound, status
+        P, I64, I64, P, P]),            # saves, ld_saves, save_stride, smaps, stream
     "nfk_fused_nsf_vjp_pack_elems": (ctypes.c_int64, [I32, I32, I32, I32]),
     "nfk_fused_nsf_vjp_pack": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P, P]),
     "nfk_fused_nsf_vjp": (ctypes.c_int, [

@@ -16,6 +16,12 @@ USE_FUSED      run NSF_CL layers whose conditioner is the stock FCNN through the
 USE_CHAIN      in inference, run consecutive fused NSF_CL layers of one shape as
                one nfk_fused_nsf_chain launch (x resident in LDS across the
                layers); results are bitwise those of the per-layer launches.
+USE_TRAIN_CHAIN training (forward direction under autograd): consecutive fused
+               NSF_CL layers of a two-tile-chain shape run as ONE
+               nfk_fused_nsf_chain_saved launch that also writes each layer's
+               input for its backward (models._ChainFn); off: one autograd
+               node and one launch per layer.  Values and gradients are bitwise
+               those of the per-layer path.
 USE_FUSED_VJP  training: NSF_CL's backward through nfk_fused_nsf_vjp (conditioner
                recompute on the matrix cores + spline VJP in one kernel) where
                the shape is supported; off: recompute GEMMs + nfk_rqs_coupling_bwd.
@@ -29,6 +35,7 @@ USE_FCNN_FWD   training: the stock FCNN's recompute forward (Linear + bias +
 STRICT_CHECKS = True
 USE_FUSED = True
 USE_CHAIN = True
+USE_TRAIN_CHAIN = True
 USE_FUSED_VJP = True
 USE_FCNN_DH = True
 USE_FCNN_FWD = True

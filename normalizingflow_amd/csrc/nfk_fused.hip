@@ -528,6 +528,9 @@ FusedArgs fused_args(const float* x, int64_t ldx, const float* wpack, const int3
     a.nlayers = 1;
     a.log_prob = nullptr;
     a.prior_inv_scale = a.prior_c2pi = a.prior_hld = 0.0f;
+    a.saves = nullptr;
+    a.ld_saves = a.save_stride = 0;
+    a.smaps = nullptr;
     {
         // NSF_CL's spline constants (flows.py:236-237 defaults), evaluated like the
         // reference's Python scalars (nfk_make_const), folded for the fixed-point knots
@@ -652,4 +655,44 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
 #undef DISPATCH_KB
 #undef DISPATCH
     return nfk_set_error("nfk_fused_nsf_chain: no kernel instance");
+}
+
+extern "C" int nfk_fused_nsf_chain_saved_ok(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K,
+                                            int32_t nlayers) {
+    if (!shape_ok(n_lo, n_up, hidden, K) || nlayers < 2) return 0;
+    const Layout L = make_layout(n_lo, n_up, hidden, K);
+    return nlayers <= chain_max_layers(L) && chain2_ok(L, K, nlayers, true) ? 1 : 0;
+}
+
+extern "C" int nfk_fused_nsf_chain_saved(const float* x, int64_t ldx, const float* const* wpacks,
+                                         const int32_t* cmaps, int32_t nlayers, int32_t n_lo, int32_t n_up,
+                                         int32_t hidden, float* z, int64_t ldz, float* logdet,
+                                         int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound,
+                                         int32_t* status, float* saves, int64_t ld_saves, int64_t save_stride,
+                                         const int32_t* smaps, nfk_stream_t stream) {
+    if (!nfk_fused_nsf_chain_saved_ok(n_lo, n_up, hidden, K, nlayers))
+        return nfk_set_error("nfk_fused_nsf_chain_saved: shape or layer count not supported");
+    if (batch < 0) return nfk_set_error("nfk_fused_nsf_chain_saved: bad batch");
+    if (batch == 0) return 0;
+    if (!x || !wpacks || !cmaps || !z || !saves || !smaps)
+        return nfk_set_error("nfk_fused_nsf_chain_saved: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf_chain_saved: null logdet");
+    const int D = n_lo + n_up;
+    if (((uintptr_t)x % 16) != 0 || ((uintptr_t)z % 16) != 0 || ((uintptr_t)saves % 16) != 0 || ldx % 4 != 0 ||
+        ldz % 4 != 0 || ld_saves % 4 != 0 || save_stride % 4 != 0 || ld_saves < D || save_stride < batch * ld_saves)
+        return nfk_set_error("nfk_fused_nsf_chain_saved: x, z and saves rows must be 16-byte aligned");
+    const Layout L = make_layout(n_lo, n_up, hidden, K);
+    FusedArgs a = fused_args(x, ldx, nullptr, nullptr, nullptr, nullptr, nullptr, L, z, ldz, logdet, logdet_mode,
+                             batch, K, tail_bound, status);
+    a.slot_blocks = split_slot_blocks(L);
+    a.xtile = 16 * D + 16;
+    a.packs = wpacks;
+    a.cmaps = cmaps;
+    a.nlayers = nlayers;
+    a.saves = saves;
+    a.ld_saves = ld_saves;
+    a.save_stride = save_stride;
+    a.smaps = smaps;
+    const int rc = launch_chain2(a, L, K, false, (hipStream_t)stream);
+    return rc >= 0 ? rc : nfk_set_error("nfk_fused_nsf_chain_saved: no kernel instance");
 }

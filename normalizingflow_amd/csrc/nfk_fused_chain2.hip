@@ -117,9 +117,15 @@ __device__ __forceinline__ void gemm_parts2(const h8 (&bh)[kC2Tiles][KBH], const
 // LDS of one workgroup: the sub-record slot, the status words and byte maps,
 // each wave's kC2Tiles x [16][D + 1] row tiles, each wave's kC2Tiles bin
 // lookup tables
-inline size_t lds_bytes_chain2(const Layout& L, int nl) {
+// byte maps of the chain: nl layers' input columns + the output map (+ the
+// training form's nl - 1 saved-input maps)
+__host__ __device__ inline int chain2_map_bytes(int nl, int D, bool saved) {
+    return (nl + 1) * D + (saved ? (nl - 1) * D : 0);
+}
+
+inline size_t lds_bytes_chain2(const Layout& L, int nl, bool saved = false) {
     const int D = L.n_lo + L.n_up;
-    return (size_t)split_slot_blocks(L) * 1024 + (size_t)((4 * nl + (nl + 1) * D + 15) / 16) * 16 +
+    return (size_t)split_slot_blocks(L) * 1024 + (size_t)((4 * nl + chain2_map_bytes(nl, D, saved) + 15) / 16) * 16 +
            (size_t)kNsfWaves * kC2Tiles * 16 * (D + 1) * sizeof(float) +
            (size_t)kNsfWaves * kC2Tiles * L.K * 64 * sizeof(int);
 }
@@ -145,8 +151,11 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
     const uint8_t* c_lo = cm;
     const uint8_t* c_up = cm;
     const uint8_t* const c_src = cm + NL * D;
+    const bool saved = A->saves != nullptr;
+    const uint8_t* const c_sav = cm + (NL + 1) * D;  // training form: saved-input maps
     const int XS = D + 1;
-    float* const xbase = reinterpret_cast<float*>(lds4 + A->slot_blocks * 64 + (4 * NL + (NL + 1) * D + 15) / 16);
+    float* const xbase =
+        reinterpret_cast<float*>(lds4 + A->slot_blocks * 64 + (4 * NL + chain2_map_bytes(NL, D, saved) + 15) / 16);
     float* const xt = xbase + wid * NTL * 16 * XS;  // this wave's NTL row tiles
     int* const scr = reinterpret_cast<int*>(xbase + kNsfWaves * NTL * 16 * XS) + wid * NTL * K * 64;
     const float* pk = A->packs[0];
@@ -215,6 +224,8 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
     }
     stage_split<KBH, T1, K, HT>(a, pk, 0, offA, offB, offC, slot, wid, lane);
     for (int i = threadIdx.x; i < (NL + 1) * D; i += 64 * kNsfWaves) cm[i] = (uint8_t)A->cmaps[i];
+    if (saved)
+        for (int i = threadIdx.x; i < (NL - 1) * D; i += 64 * kNsfWaves) cm[(NL + 1) * D + i] = (uint8_t)A->smaps[i];
     if ((int)threadIdx.x < NL) cst[threadIdx.x] = 0;
     dma_barrier();
 
@@ -228,6 +239,19 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
         const FusedConst c = *(const FusedConst*)&A->c;  // by value: SGPRs for the layer
         const float un1 = pk[3], un2 = pk[4], un3 = pk[5];
         bool any_in = false, any_nd = false;
+        if (saved && l > 0) {
+            // training form: this layer's input (the previous layer's z, in its
+            // own column order) for the layer's backward; the tile's last writes
+            // are this wave's own, retired at the barrier that ended the layer
+            const uint8_t* sm = c_sav + (l - 1) * D;
+            float* dst = A->saves + (int64_t)(l - 1) * A->save_stride;
+            for (RowWalk w(lane, D >> 2); w.r < nall; w.next()) {
+                const float* row = xt + w.r * XS;
+                const int o = 4 * w.k;
+                *reinterpret_cast<float4*>(dst + (b0 + w.r) * A->ld_saves + o) =
+                    make_float4(row[sm[o]], row[sm[o + 1]], row[sm[o + 2]], row[sm[o + 3]]);
+            }
+        }
 
         // ---- layer 1 (nfk_fused_impl.h phase 0, per sample tile: the tile's
         // power-of-two input scale)
@@ -463,7 +487,7 @@ int launch_chain2(const FusedArgs& a, const Layout& L, int K, bool inv, hipStrea
     const int64_t per = (int64_t)kNsfWaves * 16 * kC2Tiles;
     const int64_t blocks = (a.batch + per - 1) / per;
     if (blocks == 0) return 0;
-    const size_t lds = lds_bytes_chain2(L, a.nlayers);
+    const size_t lds = lds_bytes_chain2(L, a.nlayers, a.saves != nullptr);
     const dim3 g((unsigned)blocks), b(64 * kNsfWaves);
 #define NFK_C2(h, t, k)                                                                  \
     if (L.KBH == h && L.T1 == t && K == k) {                                             \
@@ -479,12 +503,13 @@ int launch_chain2(const FusedArgs& a, const Layout& L, int K, bool inv, hipStrea
     return -1;  // no instance
 }
 
-bool chain2_ok(const Layout& L, int K, int nl) {
+bool chain2_ok(const Layout& L, int K, int nl, bool saved) {
     bool inst = false;
 #define NFK_C2CHK(h, t, k) inst |= (L.KBH == h && L.T1 == t && K == k);
     NFK_CHAIN2_SHAPES(NFK_C2CHK)
 #undef NFK_C2CHK
-    return inst && L.n_lo <= 32 && 2 * lds_alloc(lds_bytes_chain2(L, nl)) <= (size_t)kLdsBytes;
+    return inst && L.n_lo <= 32 && 2 * lds_alloc(lds_bytes_chain2(L, nl, saved)) <= (size_t)kLdsBytes &&
+           (!saved || (L.n_lo + L.n_up) % 4 == 0);
 }
 
 }  // namespace nfk_fused

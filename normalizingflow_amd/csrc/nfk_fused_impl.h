@@ -289,6 +289,13 @@ struct FusedArgs {
     // log|det|_b (z need not be written then: z may be null)
     float* log_prob;
     float prior_inv_scale, prior_c2pi, prior_hld;
+    // two-tile chain, training form (nfk_fused_nsf_chain_saved): the input of
+    // every layer l >= 1 written to saves + (l - 1) save_stride (rows of
+    // ld_saves floats) through smaps [(nlayers - 1) D] (tile column of each of
+    // that layer's input columns); saves null otherwise
+    float* saves;
+    int64_t ld_saves, save_stride;
+    const int32_t* smaps;
 };
 
 __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
@@ -1425,7 +1432,7 @@ inline bool vjp_ok(int n_lo, int n_up, int H, int K) {
 
 // the two-tile chain (nfk_fused_chain2.hip): c3-class shapes
 int launch_chain2(const FusedArgs& a, const Layout& L, int K, bool inv, hipStream_t st);
-bool chain2_ok(const Layout& L, int K, int nl);
+bool chain2_ok(const Layout& L, int K, int nl, bool saved = false);
 
 // hidden widths: KBH = full fp16 k-blocks of 32, T1 = an f16 tail step of <= 4
 // features (H = 32 KBH + 1..4); H <= 132

@@ -603,6 +603,43 @@ def fused_nsf_chain(x, wpacks, cmaps, nlayers, n_lo, n_up, hidden, z, *, logdet,
            _vec(log_prob, B, "log_prob"), float(prior_scale), float(prior_hld), _stream(dev))
 
 
+_CHAIN_SAVED_OK = {}
+
+
+def fused_nsf_chain_saved_ok(n_lo, n_up, hidden, K, nlayers):
+    """Whether nfk_fused_nsf_chain_saved takes this shape and layer count."""
+    key = (n_lo, n_up, hidden, K, nlayers)
+    ok = _CHAIN_SAVED_OK.get(key)
+    if ok is None:
+        ok = _CHAIN_SAVED_OK[key] = bool(_lib.load().nfk_fused_nsf_chain_saved_ok(n_lo, n_up, hidden, K, nlayers))
+    return ok
+
+
+def fused_nsf_chain_saved(x, wpacks, cmaps, smaps, nlayers, n_lo, n_up, hidden, z, saves, *, logdet,
+                          logdet_mode, K, tail_bound, status=None):
+    """The training forward of a chain (include/nfk.h nfk_fused_nsf_chain_saved):
+    z and log|det| of nlayers fused NSF_CL layers, and saves[l - 1] = the input
+    of layer l >= 1 ([nlayers - 1, batch, D], contiguous rows); smaps: int32
+    device tensor [(nlayers - 1) * D] of the tile columns of those inputs."""
+    dev = _require_hip(x, wpacks, cmaps, smaps, z, saves, logdet, status)
+    B = x.shape[0]
+    D = n_lo + n_up
+    if wpacks.dtype != torch.int64 or wpacks.numel() != nlayers:
+        raise ValueError("wpacks must hold %d int64 pack pointers" % nlayers)
+    _vec(cmaps, nlayers * D + D, "cmaps", torch.int32)
+    _vec(smaps, (nlayers - 1) * D, "smaps", torch.int32)
+    if saves.dtype != F32 or saves.dim() != 3 or tuple(saves.shape) != (nlayers - 1, B, D) or \
+            saves.stride(2) != 1:
+        raise ValueError("saves must be a float32 [%d, %d, %d] tensor with unit column stride"
+                         % (nlayers - 1, B, D))
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    _timed("nfk_fused_nsf_chain_saved", dev, "nfk_fused_nsf_chain_saved", xp, ldx, wpacks.data_ptr(),
+           cmaps.data_ptr(), nlayers, n_lo, n_up, hidden, zp, ldz, _vec(logdet, B, "logdet"), logdet_mode, B, K,
+           float(tail_bound), _vec(status, nlayers, "status", torch.int32), saves.data_ptr(), saves.stride(1),
+           saves.stride(0), smaps.data_ptr(), _stream(dev))
+
+
 def fused_realnvp_supported(half_dim, hidden):
     return bool(_lib.load().nfk_fused_realnvp_supported(half_dim, hidden))
 

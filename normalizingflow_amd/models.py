@@ -85,6 +85,72 @@ def _compose_maps(run, D, device):
     return torch.tensor(out + perm, dtype=torch.int32, device=device)
 
 
+def _save_maps(run, D, device):
+    """nfk_fused_nsf_chain_saved's smaps: for layers 1 .. len(run) - 1 of the
+    run, the tile column of each of the layer's input columns (the
+    permutation _compose_maps has composed at the start of that layer)."""
+    perm = list(range(D))
+    out = []
+    for i, flow in enumerate(run):
+        if i > 0:
+            out += perm
+        lo_in, lo_out, up_in, up_out = flow._maps(device).lists
+        nxt = [0] * D
+        for o, c in zip(lo_out, lo_in):
+            nxt[o] = perm[c]
+        for o, c in zip(up_out, up_in):
+            nxt[o] = perm[c]
+        perm = nxt
+    return torch.tensor(out, dtype=torch.int32, device=device)
+
+
+class _ChainFn(torch.autograd.Function):
+    """A run of fused NSF_CL layers as ONE autograd node (training forward,
+    config.USE_TRAIN_CHAIN): the forward is one nfk_fused_nsf_chain_saved
+    launch (z, the summed log|det| and every layer's input), the backward
+    walks the layers last to first through each layer's own VJP
+    (NSF_CL._vjp, as flows._LayerFn calls it) on the saved inputs, so values
+    and gradients are bitwise those of one _LayerFn node per layer.
+
+    forward(model, run, shape, status, names, x, *params) -> (z, logdet)
+    params: the layers' parameters in order, names[l] those of layer l."""
+
+    @staticmethod
+    def forward(ctx, model, run, shape, status, names, x, *params):
+        n_lo, n_up, hidden, K, B = shape
+        D = n_lo + n_up
+        wp, cm = model._chain_args(list(run), D, False, x)
+        sm = model._chain_save_maps(run, D, x.device)
+        nb = x.shape[0]
+        z = torch.empty_like(x, memory_format=torch.contiguous_format)
+        ld = torch.empty(nb, dtype=torch.float32, device=x.device)
+        saves = torch.empty(len(run) - 1, nb, D, dtype=x.dtype, device=x.device)
+        K_.fused_nsf_chain_saved(x, wp, cm, sm, len(run), n_lo, n_up, hidden, z, saves, logdet=ld,
+                                 logdet_mode=K_.MODE_WRITE, K=K, tail_bound=B, status=status)
+        ctx.run, ctx.names = run, names
+        ctx.save_for_backward(x, saves, *params)
+        return z, ld
+
+    @staticmethod
+    def backward(ctx, gz, gld):
+        x, saves, *params = ctx.saved_tensors
+        run, names = ctx.run, ctx.names
+        need_x = ctx.needs_input_grad[5]
+        need_p = ctx.needs_input_grad[6:]
+        offs = [0]
+        for nm in names:
+            offs.append(offs[-1] + len(nm))
+        grads = [None] * len(params)
+        g = gz
+        for l in range(len(run) - 1, -1, -1):
+            a, b = offs[l], offs[l + 1]
+            need = (l > 0 or need_x,) + tuple(need_p[a:b])
+            res = run[l]._vjp(x if l == 0 else saves[l - 1], names[l], params[a:b], g, gld, False, need)
+            g = res[0]
+            grads[a:b] = res[1:]
+        return (None, None, None, None, None, g if need_x else None, *grads)
+
+
 class NormalizingFlowModel(nn.Module):
 
     def __init__(self, prior, flows, device="cpu"):
@@ -165,11 +231,15 @@ class NormalizingFlowModel(nn.Module):
         off = 0
         flows = self.flows[::-1] if inverse else self.flows
         with torch.set_grad_enabled(grad):
-            for item in self._groups(flows, x.device, grad):
+            for item in self._groups(flows, x.device, grad, inverse):
                 if isinstance(item, tuple):  # a run of fused NSF_CL or RealNVP layers: one launch
                     run, shape = item
                     k = sum(f._n_status for f in run)
-                    x = self._run_chain(run, shape, x, inverse, logdet, status[off:off + k])
+                    if grad:
+                        x, ld = self._train_chain(run, shape, x, status[off:off + k])
+                        logdet = logdet + ld
+                    else:
+                        x = self._run_chain(run, shape, x, inverse, logdet, status[off:off + k])
                     off += k
                     continue
                 flow = item
@@ -201,15 +271,19 @@ class NormalizingFlowModel(nn.Module):
     def _is_rnvp(shape):
         return shape[0] == "rnvp"
 
-    def _groups(self, flows, device, grad):
+    def _groups(self, flows, device, grad, inverse=False):
         """The layer sequence with every run of consecutive NSF_CL layers (or of
         RealNVP layers) that share one fused-kernel shape replaced by (run,
         shape) tuples of at most nfk_fused_nsf_chain_max /
-        nfk_fused_realnvp_chain_max layers (inference only; runs of one stay
-        single).  RealNVP shapes are ("rnvp", kernel half_dim, hidden, half_dim):
-        a half-dimension the kernel does not take runs zero-padded to one it
-        does (RealNVP._fused_half)."""
-        if grad or not (config.USE_FUSED and config.USE_CHAIN):
+        nfk_fused_realnvp_chain_max layers (runs of one stay single).
+        RealNVP shapes are ("rnvp", kernel half_dim, hidden, half_dim): a
+        half-dimension the kernel does not take runs zero-padded to one it
+        does (RealNVP._fused_half).  Under autograd (``grad``) only NSF_CL runs
+        in the forward direction that nfk_fused_nsf_chain_saved takes are
+        grouped (config.USE_TRAIN_CHAIN; _ChainFn)."""
+        if not (config.USE_FUSED and config.USE_CHAIN):
+            return list(flows)
+        if grad and (inverse or not config.USE_TRAIN_CHAIN):
             return list(flows)
         out, run, shape = [], [], None
 
@@ -223,11 +297,15 @@ class NormalizingFlowModel(nn.Module):
             i = 0
             while i < len(run):
                 piece = run[i:i + max(nmax, 1)]
-                out.extend([(piece, shape)] if len(piece) > 1 else piece)
+                if len(piece) > 1 and (not grad or K_.fused_nsf_chain_saved_ok(*shape[:4], len(piece))):
+                    out.append((piece, shape))
+                else:
+                    out.extend(piece)
                 i += len(piece)
 
+        kinds = (NSF_CL,) if grad else (NSF_CL, RealNVP)
         for flow in flows:
-            sh = flow._chain_shape(device) if isinstance(flow, (NSF_CL, RealNVP)) else None
+            sh = flow._chain_shape(device) if isinstance(flow, kinds) else None
             if sh is not None and sh == shape:
                 run.append(flow)
                 continue
@@ -252,6 +330,22 @@ class NormalizingFlowModel(nn.Module):
             ent = (ptrs, torch.tensor(ptrs, dtype=torch.int64, device=x.device), maps)
             self._chain_cache[key] = ent
         return ent[1], ent[2]
+
+    def _chain_save_maps(self, run, D, device):
+        key = ("save", tuple(id(f) for f in run), str(device))
+        sm = self._chain_cache.get(key)
+        if sm is None:
+            sm = self._chain_cache[key] = _save_maps(run, D, device)
+        return sm
+
+    def _train_chain(self, run, shape, x, status):
+        """A run of fused NSF_CL layers under autograd: one _ChainFn node."""
+        D = shape[0] + shape[1]
+        if not self._chain_layout_ok(x, D):
+            x = x.clone(memory_format=torch.contiguous_format)  # fresh, 16-byte aligned rows
+        named = [list(f.named_parameters()) for f in run]
+        names = tuple(tuple(n for n, _ in nm) for nm in named)
+        return _ChainFn.apply(self, tuple(run), shape, status, names, x, *(t for nm in named for _, t in nm))
 
     def _fused_log_prob(self, x):
         """evaluate() as ONE launch when the whole model is one chained run of

@@ -13,7 +13,7 @@ import torch
 
 import nf.flows as nff
 from normalizingflow_amd import _lib
-from normalizingflow_amd.models import _compose_maps
+from normalizingflow_amd.models import _compose_maps, _save_maps
 from oracle import nf_oracle as orc
 
 
@@ -59,6 +59,44 @@ def test_composed_maps_match_oracle_permutation(size, dim, masks, n):
         p = q
 
 
+@pytest.mark.parametrize("size,dim,masks,n", [
+    (4, 2, [[0], [1]], 5),
+    (3, 3, [[1], [0, 2], [2]], 4),
+])
+def test_save_maps_are_the_layer_inputs(size, dim, masks, n):
+    """nfk_fused_nsf_chain_saved's smaps (models._save_maps): for layer l >= 1,
+    column j of that layer's input sits in the tile column the chain's cmaps
+    give for it (its lower / upper input lists), and the permutation after the
+    last layer is cmaps' output map."""
+    run = _run(size, dim, masks, n)
+    D = size * dim
+    cm = _compose_maps(run, D, torch.device("cpu")).tolist()
+    sm = _save_maps(run, D, torch.device("cpu")).tolist()
+    assert len(sm) == (n - 1) * D
+    for i in range(1, n):
+        lo_in, _, up_in, _ = run[i]._maps(torch.device("cpu")).lists
+        smi = sm[(i - 1) * D:i * D]
+        assert sorted(smi) == list(range(D))
+        assert [smi[c] for c in lo_in] == cm[i * D:i * D + len(lo_in)]
+        assert [smi[c] for c in up_in] == cm[i * D + len(lo_in):(i + 1) * D]
+
+
+def test_chain_saved_validation_is_host_only():
+    lib = _lib.load()
+    assert lib.nfk_fused_nsf_chain_saved_ok(32, 32, 100, 8, 8) == 1     # c3: the two-tile chain
+    assert lib.nfk_fused_nsf_chain_saved_ok(32, 32, 100, 8, 1) == 0     # one layer: no chain
+    assert lib.nfk_fused_nsf_chain_saved_ok(32, 32, 64, 8, 8) == 0      # not a two-tile-chain shape
+    args = lambda nl, x=16, sv=16, st=256 * 64: (x, 64, 16, 16, nl, 32, 32, 100, 16, 64, 16, 1, 256, 8, 3.0,
+                                                  None, sv, 64, st, 16, None)
+    assert lib.nfk_fused_nsf_chain_saved(*args(1)) == _lib.NFK_EINVAL
+    assert b"layer count" in lib.nfk_last_error()
+    assert lib.nfk_fused_nsf_chain_saved(*args(8, sv=None)) == _lib.NFK_EINVAL
+    assert b"null pointer" in lib.nfk_last_error()
+    assert lib.nfk_fused_nsf_chain_saved(*args(8, x=4)) == _lib.NFK_EINVAL
+    assert b"aligned" in lib.nfk_last_error()
+    assert lib.nfk_fused_nsf_chain_saved(*args(8, st=64)) == _lib.NFK_EINVAL   # layer stride < batch rows
+
+
 def test_chain_layer_count_query_is_host_only():
     lib = _lib.load()
     n = lib.nfk_fused_nsf_chain_max(32, 32, 100, 8)   # c3 layer shape
@@ -90,7 +128,8 @@ def test_layer_grouping(monkeypatch):
     """NormalizingFlowModel._groups: runs of consecutive same-shape fused NSF_CL
     layers become (run, shape) items of at most nfk_fused_nsf_chain_max layers;
     other layers, shape changes and single-layer runs stay per-layer; training
-    (grad) never chains.  Fused-kernel availability is stubbed (no device)."""
+    (grad) chains only NSF_CL runs in the forward direction that the
+    saved-input chain takes.  Fused-kernel availability is stubbed (no device)."""
     import nf.models as nfm
     from normalizingflow_amd import config
     from normalizingflow_amd import kernels as K_
@@ -118,5 +157,26 @@ def test_layer_grouping(monkeypatch):
     monkeypatch.setattr(K_, "fused_nsf_chain_max", lambda *s: 0)
     assert m2._groups(m2.flows, torch.device("cpu"), False) == list(a)
     assert m._groups(m.flows, torch.device("cpu"), True) == flows
+    # training (grad): NSF_CL runs the saved-input chain takes, forward only
+    monkeypatch.setattr(K_, "fused_nsf_chain_max", lambda *s: 3)
+    monkeypatch.setattr(K_, "fused_nsf_chain_saved_ok", lambda *s: True)
+    g3 = m._groups(m.flows, torch.device("cpu"), True)
+    kinds3 = [("run", [flows.index(f) for f in it[0]]) if isinstance(it, tuple) else ("one", flows.index(it))
+              for it in g3]
+    assert kinds3 == [("run", [0, 1]), ("one", 2), ("run", [3, 4, 5]), ("one", 6), ("one", 0)]
+    assert m._groups(m.flows, torch.device("cpu"), True, inverse=True) == flows
+    monkeypatch.setattr(K_, "fused_nsf_chain_saved_ok", lambda *s: False)
+    assert m._groups(m.flows, torch.device("cpu"), True) == flows
+    monkeypatch.setattr(K_, "fused_nsf_chain_saved_ok", lambda *s: True)
+    monkeypatch.setattr(config, "USE_TRAIN_CHAIN", False)
+    assert m._groups(m.flows, torch.device("cpu"), True) == flows
+    # RealNVP runs are not grouped under grad
+    rr = [nff.RealNVP(8, hidden_dim=8) for _ in range(3)]
+    monkeypatch.setattr(config, "USE_TRAIN_CHAIN", True)
+    monkeypatch.setattr(nff.RealNVP, "_chain_shape", lambda self, dev: ("rnvp", 16, 8, 4))
+    monkeypatch.setattr(K_, "fused_realnvp_chain_max", lambda *s: 8)
+    mr = nfm.NormalizingFlowModel(None, rr)
+    assert isinstance(mr._groups(mr.flows, torch.device("cpu"), False)[0], tuple)
+    assert mr._groups(mr.flows, torch.device("cpu"), True) == rr
     monkeypatch.setattr(config, "USE_CHAIN", False)
     assert m._groups(m.flows, torch.device("cpu"), False) == flows

@@ -63,12 +63,15 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle train step")
     ap.add_argument("--no-fcnn-fwd", action="store_true",
                     help="recompute forward of FCNN conditioners on library GEMMs")
+    ap.add_argument("--no-train-chain", action="store_true",
+                    help="one autograd node and launch per layer in the forward (config.USE_TRAIN_CHAIN off)")
     ap.add_argument("--no-fcnn-dh", action="store_true",
                     help="library GEMMs + tanh_backward for the FCNN input gradients (config.USE_FCNN_DH off)")
     args = ap.parse_args()
     from normalizingflow_amd import config
     config.USE_FCNN_DH = not args.no_fcnn_dh
     config.USE_FCNN_FWD = not args.no_fcnn_fwd
+    config.USE_TRAIN_CHAIN = not args.no_train_chain
     dev = torch.device("cuda", 0)
     model, sd, _ = bench.build_model(args.workload, dev)
     x = torch.randn(args.batch, bench.WORKLOADS[args.workload][3], device=dev)
@@ -80,7 +83,8 @@ def main():
 
     res = {"metric": "samples/sec train step (NLL fwd + bwd + Adam)", "workload": args.workload,
            "batch": args.batch, "steps": args.steps,
-           "fcnn_dh": config.USE_FCNN_DH, "fcnn_fwd": config.USE_FCNN_FWD}
+           "fcnn_dh": config.USE_FCNN_DH, "fcnn_fwd": config.USE_FCNN_FWD,
+           "train_chain": config.USE_TRAIN_CHAIN}
     t = timed(ours, opt, x, args.steps, args.warmup)
     res["hip"] = {"ms_per_step": round(t * 1e3, 3), "samples_per_s": round(args.batch / t, 1)}
     if not args.no_torch:
