@@ -86,8 +86,6 @@ __device__ __forceinline__ void store_act(const f32x4 (&h)[HT], float* row, int 
     if (q == 1) row[H] = 1.0f;
 }
 
-constexpr int64_t kVjpRows = 32768;  // rows per launch (nfk_fused_nsf_vjp)
-
 template <int KBH, bool T1, int K, bool INV>
 __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
     constexpr VjpDims d = vjp_dims(KBH, T1 ? 1 : 0, K);
@@ -297,29 +295,9 @@ extern "C" int nfk_fused_nsf_vjp(const float* x, int64_t ldx, const float* vpack
     a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
     hipStream_t st = (hipStream_t)stream;
     const bool inv = inverse != 0;
-    // Launched in row blocks of kVjpRows (512 workgroups, every one resident
-    // at once, at most two per CU): launches of 49,152 rows and more gave
-    // run-to-run different dL/dparams and dL/dx (tools/dbg_vjp_det.py; cause
-    // not found -- DESIGN.md section 10), blocks of 32,768 are bitwise
-    // reproducible (tests/test_gpu_vjp.py::test_fused_vjp_full_occupancy_batch)
-    const int64_t P = 3 * K - 1;
-    for (int64_t off = 0; off < batch; off += kVjpRows) {
-        VjpArgs c = a;
-        c.batch = batch - off < kVjpRows ? batch - off : kVjpRows;
-        c.x = x + off * ldx;
-        c.gz = gz ? gz + off * ldgz : nullptr;
-        c.gld = glogdet ? glogdet + off : nullptr;
-        c.gp = gparams + off * n_up * P;
-        c.gx = gx + off * ldgx;
-        c.h1 = h1 + off * ldh;
-        c.h2 = h2 + off * ldh;
-        int rc = -1;
 #define VDISPATCH(h, t, k) \
-    if (L.KBH == h && L.T1 == t && K == k) rc = launch_vjp<h, t, k>(c, inv, st);
-        NFK_VJP_SHAPES(VDISPATCH)
+    if (L.KBH == h && L.T1 == t && K == k) return launch_vjp<h, t, k>(a, inv, st);
+    NFK_VJP_SHAPES(VDISPATCH)
 #undef VDISPATCH
-        if (rc < 0) return nfk_set_error("nfk_fused_nsf_vjp: no kernel instance");
-        if (rc != 0) return rc;
-    }
-    return 0;
+    return nfk_set_error("nfk_fused_nsf_vjp: no kernel instance");
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Fused VJP launched in 32K-row blocks (determinism fix) + the training-forward chain:
+# Fused VJP with global loads only while no LDS-DMA is in flight (determinism fix) + the training-forward chain:
 # determinism diagnostic, the VJP / train-chain / grad / chain GPU tests, then the c3 train
 # step at 2^20 with and without the training chain.
 set -u
