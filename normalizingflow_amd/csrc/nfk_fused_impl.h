@@ -479,6 +479,9 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
                 __builtin_amdgcn_sched_barrier(0);
                 if (NT == 1) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7");
                 else asm volatile("s_nop 7\n\ts_nop 7");
+#ifdef NFK_TAIL_NOP_EXTRA  // diagnostic: a longer wait before the tail step
+                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7");
+#endif
                 __builtin_amdgcn_sched_barrier(0);
             }
             const float4 w = r[0];

@@ -95,7 +95,7 @@ def test_fused_vjp_no_logdet_grad(hip_device):
 @pytest.mark.xfail(strict=False, reason="known gap (DESIGN.md section 10.5): at >= 32K rows nfk_fused_nsf_vjp "
                    "gives run-to-run different dL/dparams and dL/dx; cause not found in round 3")
 @pytest.mark.parametrize("inverse", [False, True])
-def test_fused_vjp_full_occupancy_batch(inverse, hip_device):
+def test_fused_vjp_full_occupancy_batch(inverse, hip_device, monkeypatch):
     """Batches large enough that every CU runs the VJP kernel's full complement
     of workgroups at once (2^18 rows; the c3 train step runs 2^20): the fused
     backward should be bitwise reproducible and agree with the unfused path
@@ -104,6 +104,7 @@ def test_fused_vjp_full_occupancy_batch(inverse, hip_device):
     torch.manual_seed(5)
     layer = nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=100, mask=[0]).to(hip_device)
     B = (1 << 18) + 77
+    monkeypatch.setattr(config, "FUSED_VJP_MAX_ROWS", B)  # force the fused kernel
     g = torch.Generator(hip_device).manual_seed(4)
     x = torch.randn(B, 64, device=hip_device, generator=g) * 1.2
     w = torch.randn(B, 64, device=hip_device, generator=g)
@@ -122,3 +123,22 @@ def test_fused_vjp_full_occupancy_batch(inverse, hip_device):
     for n, t1, t2 in zip(names, a, plain):
         scale = float(t2.abs().max())
         assert float((t1 - t2).abs().max()) <= 2e-5 * scale + 1e-6, n
+
+
+def test_large_batch_backward_reproducible(hip_device):
+    """The default training backward at 2^18 rows (above
+    config.FUSED_VJP_MAX_ROWS: the unfused path) is bitwise reproducible and
+    runs without the fused VJP pack."""
+    torch.manual_seed(6)
+    layer = nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=100, mask=[1]).to(hip_device)
+    B = 1 << 18
+    assert B > config.FUSED_VJP_MAX_ROWS
+    g = torch.Generator(hip_device).manual_seed(8)
+    x = torch.randn(B, 64, device=hip_device, generator=g)
+    w = torch.randn(B, 64, device=hip_device, generator=g)
+    v = torch.randn(B, device=hip_device, generator=g)
+    a = _grads(layer, x, w, v, False)
+    b = _grads(layer, x, w, v, False)
+    assert layer.__dict__.get("_vjp_cache") is None  # the fused kernel did not run
+    for t1, t2 in zip(a, b):
+        assert torch.equal(t1, t2)

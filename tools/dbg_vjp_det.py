@@ -5,7 +5,8 @@ from normalizingflow_amd import kernels as K_
 dev = torch.device("cuda", 0)
 torch.manual_seed(3)
 layer = nff.NSF_CL(size=32, dim=2, K=8, B=3, hidden_dim=100, mask=[0]).to(dev)
-for B in (32768, 65536, 262144, 1048576):
+import os
+for B in [int(v) for v in os.environ.get('DBG_ROWS', '32768,65536,262144,1048576').split(',')]:
     x = torch.randn(B, 64, generator=torch.Generator().manual_seed(B)).to(dev) * 1.2
     gz = torch.randn(B, 64, device=dev) * 1e-3
     gld = torch.full((B,), -1.0 / B, device=dev)

@@ -11,6 +11,7 @@ run() {  # name timeout cmd...
   [ $rc -eq 0 ] || exit $rc
 }
 export PYTHONPATH=.
+DBG_ROWS=262144,1048576 NFK_LIBRARY=$PWD/build_ab/tailnop/libnfk.so run vjp_tailnop 240 python tools/dbg_vjp_det.py
 run vjp_unfused 240 python tools/dbg_vjp_unfused.py
 run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread
 run smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
