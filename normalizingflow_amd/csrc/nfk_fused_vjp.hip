@@ -214,7 +214,11 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
             }
             const float xv = tile[sl * XS + m_up_in[j]];
             const float go = (a.gz != nullptr) ? a.gz[b * a.ldgz + m_up_out[j]] : 0.0f;
+#ifdef NFK_VJP_DUMP  // diagnostic: the element backward's inputs instead of its outputs
+            const float gxv = xv + 1000.0f * go + 1.0e6f * gl;
+#else
             const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, wr, hr, dr, a.c, go, gl);
+#endif
             if (row_ok) {
                 a.gx[b * a.ldgx + m_up_in[j]] = gxv;
                 float* g = a.gp + (b * n_up + j) * P;
