@@ -25,10 +25,6 @@ USE_TRAIN_CHAIN training (forward direction under autograd): consecutive fused
 USE_FUSED_VJP  training: NSF_CL's backward through nfk_fused_nsf_vjp (conditioner
                recompute on the matrix cores + spline VJP in one kernel) where
                the shape is supported; off: recompute GEMMs + nfk_rqs_coupling_bwd.
-FUSED_VJP_MAX_ROWS  training: the fused VJP kernel serves batches of at most this
-               many rows; larger ones take the unfused backward (recompute
-               GEMMs + nfk_rqs_coupling_bwd), which is run-to-run reproducible
-               where the fused kernel is not.
 USE_FCNN_DH    training: the stock FCNN backward's input-gradient GEMMs (g W,
                tanh's backward fused) on nfk_fcnn_dh (fp16-split MFMA) where
                the shape is supported; off: fp32 library GEMMs + tanh_backward.
@@ -41,6 +37,5 @@ USE_FUSED = True
 USE_CHAIN = True
 USE_TRAIN_CHAIN = True
 USE_FUSED_VJP = True
-FUSED_VJP_MAX_ROWS = 8192
 USE_FCNN_DH = True
 USE_FCNN_FWD = True

@@ -615,6 +615,8 @@ extern "C" int nfk_fused_nsf_chain(const float* x, int64_t ldx, const float* con
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf_chain: null logdet");
     if (((uintptr_t)x % 16) != 0 || ((uintptr_t)z % 16) != 0 || ldx % 4 != 0 || (z && ldz % 4 != 0))
         return nfk_set_error("nfk_fused_nsf_chain: x and z rows must be 16-byte aligned");
+    if (ldx < n_lo + n_up || (z && ldz < n_lo + n_up))
+        return nfk_set_error("nfk_fused_nsf_chain: ldx and ldz must be >= n_lo + n_up");
     FusedArgs a = fused_args(x, ldx, nullptr, nullptr, nullptr, nullptr, nullptr, L, z, ldz, logdet, logdet_mode,
                              batch, K, tail_bound, status);
     a.slot_blocks = split_slot_blocks(L);
@@ -681,6 +683,7 @@ extern "C" int nfk_fused_nsf_chain_saved(const float* x, int64_t ldx, const floa
     if (((uintptr_t)x % 16) != 0 || ((uintptr_t)z % 16) != 0 || ((uintptr_t)saves % 16) != 0 || ldx % 4 != 0 ||
         ldz % 4 != 0 || ld_saves % 4 != 0 || save_stride % 4 != 0 || ld_saves < D || save_stride < batch * ld_saves)
         return nfk_set_error("nfk_fused_nsf_chain_saved: x, z and saves rows must be 16-byte aligned");
+    if (ldx < D || ldz < D) return nfk_set_error("nfk_fused_nsf_chain_saved: ldx and ldz must be >= n_lo + n_up");
     const Layout L = make_layout(n_lo, n_up, hidden, K);
     FusedArgs a = fused_args(x, ldx, nullptr, nullptr, nullptr, nullptr, nullptr, L, z, ldz, logdet, logdet_mode,
                              batch, K, tail_bound, status);

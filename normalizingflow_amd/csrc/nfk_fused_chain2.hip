@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(e[j]));
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+                for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
                 int ex = 0;
                 if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
                 const float sx = ldexpf(1.0f, 14 - ex);

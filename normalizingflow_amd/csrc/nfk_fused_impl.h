@@ -61,7 +61,7 @@ constexpr float kActScale = 16384.0f;  // tanh outputs are split at 2^14 (|h| * 
 //            32 KBH + 0..3 of row(t, l&15): k-group l>>4 = {hi, hi, lo, 0} of 2^s W, against
 //            the B groups {a_hi, a_lo, a_hi, -} (tail_word, act_operands): the
 //            same three split products as the k-blocks, in one f16 MFMA
-//   layer 1: KB1 = ceil(n_lo/32) f16 k-blocks (x is scaled per wave), bias unscaled
+//   layer 1: KB1 = ceil(n_lo/32) f16 k-blocks (x is scaled per sample, by a power of two), bias unscaled
 //   layer 2: KBH f16 k-blocks (+ tail blocks), bias pre-scaled by 2^(s2+14)
 //   per 16-coordinate chunk: W logits (K tiles), H logits (K tiles), D logits
 //            (K-1 tiles), same form; row i of tile t = parameter t of coordinate 16c+i
@@ -1055,7 +1055,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                                      fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
             }
     #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+            for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
             int ex = 0;
             if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
             const float sx = ldexpf(1.0f, 14 - ex);

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_rnvp(RArgs a) {
         // header: per (pair, net, layer) unscale factors at hdr[16 + (2 pr + net) 3 + layer]
         const float* un = hdr + 16 + pr * 6;
 
-        // ---- phase 0: layer 1 of s and t from the (per-wave scaled) input half
+        // ---- phase 0: layer 1 of s and t from the (per-sample scaled) input half
         h8 bsh[KBH], bsl[KBH], bth[KBH], btl[KBH];
         h4 bst, btt;
         {
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_rnvp(RArgs a) {
                                      fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
             }
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+            for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
             int ex = 0;
             if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
             const float sx = ldexpf(1.0f, 14 - ex);
@@ -601,7 +601,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_rnvp_chain(RChainArgs a) 
             const int in_off = pr == 0 ? 0 : XI;  // pair 0 reads the lower half, updates the upper
             const int tg_off = pr == 0 ? XI : 0;
             const float* un = hdr + 16 + pr * 6;  // unscale factors of (net, layer) in the pair
-            // layer-1 operands of the input half, per-wave power-of-two scaled (as k_fused_rnvp)
+            // layer-1 operands of the input half, per-sample power-of-two scaled (as k_fused_rnvp)
             h8 xh[KBI], xl[KBI];
             int ex = 0;
             {
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_rnvp_chain(RChainArgs a) 
                                          fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)))));
                 }
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+                for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
                 if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
                 const float sx = ldexpf(1.0f, 14 - ex);
 #pragma unroll

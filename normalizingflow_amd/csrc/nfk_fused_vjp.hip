@@ -107,7 +107,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
     const int nrows = rem <= 0 ? 0 : (rem < 16 ? (int)rem : 16);
     const bool row_ok = sl < nrows;
     // rows past the batch compute on the wave's first row (as the forward
-    // kernel, so the per-wave input scale and hence the logits match it) and
+    // kernel, so the input scale and hence the logits match it) and
     // store nothing
     const int64_t brow0 = nrows > 0 ? b0 : 0;
     const int64_t b = row_ok ? b0 + sl : brow0;
@@ -116,10 +116,16 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
     auto stage_next = [&](float4* slot) {
         if (nsub >= a.nsub) return;
         const float* src = a.stream + (int64_t)nsub * SB * 256;
+#ifdef NFK_VJP_DIAG_PLAIN  // diagnostic: plain loads + ds_write instead of LDS-DMA
+#pragma unroll
+        for (int i = 0; i < SB / 4; ++i)
+            slot[(wid + 4 * i) * 64 + lane] = *reinterpret_cast<const float4*>(src + (int64_t)(wid + 4 * i) * 256 + lane * 4);
+#else
         const uint32_t base = lds_addr(slot);
 #pragma unroll
         for (int i = 0; i < SB / 4; ++i)
             dma16(src + (int64_t)(wid + 4 * i) * 256 + lane * 4, base + (wid + 4 * i) * 1024);
+#endif
         ++nsub;
     };
     auto step = [&](float4* freed) {
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
     int cur = 0;
     const float un1 = a.hdr[3], un2 = a.hdr[4], un3 = a.hdr[5];
 
-    // ---- layer 1 (one k-block: n_lo <= 32), per-wave power-of-two scaled x
+    // ---- layer 1 (one k-block: n_lo <= 32), per-sample power-of-two scaled x (each row its own exponent: rows stay independent)
     h8 bh[KBH], bl[KBH];
     h4 bt;
     {
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(e[j]));
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
         int ex = 0;
         if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
         const float sx = ldexpf(1.0f, 14 - ex);
@@ -193,6 +199,21 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
         if (row_ok) store_act<KBH, T1, HT>(h2, a.h2 + b * a.ldh, q, a.H);
     }
     const float gl = (a.gld != nullptr) ? a.gld[b] : 0.0f;
+#ifdef NFK_VJP_DIAG_VGPRC  // diagnostic: the spline constants in VGPRs (no SGPR pressure from them)
+    NfkSplineConst cc = a.c;
+    asm volatile("" : "+v"(cc.scale2b), "+v"(cc.lo), "+v"(cc.hi), "+v"(cc.span), "+v"(cc.ylo), "+v"(cc.yhi),
+                 "+v"(cc.yspan), "+v"(cc.min_w), "+v"(cc.fw), "+v"(cc.min_h), "+v"(cc.fh));
+    asm volatile("" : "+v"(cc.min_d), "+v"(cc.dpad), "+v"(cc.knot_eps), "+v"(cc.m2b), "+v"(cc.d_edge));
+#else
+    const NfkSplineConst& cc = a.c;
+#endif
+#ifdef NFK_VJP_DIAG_NOP
+#define NFK_VJP_NOPS() do { __builtin_amdgcn_sched_barrier(0); \
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"); \
+        __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define NFK_VJP_NOPS() do { } while (0)
+#endif
     // ---- output layer in 8-coordinate chunks: W, H, D logits of the lane's two
     // coordinates in registers, then the spline VJP of each
     for (int ch = 0; ch < a.NCH; ++ch) {
@@ -200,6 +221,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
         vjp_parts<KBH, T1, KW, 0>(bh, bl, bt, slot0, slot1, cur, lane, aw, step);
         vjp_parts<KBH, T1, KW, 0>(bh, bl, bt, slot0, slot1, cur, lane, ah, step);
         vjp_parts<KBH, T1, KD, 0>(bh, bl, bt, slot0, slot1, cur, lane, ad, step);
+        NFK_VJP_NOPS();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
             const int j = 8 * ch + 2 * q + cb;
@@ -217,7 +239,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
 #ifdef NFK_VJP_DUMP  // diagnostic: the element backward's inputs instead of its outputs
             const float gxv = xv + 1000.0f * go + 1.0e6f * gl;
 #else
-            const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, wr, hr, dr, a.c, go, gl);
+            const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, wr, hr, dr, cc, go, gl);
 #endif
             if (row_ok) {
                 a.gx[b * a.ldgx + m_up_in[j]] = gxv;
@@ -230,6 +252,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
                 for (int i = 0; i < K - 1; ++i) g[2 * K + i] = dr[i];
             }
         }
+        NFK_VJP_NOPS();
     }
     // ---- lower coordinates: the identity part of dL/dx (flows.py:239)
     for (int i = lane; i < 16 * n_lo; i += 64) {
@@ -243,7 +266,15 @@ template <int KBH, int T1, int K>
 int launch_vjp(const VjpArgs& a, bool inv, hipStream_t st) {
     const int64_t blocks = (a.batch + kNsfWaves * 16 - 1) / (kNsfWaves * 16);
     if (blocks == 0) return 0;
+#ifdef NFK_VJP_DIAG_ONEWG  // diagnostic: LDS padded so that one workgroup runs per CU
+    const size_t lds = 96 * 1024;
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nsf_vjp<KBH, T1 != 0, K, false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nsf_vjp<KBH, T1 != 0, K, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+#else
     const size_t lds = vjp_lds_bytes(vjp_dims(KBH, T1, K), a.n_lo + a.n_up);
+#endif
     if (inv)
         hipLaunchKernelGGL((k_nsf_vjp<KBH, T1 != 0, K, true>), dim3((unsigned)blocks), dim3(64 * kNsfWaves), lds,
                            st, a);

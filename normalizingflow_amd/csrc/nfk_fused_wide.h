@@ -20,7 +20,7 @@
 //     after the barrier ending s) overlaps the epilogue and the GEMM of s+1;
 //   * layer-1 operands (x at the lower coordinates) are read once per wave
 //     into registers by plain loads in the prologue, before any copy is
-//     waited on, and split there (per-wave power-of-two scale as before);
+//     waited on, and split there (per-sample power-of-two scale);
 //   * per chunk pair, each wave stages the 32 coordinates (16 upper, 16
 //     lower) of its 16 rows by LDS-DMA gathers into a 16 x 32 tile; the
 //     spline reads x there, writes z back in place (the lower coordinates
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(64 * kWideWaves, kWideWGs) void k_fused_nsf_wide(Wi
                 mx = fmaxf(mx, fabsf(xv[kb][j]));
             }
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
         int ex = 0;
         if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
         const float sx = ldexpf(1.0f, 14 - ex);

@@ -61,14 +61,18 @@ def sharded_nll(log_prob, n_global=None, group=None):
     world, so the averaged gradient is exactly that of the global
     -mean(log p) (train.py:23-27) for ANY split of the rows -- averaging per
     rank means (-mean of each shard) is that only when the shards are equal.
-    The mean over ranks of the returned values is the global NLL."""
+    The mean over ranks of the returned values is the global NLL.
+
+    Pass ``n_global`` in a training loop (the caller knows it: the sum of
+    shard_range's sizes): without it every call adds a count all-reduce,
+    kept on the device (no host sync) but still one collective per step."""
     world = 1
     if dist.is_available() and dist.is_initialized():
         world = dist.get_world_size(group)
         if n_global is None:
             cnt = torch.tensor([float(log_prob.numel())], dtype=torch.float64, device=log_prob.device)
             dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
-            n_global = float(cnt.item())
+            return -log_prob.sum() * (world / cnt[0]).to(log_prob.dtype)
     if n_global is None:
         n_global = log_prob.numel()
     return -log_prob.sum() * (world / float(n_global))

@@ -644,9 +644,7 @@ class NSF_CL(_HipFlow):
         # weight gradients); any other conditioner through autograd
         manual = _is_stock_fcnn(self.psi) and set(names) == set(
             "psi.network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias"))
-        # the fused kernel only up to config.FUSED_VJP_MAX_ROWS rows: above
-        # that it is not run-to-run reproducible
-        vpack = self._vjp_pack(x.device) if manual and x.shape[0] <= config.FUSED_VJP_MAX_ROWS else None
+        vpack = self._vjp_pack(x.device) if manual else None
         if vpack is not None:
             # fused: the conditioner recomputed on the matrix cores and the
             # spline VJP in one kernel (nfk_fused_nsf_vjp); it hands over

@@ -595,6 +595,8 @@ def fused_nsf_chain(x, wpacks, cmaps, nlayers, n_lo, n_up, hidden, z, *, logdet,
     if wpacks.dtype != torch.int64 or wpacks.numel() != nlayers:
         raise ValueError("wpacks must hold %d int64 pack pointers" % nlayers)
     _vec(cmaps, nlayers * D + D, "cmaps", torch.int32)
+    if x.dim() != 2 or x.shape[1] != D or (z is not None and tuple(z.shape) != tuple(x.shape)):
+        raise ValueError("x and z must be [batch, %d] (n_lo + n_up) tensors" % D)
     xp, ldx = _mat(x, "x")
     zp, ldz = _mat(z, "z") if z is not None else (None, 0)
     _timed("nfk_fused_nsf_chain", dev, "nfk_fused_nsf_chain", xp, ldx, wpacks.data_ptr(), cmaps.data_ptr(),
@@ -632,6 +634,8 @@ def fused_nsf_chain_saved(x, wpacks, cmaps, smaps, nlayers, n_lo, n_up, hidden, 
             saves.stride(2) != 1:
         raise ValueError("saves must be a float32 [%d, %d, %d] tensor with unit column stride"
                          % (nlayers - 1, B, D))
+    if x.dim() != 2 or x.shape[1] != D or tuple(z.shape) != tuple(x.shape):
+        raise ValueError("x and z must be [batch, %d] (n_lo + n_up) tensors" % D)
     xp, ldx = _mat(x, "x")
     zp, ldz = _mat(z, "z")
     _timed("nfk_fused_nsf_chain_saved", dev, "nfk_fused_nsf_chain_saved", xp, ldx, wpacks.data_ptr(),

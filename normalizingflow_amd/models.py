@@ -294,6 +294,9 @@ class NormalizingFlowModel(nn.Module):
                 nmax = K_.fused_realnvp_chain_max(shape[1], shape[2])
             else:
                 nmax = K_.fused_nsf_chain_max(*shape[:4])
+                if grad:  # the saved form also holds the save maps: its limit can be lower
+                    while nmax > 1 and not K_.fused_nsf_chain_saved_ok(*shape[:4], nmax):
+                        nmax -= 1
             i = 0
             while i < len(run):
                 piece = run[i:i + max(nmax, 1)]
@@ -341,6 +344,14 @@ class NormalizingFlowModel(nn.Module):
     def _train_chain(self, run, shape, x, status):
         """A run of fused NSF_CL layers under autograd: one _ChainFn node."""
         D = shape[0] + shape[1]
+        if x.dim() != 2 or x.shape[1] != D:
+            # not the run's width: per-layer nodes, whose first layer raises the
+            # reference's error (the chain kernel would read past or truncate x)
+            logdet = torch.zeros(x.shape[0], dtype=torch.float32, device=x.device)
+            for i, flow in enumerate(run):
+                x, ld = flow._call(x, False, status=status[i:i + 1] if flow._n_status else None)
+                logdet = logdet + ld
+            return x, logdet
         if not self._chain_layout_ok(x, D):
             x = x.clone(memory_format=torch.contiguous_format)  # fresh, 16-byte aligned rows
         named = [list(f.named_parameters()) for f in run]

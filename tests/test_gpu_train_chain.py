@@ -102,3 +102,22 @@ def test_train_chain_raises_like_per_layer(hip_device, monkeypatch):
         except Exception as e:  # the reference's error type, whichever it is
             errs.append((type(e), str(e)))
     assert errs[0] == errs[1]
+
+
+@pytest.mark.parametrize("width", [60, 68])
+def test_train_chain_wrong_width_raises_like_per_layer(width, hip_device, monkeypatch):
+    """A batch of the wrong width under the training chain raises the
+    per-layer path's error instead of launching the chain kernel on it (which
+    would read past x's rows or silently drop columns)."""
+    model = _model(3, hip_device)
+    x = torch.randn(512, width, device=hip_device)
+    errs = []
+    for chain in (True, False):
+        monkeypatch.setattr(config, "USE_TRAIN_CHAIN", chain)
+        with pytest.raises(Exception) as ei:
+            xg = x.clone().requires_grad_(True)
+            _, plp, ld = model(xg)
+            (-torch.mean(plp + ld)).backward()
+        errs.append((ei.type, str(ei.value)))
+    assert errs[0] == errs[1]
+    assert "got %d features" % width in errs[0][1]

@@ -67,8 +67,11 @@ def main():
                     help="one autograd node and launch per layer in the forward (config.USE_TRAIN_CHAIN off)")
     ap.add_argument("--no-fcnn-dh", action="store_true",
                     help="library GEMMs + tanh_backward for the FCNN input gradients (config.USE_FCNN_DH off)")
+    ap.add_argument("--vjp-max-rows", type=int, default=None, help="override config.FUSED_VJP_MAX_ROWS")
     args = ap.parse_args()
     from normalizingflow_amd import config
+    if args.vjp_max_rows is not None and hasattr(config, "FUSED_VJP_MAX_ROWS"):
+        config.FUSED_VJP_MAX_ROWS = args.vjp_max_rows
     config.USE_FCNN_DH = not args.no_fcnn_dh
     config.USE_FCNN_FWD = not args.no_fcnn_fwd
     config.USE_TRAIN_CHAIN = not args.no_train_chain
