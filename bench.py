@@ -69,8 +69,16 @@ WORKLOADS = {
     # nlayers 1, B = ncellx * cell_len / 2 = 4 (setup.py:42, 58)
     "ar": ("40-dim synthetic Gaussian, NSF_AR autoregressive RQS (Gaussian.yaml: K=10, H=80, B=4, "
            "1 layer), log_prob", "NSF_AR", dict(dim=40, K=10, B=4.0, hidden_dim=80), 40, 1),
+    # the applications' own NSF_AR (Einstein.yaml; LJ.yaml and Fe_*.yaml share the
+    # flow): 32 particles x 3 dims, nsplines 32, hidden 354, nlayers 2,
+    # B = (nparticles / (8 rho))^(1/3) at rho 1.28 (setup.py:42-58)
+    "ar354": ("96-dim synthetic Gaussian, NSF_AR autoregressive RQS (Einstein.yaml: K=32, H=354, "
+              "B=1.462, 2 layers), log_prob", "NSF_AR",
+              dict(dim=96, K=32, B=(32 / (8 * 1.28)) ** (1.0 / 3.0), hidden_dim=354), 96, 2),
 }
-DEFAULT_BATCH = {"c1": 4096}
+# default per-GPU rows: c1 is BASELINE's 4,096-row case; ar354's conditioners
+# (37 MFLOP per sample and layer) make 2^16 rows a ~1 s step
+DEFAULT_BATCH = {"c1": 4096, "ar354": 1 << 16}
 # BASELINE.md's published figure for the same metric: c1 is quoted on the
 # reference's own CPU path (900,334 samples/s, 8-core Xeon); no GPU figures exist
 BASELINE_CPU = {"c1": 900334.0}  # c1 B = 4096; the others 2^20
@@ -105,6 +113,7 @@ METRICS = {
     "c5": "samples/sec log_prob (1M×256, 16 RQS coupling layers, H=256, K=16)",
     "c1": "samples/sec log_prob (4096×2 two moons, 4 RealNVP affine coupling layers)",
     "ar": "samples/sec log_prob (1M×40, 1 NSF_AR autoregressive RQS layer, K=10, H=80)",
+    "ar354": "samples/sec log_prob (64K×96, 2 NSF_AR autoregressive RQS layers, K=32, H=354)",
 }
 
 
@@ -117,6 +126,8 @@ ARITH = {
     "c5": _SPLIT + " (nfk_fused_wide.h)",
     "c1": _SPLIT + _TAIL + " (nfk_fused_rnvp.hip; the D = 2 halves zero-padded to the kernel's 16)",
     "ar": _SPLIT + " (nfk_fused_ar.hip; layer 1 on the fp16-split trig features)",
+    "ar354": _SPLIT + "; the 2 tail features of H=354 as one 16x16x16 f16 MFMA per tile"
+             " (nfk_fused_ar.hip, one wave per SIMD; layer 1 on the fp16-split trig features)",
 }
 # the line's dtype: what the path computes in (fp32 values and outputs; the
 # conditioner's products on the fp16 matrix cores as a two-way split)
@@ -419,6 +430,7 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
         alg = (D * 4 + 4) * B if name.endswith("_chain") else (2 * D * 4 + 8) * B  # x (+ z, log|det|) or log p
         return {"kernel": name, "bound": bound, "achieved": round(achieved, 2),
                 "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "mfma_frac": round(floors["mfma_ms"] / mean_ms, 4),
                 "traffic": traffic, **hbm_fields(traffic, alg, mean_ms),
                 "launches": n_launch, "mean_ms": round(mean_ms, 4),
                 "floor_ms": round(t_floor, 4), "floors": floors,
@@ -501,7 +513,8 @@ def roofline_ar(kw, B, per, n_launch, mean_ms, traffic, insts):
     peak = flops / (t_floor * 1e-3) / 1e12
     alg = (2 * dim * 4 + 8) * B * per
     return {"kernel": "nfk_fused_ar", "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
-            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "mfma_frac": round(t_mfma / mean_ms, 4),
+            "traffic": traffic,
             **hbm_fields(traffic, alg, mean_ms), "launches": n_launch, "mean_ms": round(mean_ms, 4),
             "floor_ms": round(t_floor, 4), "floors": floors,
             "per_launch": "%d samples x %g layers x %.0f flop (reference FCNN flops, fp32-equivalent)"

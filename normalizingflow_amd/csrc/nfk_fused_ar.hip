@@ -59,7 +59,22 @@ namespace {
 #ifndef NFK_AR_NS
 #define NFK_AR_NS 3
 #endif
-constexpr int kArNS = NFK_AR_NS;  // output tiles per sub-record
+constexpr int kArNS = NFK_AR_NS;  // output tiles per sub-record (hidden widths up to 4 k-blocks)
+// wider conditioners (the applications' H = 354: 11 k-blocks) take 2-tile
+// sub-records, so two 46-KiB slots and the spline slabs fit one CU's LDS
+#ifdef NFK_AR_DIAG_NS2  // diagnostic: 2-tile sub-records for every width
+__host__ __device__ constexpr int ar_ns_for(int) { return 2; }
+#else
+__host__ __device__ constexpr int ar_ns_for(int kbh) { return kbh <= 4 ? kArNS : 2; }
+#endif
+// waves per SIMD the register allocation targets: two for the NSF_CL-sized
+// conditioners, one (512 registers: MFMA accumulators in AGPRs) for the wide
+// ones, which run 4-wave workgroups only (NFK_AR_WAVES is not applied)
+#ifdef NFK_AR_DIAG_ONEWAVE  // diagnostic: every width compiled for one wave per SIMD (512 registers)
+__host__ __device__ constexpr int ar_min_waves(int) { return 1; }
+#else
+__host__ __device__ constexpr int ar_min_waves(int kbh) { return kbh <= 4 ? 2 : 1; }
+#endif
 // waves per workgroup, 16 samples each: 4 (one per SIMD; two independent
 // workgroups share a CU, so the two waves on a SIMD run unsynchronised phases)
 // or 8 (one workgroup per CU; half the weight stream per sample, but its two
@@ -71,7 +86,7 @@ constexpr int kArMaxDim = 128;
 // (the NSF_CL kernels' f16 tail step), 2 = 5..16 features (a 16-row half tile:
 // two 16x16x32 MFMAs per output tile instead of a padded 32-feature k-block)
 struct ArDims {
-    int KBH, T1, HT, P, NO, NH, N3, SPC, NTG, KB1M, SB, PS;
+    int KBH, T1, HT, P, NO, NS, NH, N3, SPC, NTG, KB1M, SB, PS;
 };
 
 __host__ __device__ inline ArDims ar_dims(int hidden, int K, int dim) {
@@ -82,12 +97,13 @@ __host__ __device__ inline ArDims ar_dims(int hidden, int K, int dim) {
     d.HT = 2 * d.KBH + (d.T1 ? 1 : 0);
     d.P = 3 * K - 1;
     d.NO = (d.P + 15) / 16;
-    d.NH = (d.HT + kArNS - 1) / kArNS;
-    d.N3 = (d.NO + kArNS - 1) / kArNS;
+    d.NS = ar_ns_for(d.KBH);
+    d.NH = (d.HT + d.NS - 1) / d.NS;
+    d.N3 = (d.NO + d.NS - 1) / d.NS;
     d.SPC = 2 * d.NH + d.N3;
-    d.NTG = d.T1 == 1 ? (kArNS + 1) / 2 : (d.T1 == 2 ? 2 * kArNS : 0);
+    d.NTG = d.T1 == 1 ? (d.NS + 1) / 2 : (d.T1 == 2 ? 2 * d.NS : 0);
     d.KB1M = dim > 1 ? (2 * (dim - 1) + 31) / 32 : 1;
-    const int s1 = d.KB1M * kArNS * 2 + 1, s2 = d.KBH * kArNS * 2 + d.NTG + 1;
+    const int s1 = d.KB1M * d.NS * 2 + 1, s2 = d.KBH * d.NS * 2 + d.NTG + 1;
     d.SB = s1 > s2 ? s1 : s2;
     d.PS = 16 * d.NO + 4;  // slab row stride: = 4 mod 8 floats, conflict-free 16-B reads
     return d;
@@ -110,7 +126,12 @@ inline size_t ar_lds_bytes(const ArDims& d, int dim, bool inv, int nw = kArWaves
     X(2, 2, 10, 4)  /* applications/input/Gaussian.yaml: dim 40, K 10, H 80 (64 + a 16 tail) */ \
     X(3, 1, 8, 4)   /* H = 100 (config.py:40), K 8, dim <= 64 */                                 \
     X(3, 1, 10, 4)  /* H = 100, K 10 */                                                           \
-    X(3, 1, 32, 4)  /* config.py defaults: H = 100, K 32 (nsplines), dim <= 64 */
+    X(3, 1, 32, 4)  /* config.py defaults: H = 100, K 32 (nsplines), dim <= 64 */                \
+    X(11, 1, 32, 6) /* Einstein / LJ / Fe_*.yaml: H = 354 (11 k-blocks + 2), K 32, dim <= 96 */ \
+    NFK_AR_DIAG_SHAPES(X)
+#ifndef NFK_AR_DIAG_SHAPES
+#define NFK_AR_DIAG_SHAPES(X)
+#endif
 
 inline bool ar_instance(const ArDims& d, int K, int* kbx) {
 #define NFK_AR_CHK(h, t, k, x)                                          \
@@ -124,12 +145,13 @@ inline bool ar_instance(const ArDims& d, int K, int* kbx) {
 }
 
 inline bool ar_ok(int dim, int hidden, int K) {
-    if (dim < 2 || dim > kArMaxDim || hidden < 1 || hidden > 132 || K < 2) return false;
+    if (dim < 2 || dim > kArMaxDim || hidden < 1 || K < 2) return false;
     const ArDims d = ar_dims(hidden, K, dim);
     int kbx;
     if (!ar_instance(d, K, &kbx)) return false;
-    // both directions fit one workgroup per CU
-    return ar_lds_bytes(d, dim, false) <= (size_t)kLdsBytes && ar_lds_bytes(d, dim, true) <= (size_t)kLdsBytes;
+    // both directions fit one workgroup per CU (at the most waves a workgroup may have)
+    const int nw = ar_min_waves(d.KBH) == 1 ? 4 : kArWavesMax;
+    return ar_lds_bytes(d, dim, false, nw) <= (size_t)kLdsBytes && ar_lds_bytes(d, dim, true, nw) <= (size_t)kLdsBytes;
 }
 
 // ---------------------------------------------------------------------------
@@ -186,20 +208,20 @@ __device__ int ar_scale_exp(float maxw) {  // 2^s max|W| in [2^14, 2^15)
 // record's bias block [tile][row].  Block order and word layout are those
 // gemm_h reads (nfk_fused_impl.h: k-block fragments, tail_word, bias).
 template <class ValF, class BiasF>
-__device__ uint32_t ar_sub_word(int blk, int wl, int kbn, int t1, int nt, int T0, float sc, float bsc, ValF val,
-                                BiasF bias) {
-    const int nf = kbn * kArNS * 2, ntg = t1 == 1 ? (kArNS + 1) / 2 : 0;
+__device__ uint32_t ar_sub_word(int ns, int blk, int wl, int kbn, int t1, int nt, int T0, float sc, float bsc,
+                                ValF val, BiasF bias) {
+    const int nf = kbn * ns * 2, ntg = t1 == 1 ? (ns + 1) / 2 : 0;
     if (t1 == 2 && blk >= nf) {
         // 16-feature tail: the bias block first, then per tile {A1, A2}: lane l
         // (row l & 15, lane group g = l >> 4) element j of A1 = lo (j < 4) / hi
         // (j >= 4) weight of feature 32 kbn + 4 g + (j & 3), of A2 = hi (j < 4) / 0;
         // against B1 = {hi, lo} and B2 = {hi, 0} of the half tile's 4 rows
-        if (blk == nf) {
-            const int t = wl >> 4, r = wl & 15;
-            return __float_as_uint(t < nt ? bias(t, r) * bsc : 0.0f);
+        if (blk == nf) {  // the sub-record's own tiles (gemm_h BREL)
+            const int tt = wl >> 4, t = T0 + tt, r = wl & 15;
+            return __float_as_uint(tt < ns && t < nt ? bias(t, r) * bsc : 0.0f);
         }
         const int tt = blk - nf - 1;
-        if (tt >= 2 * kArNS) return 0u;
+        if (tt >= 2 * ns) return 0u;
         const int t = T0 + (tt >> 1), which = tt & 1;
         if (t >= nt) return 0u;
         const int lane = wl >> 2, g = lane >> 4, row = lane & 15, jp = 2 * (wl & 3);
@@ -217,7 +239,7 @@ __device__ uint32_t ar_sub_word(int blk, int wl, int kbn, int t1, int nt, int T0
         return (uint32_t)__builtin_bit_cast(uint16_t, hv[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, hv[1]) << 16);
     }
     if (blk < nf) {
-        const int part = blk & 1, idx = blk >> 1, kb = idx / kArNS, t = T0 + (idx - kb * kArNS);
+        const int part = blk & 1, idx = blk >> 1, kb = idx / ns, t = T0 + (idx - kb * ns);
         if (t >= nt) return 0u;
         const int lane = wl >> 2, j = 2 * (wl & 3), k0 = 32 * kb + 8 * (lane >> 4) + j;
         return nfk_f16_part_pair(val(t, lane & 15, k0) * sc, val(t, lane & 15, k0 + 1) * sc, part);
@@ -229,9 +251,9 @@ __device__ uint32_t ar_sub_word(int blk, int wl, int kbn, int t1, int nt, int T0
         return nfk_f16_part_pair(val(t, lane & 15, kb0 + j) * sc, val(t, lane & 15, kb0 + j + 1) * sc,
                                  qq == 2 ? 1 : 0);
     }
-    if (blk == nf + ntg) {
-        const int t = wl >> 4, r = wl & 15;
-        return __float_as_uint(t < nt ? bias(t, r) * bsc : 0.0f);
+    if (blk == nf + ntg) {  // the sub-record's own tiles (gemm_h BREL): records of > 16 tiles
+        const int tt = wl >> 4, t = T0 + tt, r = wl & 15;
+        return __float_as_uint(tt < ns && t < nt ? bias(t, r) * bsc : 0.0f);
     }
     return 0u;  // padding to SB blocks
 }
@@ -267,7 +289,7 @@ __global__ __launch_bounds__(256) void k_ar_pack(ArPackArgs a) {
             const float* b1 = pw[1];
             const int kb1 = (2 * i + 31) / 32;
             v = ar_sub_word(
-                blk, wl, kb1, 0, d.HT, kArNS * u, ldexpf(1.0f, s1), ldexpf(1.0f, s1 + 14),
+                d.NS, blk, wl, kb1, 0, d.HT, d.NS * u, ldexpf(1.0f, s1), ldexpf(1.0f, s1 + 14),
                 [&](int t, int r, int k) -> float {
                     const int f = hid(t, r);
                     if (f >= H || k >= 2 * i) return 0.0f;
@@ -281,7 +303,7 @@ __global__ __launch_bounds__(256) void k_ar_pack(ArPackArgs a) {
             const float* W2 = pw[2];
             const float* b2 = pw[3];
             v = ar_sub_word(
-                blk, wl, kbh, d.T1, d.HT, kArNS * (u - d.NH), ldexpf(1.0f, s2), ldexpf(1.0f, s2 + 14),
+                d.NS, blk, wl, kbh, d.T1, d.HT, d.NS * (u - d.NH), ldexpf(1.0f, s2), ldexpf(1.0f, s2 + 14),
                 [&](int t, int r, int k) -> float {
                     const int f = hid(t, r);
                     return (f < H && k < H) ? W2[(int64_t)f * H + k] : 0.0f;
@@ -295,7 +317,7 @@ __global__ __launch_bounds__(256) void k_ar_pack(ArPackArgs a) {
             const float* b3 = pw[5];
             const int P = d.P;
             v = ar_sub_word(
-                blk, wl, kbh, d.T1, d.NO, kArNS * (u - 2 * d.NH), ldexpf(1.0f, s3), ldexpf(1.0f, s3 + 14),
+                d.NS, blk, wl, kbh, d.T1, d.NO, d.NS * (u - 2 * d.NH), ldexpf(1.0f, s3), ldexpf(1.0f, s3 + 14),
                 [&](int t, int r, int k) -> float {
                     const int p = 16 * t + r;
                     return (p < P && k < H) ? W3[(int64_t)p * H + k] : 0.0f;
@@ -325,27 +347,27 @@ struct ArArgs {
 
 // GEMM over the sub-records J, J + 1, ... of an NT-tile record; end() after
 // each ends the sub-record (barrier, next copy) and moves to the next slot.
-template <int KB, bool T1, int NT, int J, class SlotF, class EndF>
+template <int NS, int KB, bool T1, int NT, int J, class SlotF, class EndF>
 __device__ __forceinline__ void ar_parts(const h8 (&bh)[KB], const h8 (&bl)[KB], h4 bt, int lane,
                                          f32x4 (&acc)[NT], SlotF slot, EndF end) {
-    constexpr int T0 = J * kArNS;
-    constexpr int N = (NT - T0) < kArNS ? (NT - T0) : kArNS;
-    gemm_h<KB, T1, N, kArNS, T0, NT>(bh, bl, bt, slot(), lane, acc);
+    constexpr int T0 = J * NS;
+    constexpr int N = (NT - T0) < NS ? (NT - T0) : NS;
+    gemm_h<KB, T1, N, NS, T0, NT, true, T0 + NS >= NT>(bh, bl, bt, slot(), lane, acc);
     end();
-    if constexpr (T0 + kArNS < NT) ar_parts<KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end);
+    if constexpr (T0 + NS < NT) ar_parts<NS, KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end);
 }
 
 // The same over a hidden width with a 16-feature tail (tail kind 2): the full
 // k-blocks by gemm_h (its bias block sits right after them), then per output
 // tile the tail's two MFMAs on B1 = {hi, lo}, B2 = {hi, 0} of the half tile
-template <int KB, int NT, int J, class SlotF, class EndF>
+template <int NS, int KB, int NT, int J, class SlotF, class EndF>
 __device__ __forceinline__ void ar_parts16(const h8 (&bh)[KB], const h8 (&bl)[KB], h8 b1, h8 b2, int lane,
                                            f32x4 (&acc)[NT], SlotF slot, EndF end) {
-    constexpr int T0 = J * kArNS;
-    constexpr int N = (NT - T0) < kArNS ? (NT - T0) : kArNS;
+    constexpr int T0 = J * NS;
+    constexpr int N = (NT - T0) < NS ? (NT - T0) : NS;
     const float4* sl = slot();
-    gemm_h<KB, false, N, kArNS, T0, NT>(bh, bl, h4{0, 0, 0, 0}, sl, lane, acc);
-    const float4* t16 = sl + (KB * kArNS * 2 + 1) * 64;
+    gemm_h<KB, false, N, NS, T0, NT, true>(bh, bl, h4{0, 0, 0, 0}, sl, lane, acc);
+    const float4* t16 = sl + (KB * NS * 2 + 1) * 64;
 #pragma unroll
     for (int t = 0; t < N; ++t) {
         const h8 a1 = __builtin_bit_cast(h8, t16[(2 * t) * 64 + lane]);
@@ -353,8 +375,9 @@ __device__ __forceinline__ void ar_parts16(const h8 (&bh)[KB], const h8 (&bl)[KB
         acc[T0 + t] = mfma16(a1, b1, acc[T0 + t]);
         acc[T0 + t] = mfma16(a2, b2, acc[T0 + t]);
     }
+    if constexpr (T0 + NS >= NT) mfma_result_wait();
     end();
-    if constexpr (T0 + kArNS < NT) ar_parts16<KB, NT, J + 1>(bh, bl, b1, b2, lane, acc, slot, end);
+    if constexpr (T0 + NS < NT) ar_parts16<NS, KB, NT, J + 1>(bh, bl, b1, b2, lane, acc, slot, end);
 }
 
 // activations of a hidden layer with a 16-feature tail: the full tiles by
@@ -386,13 +409,29 @@ __device__ __forceinline__ void trig_split(float v, float pi, float bnd, _Float1
     sl = (_Float16)(s - (float)sh);
 }
 
+#ifdef NFK_AR_DIAG_DUMP  // diagnostic: conditioner 1's activations and logits of workgroup 0
+__device__ float g_ar_dbg[3 * 64 * 512];
+template <int HT>
+__device__ void ar_dump_act(int stage, const f32x4 (&h)[HT], int kbh, int row, int q) {
+    for (int t = 0; t < HT; ++t)
+        for (int r = 0; r < 4; ++r) {
+            const int f = hid_feature(t, 4 * q + r, kbh);
+            if (f < 512) g_ar_dbg[(stage * 64 + row) * 512 + f] = h[t][r] * (1.0f / kActScale);
+        }
+}
+extern "C" int nfk_ar_dbg_copy(float* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ar_dbg), sizeof(g_ar_dbg), 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 template <int KBH, int TK, int K, int KBX, bool INV, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
+__global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs a) {
     constexpr int kArWaves = NW;
     constexpr bool T1 = TK == 1;  // the f16 4-feature tail step; TK == 2: the 16-feature tail
     constexpr int HT = 2 * KBH + (TK ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
-    constexpr int NH = (HT + kArNS - 1) / kArNS, N3 = (NO + kArNS - 1) / kArNS, SPC = 2 * NH + N3;
-    constexpr int NTG = TK == 1 ? (kArNS + 1) / 2 : (TK == 2 ? 2 * kArNS : 0);
+    constexpr int NS = ar_ns_for(KBH);
+    constexpr int NH = (HT + NS - 1) / NS, N3 = (NO + NS - 1) / NS, SPC = 2 * NH + N3;
+    constexpr int NTG = TK == 1 ? (NS + 1) / 2 : (TK == 2 ? 2 * NS : 0);
     constexpr int PS = 16 * NO + 4, G = ar_group(INV, PS);
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -414,7 +453,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
     int st_s = 0, st_i = 1, st_u = 0;
     auto stage_next = [&]() {
         if (st_s >= a.nsr) return;
-        const int nblk = st_u < NH ? ((2 * st_i + 31) / 32) * kArNS * 2 + 1 : KBH * kArNS * 2 + NTG + 1;
+        const int nblk = st_u < NH ? ((2 * st_i + 31) / 32) * NS * 2 + 1 : KBH * NS * 2 + NTG + 1;
         stage_record<kArWaves>(a.pack + 256 + (int64_t)st_s * a.sb * 256, nblk, (st_s & 1) ? slot1 : slot0, wid,
                                lane);
         ++st_s;
@@ -459,6 +498,11 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         stage_next();  // sub-record s + 2
+#ifdef NFK_AR_DIAG_SYNC  // diagnostic: every copy waited for at once (no copy in flight during a GEMM)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#endif
         ++s;
     };
     const float c21 = -2.0f * kL2E * un1, c22 = -2.0f * kL2E * un2;
@@ -499,13 +543,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
                         ml[KB - 1][j] = j < lim ? ml[KB - 1][j] : (_Float16)0.0f;
                     }
                 }
-                ar_parts<KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end);
+                ar_parts<NS, KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end);
             };
             switch (kb1) {
                 case 1: layer1(std::integral_constant<int, 1>{}); break;
                 case 2: if constexpr (KBX >= 2) layer1(std::integral_constant<int, 2>{}); break;
                 case 3: if constexpr (KBX >= 3) layer1(std::integral_constant<int, 3>{}); break;
                 case 4: if constexpr (KBX >= 4) layer1(std::integral_constant<int, 4>{}); break;
+                case 5: if constexpr (KBX >= 5) layer1(std::integral_constant<int, 5>{}); break;
+                case 6: if constexpr (KBX >= 6) layer1(std::integral_constant<int, 6>{}); break;
                 default: break;
             }
             f32x4 o[NO];
@@ -514,20 +560,31 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fused_ar(ArArgs a) {
                 act_operands16<KBH, HT>(h, c21, bh, bl, b1, b2);
                 {
                     f32x4 h2[HT];
-                    ar_parts16<KBH, HT, 0>(bh, bl, b1, b2, lane, h2, slot, end);
+                    ar_parts16<NS, KBH, HT, 0>(bh, bl, b1, b2, lane, h2, slot, end);
                     act_operands16<KBH, HT>(h2, c22, bh, bl, b1, b2);
                 }
-                ar_parts16<KBH, NO, 0>(bh, bl, b1, b2, lane, o, slot, end);
+                ar_parts16<NS, KBH, NO, 0>(bh, bl, b1, b2, lane, o, slot, end);
             } else {
                 act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
+#ifdef NFK_AR_DIAG_DUMP
+                if (i == 1 && blockIdx.x == 0) ar_dump_act<HT>(0, h, KBH, wid * 16 + sl, q);
+#endif
                 {
                     f32x4 h2[HT];
-                    ar_parts<KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+                    ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
                     act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
+#ifdef NFK_AR_DIAG_DUMP
+                    if (i == 1 && blockIdx.x == 0) ar_dump_act<HT>(1, h2, KBH, wid * 16 + sl, q);
+#endif
                 }
-                ar_parts<KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+                ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
             }
             // logits (unscaled: the exact power of two) into the slab, [sample][param]
+#ifdef NFK_AR_DIAG_DUMP
+            if (i == 1 && blockIdx.x == 0)
+                for (int t = 0; t < NO; ++t)
+                    for (int r = 0; r < 4; ++r) g_ar_dbg[(2 * 64 + wid * 16 + sl) * 512 + 16 * t + 4 * q + r] = o[t][r] * un3;
+#endif
 #pragma unroll
             for (int t = 0; t < NO; ++t) {
                 const int p = 16 * t + 4 * q;
@@ -614,11 +671,20 @@ int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
         const char* e = std::getenv("NFK_AR_WAVES");
         return (e != nullptr && e[0] == '8') ? 8 : 4;
     }();
-    const int nw = nw_env;
-    const size_t lds = ar_lds_bytes(d, a.dim, inv, nw);
+    constexpr bool wide = ar_min_waves(KBH) == 1;  // one workgroup of 4 waves per CU
+    const int nw = wide ? 4 : nw_env;
+    size_t lds = ar_lds_bytes(d, a.dim, inv, nw);
+#ifdef NFK_AR_DIAG_PAD  // diagnostic: LDS padded to 96 KiB, one workgroup (one wave per SIMD) per CU
+    lds = lds < 96 * 1024 ? 96 * 1024 : lds;
+#endif
     const int64_t per = (int64_t)nw * 16;
     const dim3 g((unsigned)((a.batch + per - 1) / per)), b(64 * nw);
-    if (nw == 8) {
+    if constexpr (wide) {
+        if (inv)
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, true, 4>), g, b, lds, st, a);
+        else
+            hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, false, 4>), g, b, lds, st, a);
+    } else if (nw == 8) {
         if (inv)
             hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, true, 8>), g, b, lds, st, a);
         else

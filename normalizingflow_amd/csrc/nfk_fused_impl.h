@@ -420,6 +420,18 @@ __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, 
     }
 }
 
+// Wait after a GEMM's last MFMA before its accumulators are read (32 wait
+// states).  Measured on the wide fused NSF_AR (nfk_fused_ar.hip, one wave per
+// SIMD, accumulators in AGPRs): without it the last output tile's register 3
+// (the MFMA's last-written rows) was read stale in some builds -- the compiler's
+// own MFMA -> read wait states did not cover it (tools/dbg_ar_dump.py,
+// profiles/r4_ar_wide_debug.txt).
+__device__ __forceinline__ void mfma_result_wait() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // acc[t] = bias + 2^s W[tile t] . act^T: KBH k-blocks of 32 in the fp16
 // split, three MFMAs per (tile, k-block), small terms first, then the tail
 // step (T1: one f16 MFMA holding the three split products of the <= 4 tail
@@ -432,7 +444,12 @@ __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, 
 // tiles [T0, T0 + NT) of a record, at a tile stride of NS per k-block, then
 // the tail blocks holding them and the record's whole bias block; acc has NA
 // tiles and this call fills acc[T0 .. T0 + NT).  Whole records: NS = NA = NT.
-template <int KBH, bool T1, int NT, int NS = NT, int T0 = 0, int NA = NT>
+// BREL: the sub-record's bias block holds its own tiles (row t - T0; records
+// of more than 16 tiles, whose biases exceed one 1-KiB block); else the
+// record's whole bias block (tile t at row t).
+// WAIT: the last MFMA's results are read soon after (a record's last
+// sub-record): wait them out here (see kMfmaResultWait).
+template <int KBH, bool T1, int NT, int NS = NT, int T0 = 0, int NA = NT, bool BREL = false, bool WAIT = false>
 __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH], h4 btail,
                                        const float4* slot, int lane, f32x4 (&acc)[NA]) {
     constexpr int NPR = (NT + 1) / 2;  // tile pairs (the last may be a single tile)
@@ -443,7 +460,12 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
     const float4* tail = slot + KBH * NS * 2 * 64;
     const float4* bias = tail + NTG * 64;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[T0 + t] = as_f32x4(bias[(T0 + t) * 4 + q]);
+    for (int t = 0; t < NT; ++t) acc[T0 + t] = as_f32x4(bias[((BREL ? 0 : T0) + t) * 4 + q]);
+#ifdef NFK_DIAG_BIAS_NOP  // diagnostic: a wait between the bias initialisation and the first MFMA
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // fragments of step i into a ring slot: k-block step i = (kb, pr): tile
     // t0 = 2 pr {hi, lo}, tile t0 + 1 {hi, lo}; tail step N + pr: one 16-B
     // word per lane holding both tiles' tail fragments (tail block pr)
@@ -490,20 +512,30 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
             continue;
         }
         const h8 ahi0 = __builtin_bit_cast(h8, r[0]), alo0 = __builtin_bit_cast(h8, r[1]);
+#ifdef NFK_DIAG_MFMA_NOP  // diagnostic: a wait between the alternating MFMAs of a tile pair
+#define NFK_MN() do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_nop 7\n\ts_nop 3"); \
+                      __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define NFK_MN() do { } while (0)
+#endif
         if (two) {
             const h8 ahi1 = __builtin_bit_cast(h8, r[2]), alo1 = __builtin_bit_cast(h8, r[3]);
             acc[t0] = mfma16(alo0, bh[kb], acc[t0]);
             acc[t0 + 1] = mfma16(alo1, bh[kb], acc[t0 + 1]);
+            NFK_MN();
             acc[t0] = mfma16(ahi0, bl[kb], acc[t0]);
             acc[t0 + 1] = mfma16(ahi1, bl[kb], acc[t0 + 1]);
+            NFK_MN();
             acc[t0] = mfma16(ahi0, bh[kb], acc[t0]);
             acc[t0 + 1] = mfma16(ahi1, bh[kb], acc[t0 + 1]);
+            NFK_MN();
         } else {
             acc[t0] = mfma16(alo0, bh[kb], acc[t0]);
             acc[t0] = mfma16(ahi0, bl[kb], acc[t0]);
             acc[t0] = mfma16(ahi0, bh[kb], acc[t0]);
         }
     }
+    if constexpr (WAIT) mfma_result_wait();
 }
 
 // layer 1 from a whole layer-1 record (KBI f16 k-blocks x HT tiles, then the

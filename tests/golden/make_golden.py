@@ -476,6 +476,31 @@ def negdisc_cl_cases():
     print("model: reference asserts on %d of %d knife-edge rows" % (len(m_rows), n))
 
 
+def case_layer_seeded(name, ctor, kwargs, x, seed=1234):
+    """case_layer for a layer too large to commit its weights (the
+    applications' NSF_AR: 18 M parameters): the fixture holds the seed and, per
+    state_dict entry, the fp64 sum, the fp64 sum of squares and the first 8
+    values; tests/golden_io.py rebuilds the weights from the seed through the
+    package's own constructor (same init order as the reference) and checks
+    them against these before use."""
+    torch.manual_seed(seed)
+    layer = ctor(**kwargs)
+    arrays = dict(x=x)
+    with torch.no_grad():
+        z, ld = layer.forward(x.clone())
+        arrays.update(z=z, ld=ld)
+        xi, ldi = layer.inverse(z.clone())
+        arrays.update(rt_x=xi, rt_ld=ldi)
+        xa, lda = layer.inverse(x.clone())
+        arrays.update(inv_x=xa, inv_ld=lda)
+    for k, v in layer.state_dict().items():
+        v64 = v.detach().double().flatten()
+        arrays["sdsum." + k] = torch.stack([v64.sum(), v64.square().sum()])
+        arrays["sdhead." + k] = v.detach().flatten()[:8].clone()
+    meta = dict(kind="layer", type=ctor.__name__, kwargs=kwargs, seed=seed, sd_from_seed=True)
+    _save(name, meta, arrays)
+
+
 def ar_cases():
     """NSF_AR at the shapes of the fused layer kernel (nfk_fused_ar): the
     applications' Gaussian.yaml flow (nparticles 20 x dim 2 = 40 coordinates,
@@ -488,9 +513,22 @@ def ar_cases():
     case_layer("nsfar_d24_k32_h100", rflows.NSF_AR, dict(dim=24, K=32, B=3, hidden_dim=100), x24)
 
 
+def ar_app_cases():
+    """NSF_AR at the applications' own shape: Einstein.yaml / LJ.yaml / Fe_*.yaml
+    (flow NSF_AR, nsplines 32, hidden_dim 354; nparticles 32 x dim 3 = 96
+    coordinates, setup.py:48, 57-58), B = (nparticles / (8 rho))^(1/3) at
+    Einstein's rho 1.28 (setup.py:42-43); positions inside the box mostly."""
+    B = (32 / (8 * 1.28)) ** (1.0 / 3.0)
+    g = torch.Generator().manual_seed(37)
+    x = torch.randn(64, 96, generator=g) * (0.6 * B)
+    case_layer_seeded("nsfar_d96_k32_h354", rflows.NSF_AR, dict(dim=96, K=32, B=B, hidden_dim=354), x)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["ar"]:
         ar_cases()
+    elif sys.argv[1:] == ["ar_app"]:
+        ar_app_cases()
     elif sys.argv[1:] == ["negdisc_cl"]:
         negdisc_cl_cases()
     elif sys.argv[1:] == ["extra"]:

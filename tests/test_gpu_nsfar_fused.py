@@ -4,8 +4,10 @@ path (nf/flows.py:152-209).
 
 Shapes: the reference-generated fixtures nsfar_d4_k4 (H 16),
 nsfar_d40_k10_h80 (applications/input/Gaussian.yaml: 20 particles x 2 dims,
-nsplines 10, hidden 80, B 4) and nsfar_d24_k32_h100 (config.py defaults:
-nsplines 32, hidden 100), plus random ones.  Tolerances: z rtol 1e-5 / atol
+nsplines 10, hidden 80, B 4), nsfar_d24_k32_h100 (config.py defaults:
+nsplines 32, hidden 100) and nsfar_d96_k32_h354 (Einstein / LJ / Fe_*.yaml:
+32 particles x 3 dims, nsplines 32, hidden 354; weights rebuilt from the
+fixture's seed), plus random ones.  Tolerances: z rtol 1e-5 / atol
 2e-5, log|det| rtol 1e-5 / atol 5e-5 (a sum over dim columns), as in
 test_gpu_parity.py; the inverse conditions on its own outputs, so it is
 compared at 1e-4 absolute where the forward uses 2e-5."""
@@ -45,7 +47,7 @@ def _launches(fn):
     return out, {k: v[0] for k, v in summ.items()}
 
 
-@pytest.mark.parametrize("name", ["nsfar_d4_k4", "nsfar_d40_k10_h80", "nsfar_d24_k32_h100"])
+@pytest.mark.parametrize("name", ["nsfar_d4_k4", "nsfar_d40_k10_h80", "nsfar_d24_k32_h100", "nsfar_d96_k32_h354"])
 def test_fused_ar_vs_reference_golden(name, hip_device):
     meta, data, sd = gio.load(name)
     kw = meta["kwargs"]
@@ -68,7 +70,7 @@ def test_fused_ar_vs_reference_golden(name, hip_device):
 
 @pytest.mark.parametrize("dim,K,H,B,rows", [(40, 10, 80, 4.0, 3000), (17, 8, 100, 3.0, 1000),
                                            (64, 10, 100, 3.0, 2049), (2, 4, 16, 3.0, 77),
-                                           (33, 32, 100, 2.5, 640)])
+                                           (33, 32, 100, 2.5, 640), (96, 32, 354, 1.462, 333)])
 def test_fused_ar_vs_oracle_and_unfused(dim, K, H, B, rows, hip_device):
     """Random weights and ragged batches: the fused layer vs the oracle, and
     the unfused per-column path (library GEMMs + nfk_rqs_coupling) vs the
@@ -93,10 +95,12 @@ def test_fused_ar_vs_oracle_and_unfused(dim, K, H, B, rows, hip_device):
             zu, ldu = layer(xd)
         finally:
             config.USE_FUSED = prev
+    # log|det| sums dim columns: its slack grows with dim (5e-5 up to 40 columns)
+    ld_atol = LD_ATOL * max(1.0, dim / 40.0)
     close(z, z_ref, Z_RTOL, Z_ATOL)
-    close(ld, ld_ref, LD_RTOL, LD_ATOL)
+    close(ld, ld_ref, LD_RTOL, ld_atol)
     close(zu, z_ref, Z_RTOL, Z_ATOL)
-    close(ldu, ld_ref, LD_RTOL, LD_ATOL)
+    close(ldu, ld_ref, LD_RTOL, ld_atol)
     close(xi, xi_ref, 1e-5, 1e-4)
     close(ldi, ldi_ref, 1e-5, 1e-4)
     flush_status_checks()

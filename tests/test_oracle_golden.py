@@ -42,10 +42,14 @@ def test_layer_fixture(name):
     z, ld = orc.apply_layer(spec, d["x"], sd)
     _close(z, d["z"]); _close(ld.expand_as(d["ld"]), d["ld"])
     if "rt_x" in d:
+        # NSF_AR's inverse is sequential (each inverted coordinate conditions the
+        # next ones, flows.py:191-209): ulp-level spline differences propagate
+        # through dim conditioners, so its slack grows with dim (1e-5 at 24)
+        at = 1e-5 * max(1.0, meta["kwargs"].get("dim", 0) / 24.0) if meta["type"] == "NSF_AR" else 1e-5
         xi, ldi = orc.apply_layer(spec, d["z"], sd, inverse=True)
-        _close(xi, d["rt_x"], atol=1e-5); _close(ldi, d["rt_ld"], atol=1e-5)
+        _close(xi, d["rt_x"], atol=at); _close(ldi, d["rt_ld"], atol=at)
         xa, lda = orc.apply_layer(spec, d["x"], sd, inverse=True)
-        _close(xa, d["inv_x"], atol=1e-5); _close(lda, d["inv_ld"], atol=1e-5)
+        _close(xa, d["inv_x"], atol=at); _close(lda, d["inv_ld"], atol=at)
     if "z_f64" in d:
         sd64 = {k: v.double() for k, v in sd.items()}
         z64, ld64 = orc.apply_layer(spec, d["x"].double(), sd64)
