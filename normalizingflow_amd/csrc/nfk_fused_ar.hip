@@ -494,6 +494,7 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     int64_t s = 0;  // the sub-record the next GEMM reads
     auto slot = [&]() -> const float4* { return (s & 1) ? slot1 : slot0; };
     auto end = [&]() {
+        gemm_fence();
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");

@@ -426,6 +426,21 @@ __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, 
 // (the MFMA's last-written rows) was read stale in some builds -- the compiler's
 // own MFMA -> read wait states did not cover it (tools/dbg_ar_dump.py,
 // profiles/r4_ar_wide_debug.txt).
+// Fence that ends a GEMM segment before its workgroup barrier.  The barrier
+// and the copy waits are inline asm, which orders memory operations only: the
+// compiler sank a segment's last MFMAs below the barrier, and on the path that
+// skips the next copy (the stream's last sub-records) the allocator's AGPR ->
+// VGPR copies of their accumulators followed ~3 instructions after the MFMA --
+// stale rows on gfx950 (tools/ubench_mfma_raw.hip: a v_accvgpr_read of a
+// 16x16x32 MFMA result needs 5-8 wait states; profiles/r4_mfma_hazards.txt).
+// The scheduling fence keeps every MFMA above the barrier and the s_nop gives
+// the last one its wait states.
+__device__ __forceinline__ void gemm_fence() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ void mfma_result_wait() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7");

@@ -129,6 +129,9 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
         ++nsub;
     };
     auto step = [&](float4* freed) {
+#ifndef NFK_VJP_NO_FENCE
+        gemm_fence();
+#endif
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");

@@ -46,32 +46,46 @@ def _knot_distance(sd, x, size, dim, K, B, mask, inverse):
     return (up[..., None] - edges).abs().amin(dim=(1, 2))
 
 
-def _assert_grads_close(names, got, ref, tol, knife=None):
-    """Every gradient within tol of its largest element, except that dL/dx may
-    differ in rows with a knife-edge element: an input within an ulp-level
-    distance of a knot can take the neighbouring bin in one path (the two
-    recomputes' logits differ in their last bits), and d log f'(x)/dx -- the
-    log|det| part of dL/dx -- jumps there (f is C1, not C2); the jump reaches
-    the row's lower coordinates through the conditioner.  ``knife(rows)``
-    gives each row's fp64 distance to its nearest knot: every differing row
-    must be within 1e-5 of one, and at most 1 in 10^5 rows may differ.
-    Parameter gradients (sums over the batch) must all agree -- to 5x the
-    tolerance when knife-edge rows exist, whose jumps they also sum."""
-    ptol = tol
+def _knife_rows(names, got, ref, tol, knife):
+    """Rows whose dL/dx differ beyond tol: each must be a knife-edge row, an
+    input within 1e-5 (fp64) of a knot, where one path can take the
+    neighbouring bin (the two recomputes' logits differ in their last bits) and
+    d log f'(x)/dx -- the log|det| part of dL/dx -- jumps (the spline is C1,
+    not C2); at most 1 in 10^5 rows may be one.  Returns them (CPU indices)."""
+    a, r = got[0].to(ref[0].device), ref[0]
+    bad = (a - r).abs() > tol * float(r.abs().max()) + 1e-6
+    rows = bad.any(dim=1).nonzero().flatten().cpu()
+    if rows.numel():
+        assert rows.numel() <= max(1, r.shape[0] // 100000), "%d rows differ" % rows.numel()
+        dist = knife(rows)
+        assert bool((dist < 1e-5).all()), "differing rows not at a knot: %s" % dist.tolist()
+    return rows
+
+
+def _assert_grads_close(names, got, ref, tol):
+    """Every gradient within tol of its largest element."""
     for n, a, r in zip(names, got, ref):
         a = a.to(r.device)
         scale = float(r.abs().max())
         bad = (a - r).abs() > tol * scale + 1e-6
-        if n == "x" and knife is not None and bool(bad.any()):
-            rows = bad.any(dim=1).nonzero().flatten().cpu()
-            assert rows.numel() <= max(1, r.shape[0] // 100000), "%d rows differ" % rows.numel()
-            dist = knife(rows)
-            assert bool((dist < 1e-5).all()), "differing rows not at a knot: %s" % dist.tolist()
-            ptol = 5 * tol
-            continue
-        bad = (a - r).abs() > ptol * scale + 1e-6
         assert not bool(bad.any()), "%s: %d elements beyond %.1e x max (max diff %.3g, scale %.3g)" % (
-            n, int(bad.sum()), ptol, float((a - r).abs().max()), scale)
+            n, int(bad.sum()), tol, float((a - r).abs().max()), scale)
+
+
+def _compare(names, run_a, run_b, w, v, tol, knife):
+    """Gradients of two paths on (w, v)-weighted losses: knife-edge rows
+    (_knife_rows) are checked, then zero-weighted (a row with no upstream
+    gradient contributes nothing to any gradient, in either path) and every
+    gradient is compared on the rest."""
+    got, ref = run_a(w, v), run_b(w, v)
+    rows = _knife_rows(names, got, ref, tol, knife)
+    if rows.numel():
+        w, v = w.clone(), v.clone()
+        w[rows.to(w.device)] = 0
+        v[rows.to(v.device)] = 0
+        got, ref = run_a(w, v), run_b(w, v)
+    _assert_grads_close(names, got, ref, tol)
+    return rows
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "s%d_k%d_h%d_m%d" % (s[0], s[2], s[3], s[4][0]))
@@ -156,17 +170,18 @@ def test_fused_vjp_full_occupancy_batch(inverse, hip_device):
         b = _grads(layer, x, w, v, inverse)
         for t1, t2 in zip(a, b):
             assert torch.equal(t1, t2)
-    prev = config.USE_FUSED_VJP
-    config.USE_FUSED_VJP = False
-    try:
-        plain = _grads(layer, x, w, v, inverse)
-    finally:
-        config.USE_FUSED_VJP = prev
+    def plain(ww, vv):
+        prev = config.USE_FUSED_VJP
+        config.USE_FUSED_VJP = False
+        try:
+            return _grads(layer, x, ww, vv, inverse)
+        finally:
+            config.USE_FUSED_VJP = prev
     names = ["x"] + [n for n, _ in layer.named_parameters()]
     sd = {k: t.detach().cpu() for k, t in layer.state_dict().items()}
     xc = x.cpu()
-    _assert_grads_close(names, a, plain, 2e-5,
-                        knife=lambda rows: _knot_distance(sd, xc[rows], 32, 2, 8, 3, [0], inverse))
+    _compare(names, lambda ww, vv: _grads(layer, x, ww, vv, inverse), plain, w, v, 2e-5,
+             knife=lambda rows: _knot_distance(sd, xc[rows], 32, 2, 8, 3, [0], inverse))
 
 
 @pytest.mark.parametrize("inverse", [False, True])
@@ -184,22 +199,29 @@ def test_fused_vjp_large_batch_vs_oracle(inverse, hip_device):
     w = torch.randn(B, 64, generator=g)
     v = torch.randn(B, generator=g)
     dev = layer.to(hip_device)
-    got = _grads(dev, x.to(hip_device), w.to(hip_device), v.to(hip_device), inverse)
-    assert dev.__dict__.get("_vjp_cache") is not None  # the fused kernel ran
     names = ["x"] + [n for n, _ in dev.named_parameters()]
-    gx, gp = [], {n: torch.zeros_like(sd[n]) for n in names[1:]}
-    for c in range(0, B, 1 << 15):
-        xo = x[c:c + (1 << 15)].clone().requires_grad_(True)
-        po = {k: t.clone().requires_grad_(True) for k, t in sd.items()}
-        zo, ldo = orc.nsf_cl(xo, po, "", 32, 2, 8, 3, [1], inverse=inverse)
-        r = torch.autograd.grad((zo * w[c:c + (1 << 15)]).sum() + (ldo * v[c:c + (1 << 15)]).sum(),
-                                [xo] + [po[n] for n in names[1:]])
-        gx.append(r[0])
-        for n, t in zip(names[1:], r[1:]):
-            gp[n] += t
-    ref = [torch.cat(gx)] + [gp[n] for n in names[1:]]
-    _assert_grads_close(names, got, ref, 1e-4,
-                        knife=lambda rows: _knot_distance(sd, x[rows], 32, 2, 8, 3, [1], inverse))
+    xd = x.to(hip_device)
+
+    def ours(ww, vv):
+        g = _grads(dev, xd, ww.to(hip_device), vv.to(hip_device), inverse)
+        assert dev.__dict__.get("_vjp_cache") is not None  # the fused kernel ran
+        return [t.cpu() for t in g]
+
+    def oracle(ww, vv):
+        gx, gp = [], {n: torch.zeros_like(sd[n]) for n in names[1:]}
+        for c in range(0, B, 1 << 15):
+            xo = x[c:c + (1 << 15)].clone().requires_grad_(True)
+            po = {k: t.clone().requires_grad_(True) for k, t in sd.items()}
+            zo, ldo = orc.nsf_cl(xo, po, "", 32, 2, 8, 3, [1], inverse=inverse)
+            r = torch.autograd.grad((zo * ww[c:c + (1 << 15)]).sum() + (ldo * vv[c:c + (1 << 15)]).sum(),
+                                    [xo] + [po[n] for n in names[1:]])
+            gx.append(r[0])
+            for n, t in zip(names[1:], r[1:]):
+                gp[n] += t
+        return [torch.cat(gx)] + [gp[n] for n in names[1:]]
+
+    _compare(names, ours, oracle, w, v, 1e-4,
+             knife=lambda rows: _knot_distance(sd, x[rows], 32, 2, 8, 3, [1], inverse))
 
 
 def test_train_batch_backward_reproducible(hip_device):
