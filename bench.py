@@ -605,10 +605,11 @@ def main():
         """auto: a HIP graph replay where launches are a visible part of the
         step -- the small-batch workloads (c1) and per-rank batches of at most
         2^17 rows (the 8-GPU strong-scaling shard), where the host-side launch
-        and status-copy overhead is ~2 % of a step."""
+        and status-copy overhead is ~2 % of a step.  Not ar354, whose step is
+        milliseconds at any batch (and whose roofline needs the kernel timer)."""
         if args.graph != "auto":
             return args.graph == "on"
-        return args.workload in DEFAULT_BATCH or B <= (1 << 17)
+        return args.workload == "c1" or (B <= (1 << 17) and args.workload != "ar354")
 
     def run(mode):
         """One mode's timed loop: W warm-up steps, then K steps bracketed by a

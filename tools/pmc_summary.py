@@ -38,7 +38,8 @@ def main():
     out = {}
     for k in kernels:
         m = {c: sum(v) / len(v) for (kk, c), v in vals.items() if kk == k}
-        short = re.sub(r"\(.*", "", k)[:80]
+        # drop the argument list only (names may hold "(anonymous namespace)")
+        short = re.sub(r"\((?!anonymous namespace\))[^()]*\)\s*$", "", k).replace("(anonymous namespace)::", "")[:90]
         print("==", short)
         for c in sorted(m):
             print("  %-36s %16.1f" % (c, m[c]))
