@@ -477,6 +477,13 @@ def hbm_fields(traffic, alg_bytes, mean_ms):
     return out
 
 
+def ar_weight_bytes(dim, K, H):
+    """Bytes of one NSF_AR layer's conditioner weights and biases at 4 B each
+    (FCNN(2i, 3K-1, H), i = 1 .. dim-1, flows.py:166-167)."""
+    P = 3 * K - 1
+    return 4 * sum(2 * i * H + H + H * H + H + P * H + P for i in range(1, dim))
+
+
 def ar_mfma_per_wave_layer(dim, K, H):
     """MFMA instructions of one 16-sample wave per NSF_AR layer in
     nfk_fused_ar's formulation: conditioner i = 1 .. dim-1 runs layer 1 over
@@ -511,7 +518,9 @@ def roofline_ar(kw, B, per, n_launch, mean_ms, traffic, insts):
             bound, t_floor = "valu-issue", t_valu
     achieved = flops / (mean_ms * 1e-3) / 1e12
     peak = flops / (t_floor * 1e-3) / 1e12
-    alg = (2 * dim * 4 + 8) * B * per
+    # x in, z and log|det| out, and every conditioner's weights once per launch
+    # (fp16 hi + lo: 4 B per weight; a launch must read them at least once)
+    alg = ((2 * dim * 4 + 8) * B + ar_weight_bytes(dim, K, H)) * per
     return {"kernel": "nfk_fused_ar", "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "mfma_frac": round(t_mfma / mean_ms, 4),
             "traffic": traffic,
@@ -537,7 +546,11 @@ def load_traffic(kernel, workload, batch=None):
         rec = tab.get(kernel)
     if rec is None or not rec.get("bytes_per_launch"):
         return None
-    # every entry was measured at 2^20 rows per launch: scaled to this batch
+    # an entry measured at another batch is scaled to this one (streaming
+    # kernels: bytes per row), unless its bytes do not scale with the batch
+    # (the fused NSF_AR's weight stream: "batch_exact")
+    if rec.get("batch_exact") and batch is not None and batch != rec.get("batch"):
+        return None
     scale = 1.0 if batch is None else batch / float(rec.get("batch", 1 << 20))
     return int(rec["bytes_per_launch"] * scale)
 

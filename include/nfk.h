@@ -221,6 +221,16 @@ int nfk_fused_ar_pack(const float* const* weights, const float* init_param, int3
 int nfk_fused_ar(const float* x, int64_t ldx, const float* pack, int32_t dim, int32_t hidden, int32_t K,
                  double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,
                  int64_t batch, int32_t inverse, int32_t* status, nfk_stream_t stream);
+/* The same with a workspace: a forward whose batch is too small to fill the
+ * GPU splits the conditioners over workgroups (they are independent given x,
+ * flows.py:182-189) when workspace holds nfk_fused_ar_workspace() floats (the
+ * per-column log|det| terms, summed in column order: results bitwise those of
+ * nfk_fused_ar).  A null or short workspace runs unsplit; 0 = none needed. */
+int64_t nfk_fused_ar_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch, int32_t inverse);
+int nfk_fused_ar_ws(const float* x, int64_t ldx, const float* pack, int32_t dim, int32_t hidden, int32_t K,
+                    double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,
+                    int64_t batch, int32_t inverse, int32_t* status, float* workspace, int64_t workspace_floats,
+                    nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Fused NSF coupling layer: conditioner MLP (FCNN, flows.py:20-35) on MFMA

@@ -68,6 +68,11 @@ SIGNATURES = {
         P, I64, P, I32, I32, I32,       # x, ldx, pack, dim, hidden, K
         F64, P, I64, P, I32,            # tail_bound, out, ldo, logdet, logdet_mode
         I64, I32, P, P]),               # batch, inverse, status, stream
+    "nfk_fused_ar_workspace": (ctypes.c_int64, [I32, I32, I32, I64, I32]),
+    "nfk_fused_ar_ws": (ctypes.c_int, [
+        P, I64, P, I32, I32, I32,       # x, ldx, pack, dim, hidden, K
+        F64, P, I64, P, I32,            # tail_bound, out, ldo, logdet, logdet_mode
+        I64, I32, P, P, I64, P]),       # batch, inverse, status, workspace, workspace_floats, stream
     "nfk_fused_nsf_supported": (ctypes.c_int, [I32, I32, I32, I32]),
     "nfk_fused_nsf_pack_elems": (ctypes.c_int64, [I32, I32, I32, I32]),
     "nfk_fused_nsf_pack": (ctypes.c_int, [P, P, P, P, P, P, I32, I32, I32, I32, P, P]),

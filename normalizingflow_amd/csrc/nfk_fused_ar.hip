@@ -341,6 +341,9 @@ struct ArArgs {
     int64_t ldx, ldo, batch;
     int32_t dim, mode, sb, kb1m;
     int64_t nsr;       // sub-records in the stream
+    int32_t csplit;    // forward: column ranges (1: the whole layer per workgroup)
+    int64_t rblocks;   // row blocks of the batch
+    float* ld_cols;    // csplit > 1: per-column log|det| terms [dim][batch], summed by k_ar_ld_sum
     float pi, bnd;     // trig features: (pi v) / B (nfk_trig_features' operation order)
     NfkSplineConst c;
 };
@@ -442,7 +445,22 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     float4* const slot1 = lds4 + a.sb * 64;
     float* const scr = reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + wid * (G * 16 * PS);
     int* const cst = reinterpret_cast<int*>(reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + kArWaves * G * 16 * PS);
-    const int64_t b0 = ((int64_t)blockIdx.x * kArWaves + wid) * 16;
+    // column range of this workgroup: the forward's conditioners are
+    // independent given x, so a small batch splits them over workgroups.
+    // Split grids are XCD-affine: blocks b and b + 8 share an XCD (round-robin
+    // dispatch, MI355X_MICROARCH.md), so virtual id v = (b % 8) G/8 + b / 8
+    // puts the row blocks of one column range on one XCD, whose L2 then
+    // fetches that range's weights once (G padded to a multiple of 8)
+    int sp = 0;
+    int64_t rbk = blockIdx.x;
+    if (a.csplit > 1) {
+        const int64_t v = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+        if (v >= a.rblocks * a.csplit) return;  // padding workgroup (uniform: before any barrier)
+        sp = (int)(v / a.rblocks);
+        rbk = v - (int64_t)sp * a.rblocks;
+    }
+    const int i_lo = (int)(((int64_t)sp * D) / a.csplit), i_hi = (int)(((int64_t)(sp + 1) * D) / a.csplit);
+    const int64_t b0 = (rbk * kArWaves + wid) * 16;
     const bool row_ok = b0 + sl < a.batch;
     const int64_t brow = row_ok ? b0 + sl : a.batch - 1;  // rows past the batch re-read the last one
 
@@ -450,9 +468,11 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     // layer-1 sub-records hold ceil(2i / 32) k-blocks.  Called once per
     // sub-record in stream order, so a cursor replaces the 64-bit division
     // s / SPC (a long SALU sequence per call: 15k SALU instructions a wave)
-    int st_s = 0, st_i = 1, st_u = 0;
+    int st_i = i_lo > 1 ? i_lo : 1, st_u = 0;
+    int64_t st_s = (int64_t)(st_i - 1) * SPC;
+    const int64_t s_end = (int64_t)(i_hi - 1) * SPC;  // conditioners st_i .. i_hi - 1
     auto stage_next = [&]() {
-        if (st_s >= a.nsr) return;
+        if (st_s >= s_end) return;
         const int nblk = st_u < NH ? ((2 * st_i + 31) / 32) * NS * 2 + 1 : KBH * NS * 2 + NTG + 1;
         stage_record<kArWaves>(a.pack + 256 + (int64_t)st_s * a.sb * 256, nblk, (st_s & 1) ? slot1 : slot0, wid,
                                lane);
@@ -491,7 +511,7 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     stage_next();
     dma_barrier();
 
-    int64_t s = 0;  // the sub-record the next GEMM reads
+    int64_t s = (int64_t)(st_i - 1) * SPC;  // the sub-record the next GEMM reads
     auto slot = [&]() -> const float4* { return (s & 1) ? slot1 : slot0; };
     auto end = [&]() {
         gemm_fence();
@@ -512,8 +532,8 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     h8 bh[KBH], bl[KBH];
     h4 btail = h4{0, 0, 0, 0};
 
-    for (int i = 0; i < D; ++i) {
-        const int c = INV ? 0 : (i % G);  // slab of column i
+    for (int i = i_lo; i < i_hi; ++i) {
+        const int c = INV ? 0 : ((i - i_lo) % G);  // slab of column i
         if (c == 0) {  // first column of a pass: this lane's spline input, loaded early
             const int col = INV ? i : i + (q < G ? q : 0);
             xin = col < D ? a.x[brow * a.ldx + col] : 0.0f;
@@ -594,7 +614,7 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
                         make_float4(o[t][0] * un3, o[t][1] * un3, o[t][2] * un3, o[t][3] * un3);
             }
         }
-        if (!(INV || c == G - 1 || i == D - 1)) continue;
+        if (!(INV || c == G - 1 || i == i_hi - 1)) continue;
 
         // ---- spline pass: columns i - c .. i (forward: lane group q takes
         // column i - c + q; inverse: every lane group column i)
@@ -617,8 +637,14 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
         const bool live = act && row_ok;
         if (live && (!INV || q == 0)) a.out[(b0 + sl) * a.ldo + col] = out;
         const float lm = act ? lad : 0.0f;
+        if (!INV && a.ld_cols != nullptr) {
+            // split columns: each term to its column's row, summed in column
+            // order by k_ar_ld_sum (the same additions as ld_acc below)
+            if (live) a.ld_cols[(int64_t)col * a.batch + b0 + sl] = lad;
+        } else {
 #pragma unroll
-        for (int g = 0; g < G; ++g) ld_acc = ld_acc + __shfl(lm, sl + 16 * g, 64);
+            for (int g = 0; g < G; ++g) ld_acc = ld_acc + __shfl(lm, sl + 16 * g, 64);
+        }
         // status bits of each column of the pass
         const uint64_t m_in = __ballot(live && inside), m_nd = __ballot(live && inside && nd);
         if (lane == 0) {
@@ -653,7 +679,7 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     }
 
     // ---- log|det| of the layer, the status words
-    if (q == 0 && row_ok && a.mode != 0) {
+    if (q == 0 && row_ok && a.mode != 0 && a.ld_cols == nullptr) {
         float* ld = a.logdet + b0 + sl;
         *ld = a.mode == 2 ? *ld + ld_acc : ld_acc;
     }
@@ -666,20 +692,54 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     }
 }
 
-template <int KBH, int T1, int K, int KBX>
-int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
+// log|det| of a column-split forward: the per-column terms summed in column
+// order from 0 (bitwise the single-range kernel's ld_acc), then mode 1/2
+__global__ __launch_bounds__(256) void k_ar_ld_sum(const float* cols, float* logdet, int64_t batch, int dim, int mode) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= batch) return;
+    float acc = 0.0f;
+    for (int c = 0; c < dim; ++c) acc = acc + cols[(int64_t)c * batch + r];
+    logdet[r] = mode == 2 ? logdet[r] + acc : acc;
+}
+
+// waves per workgroup of an instance (the wide conditioners: 4)
+inline int ar_waves(const ArDims& d) {
     static const int nw_env = [] {
         const char* e = std::getenv("NFK_AR_WAVES");
         return (e != nullptr && e[0] == '8') ? 8 : 4;
     }();
+    return ar_min_waves(d.KBH) == 1 ? 4 : nw_env;
+}
+
+// column ranges of a forward launch: enough workgroups for every CU
+// (resident workgroups per CU: 1 for the wide conditioners, else 8 / waves),
+// one range per conditioner at most; the inverse is sequential (1)
+inline int ar_csplit(const ArDims& d, int dim, int64_t batch, bool inv) {
+    if (inv || batch <= 0) return 1;
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int nw = ar_waves(d);
+    const int64_t rb = (batch + 16 * nw - 1) / (16 * nw);
+    const int64_t want = (int64_t)cus * (ar_min_waves(d.KBH) == 1 ? 1 : 8 / nw);
+    if (rb >= want) return 1;
+    const int64_t cs = (want + rb - 1) / rb;
+    return (int)(cs < dim ? cs : dim);
+}
+
+template <int KBH, int T1, int K, int KBX>
+int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
     constexpr bool wide = ar_min_waves(KBH) == 1;  // one workgroup of 4 waves per CU
-    const int nw = wide ? 4 : nw_env;
+    const int nw = ar_waves(d);
     size_t lds = ar_lds_bytes(d, a.dim, inv, nw);
 #ifdef NFK_AR_DIAG_PAD  // diagnostic: LDS padded to 96 KiB, one workgroup (one wave per SIMD) per CU
     lds = lds < 96 * 1024 ? 96 * 1024 : lds;
 #endif
-    const int64_t per = (int64_t)nw * 16;
-    const dim3 g((unsigned)((a.batch + per - 1) / per)), b(64 * nw);
+    const int64_t nblk = a.csplit > 1 ? (a.rblocks * a.csplit + 7) / 8 * 8 : a.rblocks;
+    const dim3 g((unsigned)nblk), b(64 * nw);
     if constexpr (wide) {
         if (inv)
             hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, true, 4>), g, b, lds, st, a);
@@ -696,6 +756,9 @@ int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
         else
             hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, false, 4>), g, b, lds, st, a);
     }
+    if (a.csplit > 1 && a.mode != 0)
+        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, a.ld_cols,
+                           a.logdet, a.batch, a.dim, a.mode);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -725,9 +788,22 @@ extern "C" int nfk_fused_ar_pack(const float* const* weights, const float* init_
     return e == hipSuccess ? 0 : (int)e;
 }
 
+extern "C" int64_t nfk_fused_ar_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch, int32_t inverse) {
+    if (!ar_ok(dim, hidden, K) || batch <= 0) return 0;
+    return ar_csplit(ar_dims(hidden, K, dim), dim, batch, inverse != 0) > 1 ? (int64_t)dim * batch : 0;
+}
+
 extern "C" int nfk_fused_ar(const float* x, int64_t ldx, const float* pack, int32_t dim, int32_t hidden, int32_t K,
                             double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,
                             int64_t batch, int32_t inverse, int32_t* status, nfk_stream_t stream) {
+    return nfk_fused_ar_ws(x, ldx, pack, dim, hidden, K, tail_bound, out, ldo, logdet, logdet_mode, batch, inverse,
+                           status, nullptr, 0, stream);
+}
+
+extern "C" int nfk_fused_ar_ws(const float* x, int64_t ldx, const float* pack, int32_t dim, int32_t hidden, int32_t K,
+                               double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,
+                               int64_t batch, int32_t inverse, int32_t* status, float* workspace,
+                               int64_t workspace_floats, nfk_stream_t stream) {
     if (!ar_ok(dim, hidden, K)) return nfk_set_error("nfk_fused_ar: shape not supported");
     if (batch < 0) return nfk_set_error("nfk_fused_ar: bad batch");
     if (batch == 0) return 0;
@@ -754,6 +830,13 @@ extern "C" int nfk_fused_ar(const float* x, int64_t ldx, const float* pack, int3
     // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:186-187)
     a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
     const bool inv = inverse != 0;
+    // the column split needs the per-column log|det| workspace; without one
+    // (or a smaller one) the launch keeps one range per workgroup
+    a.csplit = ar_csplit(d, dim, batch, inv);
+    if (a.csplit > 1 && (workspace == nullptr || workspace_floats < (int64_t)dim * batch)) a.csplit = 1;
+    a.ld_cols = a.csplit > 1 ? workspace : nullptr;
+    const int64_t per = (int64_t)ar_waves(d) * 16;
+    a.rblocks = (batch + per - 1) / per;
     hipStream_t st = (hipStream_t)stream;
     int kbx = 0;
     ar_instance(d, K, &kbx);

@@ -486,17 +486,23 @@ def fused_ar_pack(weights, init_param, dim, hidden, K):
     return pack, (table, init, flat)
 
 
-def fused_ar(x, pack, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, inverse=False, status=None):
-    """One fused NSF_AR layer (include/nfk.h nfk_fused_ar)."""
+def fused_ar(x, pack, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, inverse=False, status=None,
+             split=True):
+    """One fused NSF_AR layer (include/nfk.h nfk_fused_ar_ws; split=False: no
+    column split, the nfk_fused_ar launch)."""
     dev = _require_hip(x, pack, out, logdet, status)
     B = x.shape[0]
     xp, ldx = _mat(x, "x")
     op, ldo = _mat(out, "out")
     if x.shape[1] != dim or out.shape != x.shape:
         raise ValueError("fused_ar: x and out must be [B, %d]" % dim)
-    _timed("nfk_fused_ar", dev, "nfk_fused_ar", xp, ldx, pack.data_ptr(), dim, hidden, K, float(tail_bound),
+    # a batch too small to fill the GPU splits the forward's conditioners over
+    # workgroups; the per-column log|det| terms go through a workspace
+    nws = int(_lib.load().nfk_fused_ar_workspace(dim, hidden, K, B, 1 if inverse else 0)) if split else 0
+    ws = torch.empty(nws, dtype=F32, device=dev) if nws > 0 else None
+    _timed("nfk_fused_ar", dev, "nfk_fused_ar_ws", xp, ldx, pack.data_ptr(), dim, hidden, K, float(tail_bound),
            op, ldo, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0,
-           _vec(status, dim, "status", torch.int32), _stream(dev))
+           _vec(status, dim, "status", torch.int32), None if ws is None else ws.data_ptr(), nws, _stream(dev))
 
 
 def fused_nsf_supported(n_lo, n_up, hidden, K):

@@ -158,3 +158,42 @@ def test_fused_ar_no_element_inside_raises(hip_device):
             layer(x)
     finally:
         config.STRICT_CHECKS = prev
+
+
+@pytest.mark.parametrize("dim,K,H,B", [(96, 32, 354, 1.462), (40, 10, 80, 4.0), (24, 32, 100, 3.0)])
+@pytest.mark.parametrize("rows", [1, 40, 50, 333, 4096])
+def test_fused_ar_column_split_bitwise(dim, K, H, B, rows, hip_device):
+    """The forward's column split (small batches: the conditioners spread over
+    workgroups, include/nfk.h nfk_fused_ar_ws) gives bitwise the unsplit
+    launch's z, log|det| (modes 1 and 2) and status words; the applications'
+    batch sizes (40 and 50, applications/input/*.yaml) included."""
+    torch.manual_seed(dim + rows)
+    layer = nff.NSF_AR(dim=dim, K=K, B=B, hidden_dim=H).to(hip_device)
+    x = torch.randn(rows, dim, device=hip_device) * 1.2
+    x[0, dim // 2] = 50.0  # one element outside [-B, B]: the identity tail
+    pack = layer._fused_pack(x.device)
+    assert pack is not None
+    if rows <= 333:
+        assert K_._lib.load().nfk_fused_ar_workspace(dim, H, K, rows, 0) == dim * rows  # split
+    assert K_._lib.load().nfk_fused_ar_workspace(dim, H, K, rows, 1) == 0  # the inverse never splits
+    res = {}
+    for split in (False, True):
+        z = torch.empty_like(x)
+        ld1 = torch.full((rows,), 7.0, device=hip_device)
+        ld2 = torch.linspace(-3.0, 3.0, rows, device=hip_device)
+        st = torch.zeros(dim, dtype=torch.int32, device=hip_device)
+        K_.fused_ar(x, pack, dim, H, K, B, z, logdet=ld1, logdet_mode=1, status=st, split=split)
+        z2 = torch.empty_like(x)
+        K_.fused_ar(x, pack, dim, H, K, B, z2, logdet=ld2, logdet_mode=2, split=split)
+        torch.cuda.synchronize()
+        assert torch.equal(z, z2)
+        res[split] = (z, ld1, ld2, st)
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
+    if rows > 333:
+        return
+    # and the oracle on the split result
+    with torch.no_grad():
+        z_ref, ld_ref = orc.nsf_ar(x.cpu(), _sd(layer), "", dim, K, B)
+    close(res[True][0], z_ref, Z_RTOL, Z_ATOL)
+    close(res[True][1], ld_ref, LD_RTOL, LD_ATOL * max(1.0, dim / 40.0))

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--alg-bytes", type=int, default=None)
     ap.add_argument("--insts", action="store_true")
     ap.add_argument("--traffic", action="store_true")
+    ap.add_argument("--batch-exact", action="store_true",
+                    help="bytes do not scale with the batch (bench.py uses the entry at this batch only)")
     a = ap.parse_args()
     summ = json.load(open(a.summary))
     hits = [k for k in summ if re.search(a.kernel, k)]
@@ -58,6 +60,8 @@ def main():
                "batch": a.batch, "kernel": name, "source": a.source}
         if a.alg_bytes:
             ent["algorithmic_bytes_per_launch"] = a.alg_bytes
+        if a.batch_exact:
+            ent["batch_exact"] = True
         tab[a.key] = ent
         json.dump(tab, open(p, "w"), indent=1)
         print("pmc_traffic.json[%s] <- %s: %d B/launch" % (a.key, name, int(rd + wr)))
