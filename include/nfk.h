@@ -444,6 +444,12 @@ int nfk_trig_features_bwd(const float* x, int64_t ldx, const float* gfeat, int64
  * to it (e.g. the lower columns of a layer's dL/dx, written in place).
  * ------------------------------------------------------------------------- */
 int64_t nfk_fcnn_dh_pack_floats(int32_t P, int32_t H);
+/* [x[:, cols] | 1] for a weight gradient that carries its bias gradient in
+ * the last column (the bias of flows.py:26's first nn.Linear):
+ *   out[b, j] = x[b*ldx + cols[j]] (j < n), out[b, n] = 1, out[b, n+1 .. ldo) = 0
+ * ldo a multiple of 4 and >= n + 1, out 16-byte aligned. */
+int nfk_gather_cols_ones(const float* x, int64_t ldx, const int32_t* cols, int32_t n, int64_t batch,
+                         float* out, int64_t ldo, nfk_stream_t stream);
 int nfk_fcnn_dh_pack(const float* W, int32_t P, int32_t H, float* pack, nfk_stream_t stream);
 int nfk_fcnn_dh(const float* g, int64_t ldg, int32_t P, const float* pack, const float* h, int64_t ldh,
                 int32_t H, float* out, int64_t ldo, int64_t out_col_stride, int32_t accumulate,

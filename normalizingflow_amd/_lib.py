@@ -68,6 +68,7 @@ SIGNATURES = {
         P, I64, P, I32, I32, I32,       # x, ldx, pack, dim, hidden, K
         F64, P, I64, P, I32,            # tail_bound, out, ldo, logdet, logdet_mode
         I64, I32, P, P]),               # batch, inverse, status, stream
+    "nfk_gather_cols_ones": (ctypes.c_int, [P, I64, P, I32, I64, P, I64, P]),
     "nfk_fused_ar_workspace": (ctypes.c_int64, [I32, I32, I32, I64, I32]),
     "nfk_fused_ar_ws": (ctypes.c_int, [
         P, I64, P, I32, I32, I32,       # x, ldx, pack, dim, hidden, K

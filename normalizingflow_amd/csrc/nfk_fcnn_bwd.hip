@@ -243,6 +243,40 @@ __global__ __launch_bounds__(64 * kDhWaves) void k_dh(const float* __restrict__ 
 
 }  // namespace
 
+namespace {
+// out[b, j] = x[b, cols[j]] (j < n), out[b, n] = 1, out[b, n + 1 .. ldo) = 0:
+// one thread per float4 of an output row, the gathers of a wave spread over
+// a few consecutive x rows (their cache lines read once)
+__global__ __launch_bounds__(256) void k_gather_cols1(const float* __restrict__ x, int64_t ldx,
+                                                      const int32_t* __restrict__ cols, int n, int64_t batch,
+                                                      float* __restrict__ out, int64_t ldo) {
+    const int q4 = (int)(ldo >> 2);
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t r = t / q4;
+    if (r >= batch) return;
+    const int j0 = 4 * (int)(t - r * q4);
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = j0 + k;
+        v[k] = j < n ? x[r * ldx + cols[j]] : (j == n ? 1.0f : 0.0f);
+    }
+    *reinterpret_cast<float4*>(out + r * ldo + j0) = make_float4(v[0], v[1], v[2], v[3]);
+}
+}  // namespace
+
+extern "C" int nfk_gather_cols_ones(const float* x, int64_t ldx, const int32_t* cols, int32_t n, int64_t batch,
+                                    float* out, int64_t ldo, nfk_stream_t stream) {
+    if (n < 0 || batch < 0 || ldo < n + 1 || (ldo & 3)) return nfk_set_error("nfk_gather_cols_ones: bad shape");
+    if (batch == 0) return 0;
+    if (!x || !out || (n > 0 && !cols)) return nfk_set_error("nfk_gather_cols_ones: null pointer");
+    if (reinterpret_cast<uintptr_t>(out) & 15) return nfk_set_error("nfk_gather_cols_ones: out must be 16-byte aligned");
+    const int64_t threads = batch * (ldo >> 2);
+    hipLaunchKernelGGL(k_gather_cols1, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                       ldx, cols, n, batch, out, ldo);
+    return launch_status("nfk_gather_cols_ones");
+}
+
 extern "C" int64_t nfk_fcnn_dh_pack_floats(int32_t P, int32_t H) {
     if (P <= 0 || H <= 0 || H > 16 * kDhMaxNT || (P & 3)) return 0;
     const int64_t KB = (P + 31) / 32, NT = (H + 15) / 16;

@@ -336,6 +336,35 @@ __device__ __forceinline__ void dma16(const float* gsrc, uint32_t lds) {
                  : "memory");
 }
 
+// The same from a WAVE-UNIFORM source address: the saddr form (SGPR base +
+// a 32-bit per-lane VGPR offset), so stepping the source costs two SALU adds
+// instead of a 64-bit VALU add per lane and block (NFK_DMA_SADDR=0: dma16)
+#ifndef NFK_DMA_SADDR
+#define NFK_DMA_SADDR 1
+#endif
+__device__ __forceinline__ void dma16u(const float* gbase, uint32_t voff, uint32_t lds) {
+    const uint64_t p = (uint64_t)gbase;
+    // (readfirstlane returns int: each half through uint32_t, or the low half
+    // would sign-extend into the high one)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));
+    const uint64_t ps = ((uint64_t)hi << 32) | (uint64_t)lo;
+    uint32_t saved;  // m0 is reserved by the compiler: restore it
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(ps)
+                 : "memory");
+}
+// one 1-KiB block at uniform address g (lane l copies bytes 16 l .. 16 l + 15)
+__device__ __forceinline__ void dma_blk(const float* g, int lane, uint32_t lds) {
+#if NFK_DMA_SADDR
+    dma16u(g, (uint32_t)lane * 16u, lds);
+#else
+    dma16(g + lane * 4, lds);
+#endif
+}
+
 __device__ __forceinline__ void dma4(const float* gsrc, uint32_t lds) {
     uint32_t saved;  // m0 is reserved by the compiler: restore it
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
@@ -359,7 +388,7 @@ template <int NW = kWaves>
 __device__ __forceinline__ void stage_record(const float* __restrict__ src, int nblk, float4* slot,
                                              int wid, int lane) {
     const uint32_t base = lds_addr(slot);
-    for (int i = wid; i < nblk; i += NW) dma16(src + (int64_t)i * 256 + lane * 4, base + i * 1024);
+    for (int i = wid; i < nblk; i += NW) dma_blk(src + (int64_t)i * 256, lane, base + i * 1024);
 }
 
 // Walk the elements e = lane, lane + 64, ... of a [rows][row] tile as
@@ -789,7 +818,7 @@ __device__ __forceinline__ void stage_tiles(const float* __restrict__ rec, int n
         } else {
             src = KBH * nt * 2 + (T1 ? (nt + 1) / 2 : 0);
         }
-        dma16(rec + (int64_t)src * 256 + lane * 4, base + i * 1024);
+        dma_blk(rec + (int64_t)src * 256, lane, base + i * 1024);
     }
 }
 

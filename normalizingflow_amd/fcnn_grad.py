@@ -110,18 +110,18 @@ def vjp(p, pre, cache, g, need_x, need, gx_into=None):
     x, h1a, h2a = cache
     W1, b1, W2, b2, W3, b3 = linears(p, pre)
     H = W1.shape[0]
-    # the activations come as [B, H] or, from nfk_fused_nsf_vjp, as [h | 1]
-    ones = h1a.shape[1] == H + 1
+    # the activations come as [B, H] or, from nfk_fused_nsf_vjp, as [h | 1];
+    # the input likewise as x or [x | 1] (kernels.gather_cols_ones)
     h1, h2 = h1a[:, :H], h2a[:, :H]
     names = [pre + "network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias")]
     grads = {}
 
-    def put(i, g_out, act_a):
+    def put(i, g_out, act_a, n_in):
         """weight and bias gradient of Linear i: one GEMM against [act | 1] (its
         last column the bias gradient), or a GEMM and a column sum"""
         nw, nb = names[2 * i], names[2 * i + 1]
         if nw in need or nb in need:
-            if ones:
+            if act_a.shape[1] == n_in + 1:
                 wb = wgrad(g_out, act_a)
                 if nw in need:
                     grads[nw] = wb[:, :-1].contiguous()
@@ -133,13 +133,10 @@ def vjp(p, pre, cache, g, need_x, need, gx_into=None):
                 if nb in need:
                     grads[nb] = g_out.sum(0)
 
-    put(2, g, h2a)
+    put(2, g, h2a, H)
     ga2 = dh(g, W3, h2)
-    put(1, ga2, h1a)
+    put(1, ga2, h1a, H)
     ga1 = dh(ga2, W2, h1)
-    if names[0] in need:
-        grads[names[0]] = wgrad(ga1, x)
-    if names[1] in need:
-        grads[names[1]] = ga1.sum(0)
+    put(0, ga1, x, W1.shape[1])
     gx = dh(ga1, W1, None, into=gx_into) if need_x else None
     return gx, grads

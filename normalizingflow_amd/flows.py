@@ -662,13 +662,20 @@ class NSF_CL(_HipFlow):
             want = {n for n, r in zip(names, need[1:]) if r}
             n_lo = len(maps.lists[0])
             if maps.lo_prog is not None:
-                # lower columns as strided views: no gather of x, and dL/dx of
-                # the lower columns added in place by the last input-gradient GEMM
+                # dL/dx of the lower columns added in place (a strided view) by
+                # the last input-gradient GEMM
                 a, st = maps.lo_prog
-                lower = x[:, a::st][:, :n_lo]
                 into = gx[:, a::st][:, :n_lo] if need[0] else None
             else:
-                lower, into = x.index_select(1, maps.lo_in_long), None
+                into = None
+            # the first Linear's weight and bias gradients in one GEMM against
+            # [lower | 1], gathered by one kernel (a strided view of x made the
+            # library GEMM copy it, and the bias gradient was a column sum)
+            l0 = ("psi.network.0.weight", "psi.network.0.bias")
+            if any(n in want for n in l0) or maps.lo_prog is None:
+                lower = K_.gather_cols_ones(x, maps.lo_in)
+            else:
+                lower = x[:, :0]  # (unused: no first-Linear gradient wanted)
             g_lower, grads = fcnn_grad.vjp(pmap, "psi.", (lower, hbuf[0][:, :H + 1], hbuf[1][:, :H + 1]),
                                            gp, need[0], want, gx_into=into)
             if g_lower is not None:
@@ -738,6 +745,7 @@ class NSF_AR(_HipFlow):
         self.reset_parameters()
         self._cols = {}
         self._pack_cache = None
+        self._ar_tree = None  # (module-tree fingerprint, the conditioners' Linear modules)
 
     @property
     def _n_status(self):
@@ -747,20 +755,48 @@ class NSF_AR(_HipFlow):
         """The fused layer kernel's pack (nfk_fused_ar: every conditioner and
         spline of the layer in one launch), rebuilt when any parameter
         changes; None when it does not apply (non-stock conditioners, unequal
-        hidden widths, an unsupported shape)."""
-        if not config.USE_FUSED or self.dim < 2 or not all(_is_stock_fcnn(n) for n in self.layers):
+        hidden widths, an unsupported shape).
+
+        Per call this only fingerprints the module tree (object ids, read from
+        the modules' own dicts) and the parameters (storage, version): at the
+        applications' dim 96 a layer has 95 conditioners and 571 tensors, and
+        walking them through nn.Module attribute access cost more host time
+        than the whole launch at their 40-row batches."""
+        if not config.USE_FUSED or self.dim < 2:
             return None
-        lins = [[n.network[j] for j in (0, 2, 4)] for n in self.layers]
-        hidden = lins[0][0].out_features
-        if any(l[0].out_features != hidden for l in lins) or not K_.fused_ar_supported(self.dim, hidden, self.K):
+        mods = []
+        for n in self.layers._modules.values():
+            net = n.__dict__["_modules"].get("network")
+            mods.append(n)
+            mods.append(net)
+            if net is not None:
+                mods.extend(net.__dict__["_modules"].values())
+        tree = tuple(map(id, mods))
+        lin = self._ar_tree[1] if self._ar_tree is not None and self._ar_tree[0] == tree else None
+        if lin is None:
+            if not all(_is_stock_fcnn(n) for n in self.layers):
+                self._ar_tree = (tree, [])
+                return None
+            lin = [n.network[j] for n in self.layers for j in (0, 2, 4)]
+            self._ar_tree = (tree, lin)
+        if not lin:
             return None
-        params = [self.init_param] + [t for l in lins for m in l for t in (m.weight, m.bias)]
-        if any(p.device != device or p.dtype != torch.float32 for p in params):
+        params = [self.init_param]
+        for m in lin:
+            pp = m.__dict__["_parameters"]
+            params.append(pp.get("weight"))
+            params.append(pp.get("bias"))
+        if any(p is None for p in params):
             return None
-        key = tuple((p.data_ptr(), p._version) for p in params)
+        key = (device, tuple((p.data_ptr(), p._version) for p in params))
         if self._pack_cache is not None and self._pack_cache[0] == key:
             return self._pack_cache[1]
-        ws = [tuple(t for m in l for t in (m.weight, m.bias)) for l in lins]
+        hidden = lin[0].out_features
+        if any(m.out_features != hidden for m in lin[0::3]) or not K_.fused_ar_supported(self.dim, hidden, self.K):
+            return None
+        if any(p.device != device or p.dtype != torch.float32 for p in params):
+            return None
+        ws = [tuple(params[1 + 6 * i:7 + 6 * i]) for i in range(self.dim - 1)]
         pack, keep = K_.fused_ar_pack(ws, self.init_param, self.dim, hidden, self.K)
         self._pack_cache = (key, pack, hidden, keep)
         return pack

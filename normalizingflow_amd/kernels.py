@@ -335,6 +335,18 @@ def fcnn_dh(g, pack, W_shape, h, out, *, accumulate=False):
            cso, 1 if accumulate else 0, B, _stream(dev))
 
 
+def gather_cols_ones(x, cols):
+    """[x[:, cols] | 1] as the first n + 1 columns of a [B, ceil4(n + 1)]
+    buffer (include/nfk.h nfk_gather_cols_ones); returns that [B, n + 1] view."""
+    dev = _require_hip(x, cols)
+    xp, ldx = _mat(x, "x")
+    B, n = x.shape[0], cols.numel()
+    ldo = (n + 4) // 4 * 4
+    out = torch.empty(B, ldo, dtype=F32, device=dev)
+    _lib.call("nfk_gather_cols_ones", xp, ldx, cols.data_ptr(), n, B, out.data_ptr(), ldo, _stream(dev))
+    return out[:, :n + 1]
+
+
 def fcnn_linear(x, pack, W_shape, bias, out, *, tanh=False):
     """out = x @ W + bias (tanh'd when ``tanh``), W [P, H] packed by fcnn_dh_pack
     (an nn.Linear's weight transposed): the FCNN forward on the same kernel."""

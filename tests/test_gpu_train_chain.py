@@ -121,3 +121,16 @@ def test_train_chain_wrong_width_raises_like_per_layer(width, hip_device, monkey
         errs.append((ei.type, str(ei.value)))
     assert errs[0] == errs[1]
     assert "got %d features" % width in errs[0][1]
+
+
+@pytest.mark.parametrize("B,D,cols", [(1, 64, list(range(0, 64, 2))), (1000, 64, list(range(1, 64, 2))),
+                                      (777, 10, [3, 0, 9]), (5, 8, [])])
+def test_gather_cols_ones(B, D, cols, hip_device):
+    """nfk_gather_cols_ones (the first Linear's [lower | 1] for its weight and
+    bias gradients in one GEMM) is exactly [x[:, cols] | 1]."""
+    x = torch.randn(B, D, device=hip_device)
+    c = torch.tensor(cols, dtype=torch.int32, device=hip_device)
+    got = K_.gather_cols_ones(x, c)
+    want = torch.cat([x[:, cols], torch.ones(B, 1, device=hip_device)], 1)
+    assert got.shape == (B, len(cols) + 1)
+    assert torch.equal(got, want)

@@ -20,3 +20,7 @@ for b in 40 4096; do
   python tools/pmc_summary.py gpurun_out/r4s_ar354_$b --json gpurun_out/r4s_ar354_$b/summary.json > gpurun_out/r4s_ar354_$b/summary.txt
 done
 echo done
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4s_train -o train -- python3 tools/bench_train.py --batch 1048576 --steps 3 --warmup 1 --no-torch > gpurun_out/r4s_train.log 2>&1 || { tail -5 gpurun_out/r4s_train.log; exit 1; }
+tail -2 gpurun_out/r4s_train.log
+echo done2
