@@ -338,9 +338,12 @@ __device__ __forceinline__ void dma16(const float* gsrc, uint32_t lds) {
 
 // The same from a WAVE-UNIFORM source address: the saddr form (SGPR base +
 // a 32-bit per-lane VGPR offset), so stepping the source costs two SALU adds
-// instead of a 64-bit VALU add per lane and block (NFK_DMA_SADDR=0: dma16)
+// instead of a 64-bit VALU add per lane and block.  Off by default: measured
+// 3 % SLOWER on the c3 chain (5.57 vs 5.39-5.42 ms per launch, A/B on one box,
+// profiles/r4v_c3_variants.txt) -- the v_readfirstlane of a VGPR-computed
+// base puts a VALU -> SALU dependency in front of every copy
 #ifndef NFK_DMA_SADDR
-#define NFK_DMA_SADDR 1
+#define NFK_DMA_SADDR 0
 #endif
 __device__ __forceinline__ void dma16u(const float* gbase, uint32_t voff, uint32_t lds) {
     const uint64_t p = (uint64_t)gbase;
