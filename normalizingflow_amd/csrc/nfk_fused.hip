@@ -453,21 +453,36 @@ extern "C" int nfk_fused_nsf_vjp_pack(const float* w0, const float* b0, const fl
     return e == hipSuccess ? 0 : (int)e;
 }
 
+// NSF_CL layers whose conditioner is wider than these kernels take (the
+// applications' H = 354, K = 32): nfk_fused_ar.hip's k_fused_cl
+bool nfk_cl_ok(int n_lo, int n_up, int hidden, int K);
+int64_t nfk_cl_pack_floats(int n_lo, int n_up, int hidden, int K);
+int nfk_cl_pack(const float* w0, const float* b0, const float* w2, const float* b2, const float* w4,
+                const float* b4, int n_lo, int n_up, int hidden, int K, float* pack, hipStream_t st);
+int nfk_cl_launch(const float* x, int64_t ldx, const float* pack, const int32_t* up_in, const int32_t* up_out,
+                  int n_up, const int32_t* lo_in, const int32_t* lo_out, int n_lo, int hidden, float* z, int64_t ldz,
+                  float* logdet, int mode, int64_t batch, int K, double tail_bound, bool inv, int32_t* status,
+                  hipStream_t st);
+
 extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
-    return pack_ok(n_lo, n_up, hidden, K) ? 1 : 0;
+    return (pack_ok(n_lo, n_up, hidden, K) || nfk_cl_ok(n_lo, n_up, hidden, K)) ? 1 : 0;
 }
 
 extern "C" int64_t nfk_fused_nsf_pack_elems(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
-    if (!pack_ok(n_lo, n_up, hidden, K)) return 0;
+    if (!pack_ok(n_lo, n_up, hidden, K)) return nfk_cl_pack_floats(n_lo, n_up, hidden, K);
     return pack_floats(n_lo, n_up, hidden, K);
 }
 
 extern "C" int nfk_fused_nsf_pack(const float* w0, const float* b0, const float* w2, const float* b2,
                                   const float* w4, const float* b4, int32_t n_lo, int32_t n_up,
                                   int32_t hidden, int32_t K, float* wpack, nfk_stream_t stream) {
-    if (!pack_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_pack: shape not supported");
     if (!w0 || !b0 || !w2 || !b2 || !w4 || !b4 || !wpack)
         return nfk_set_error("nfk_fused_nsf_pack: null pointer");
+    if (!pack_ok(n_lo, n_up, hidden, K)) {
+        if (nfk_cl_ok(n_lo, n_up, hidden, K))
+            return nfk_cl_pack(w0, b0, w2, b2, w4, b4, n_lo, n_up, hidden, K, wpack, (hipStream_t)stream);
+        return nfk_set_error("nfk_fused_nsf_pack: shape not supported");
+    }
     PackArgs a{w0, b0, w2, b2, w4, b4, wpack, pack_layout(n_lo, n_up, hidden, K)};
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(wpack, 0, 3 * sizeof(float), st);
@@ -558,12 +573,16 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
                              int32_t K, double tail_bound, int32_t inverse, int32_t* status,
                              nfk_stream_t stream) {
     const bool narrow = shape_ok(n_lo, n_up, hidden, K);
-    if (!narrow && !wide_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
+    const bool cl = !narrow && !wide_ok(n_lo, n_up, hidden, K) && nfk_cl_ok(n_lo, n_up, hidden, K);
+    if (!narrow && !cl && !wide_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
     if (batch < 0) return nfk_set_error("nfk_fused_nsf: bad batch");
     if (batch == 0) return 0;
     if (!x || !wpack || !up_in || !up_out || !lo_in || !lo_out || !z)
         return nfk_set_error("nfk_fused_nsf: null pointer");
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf: null logdet");
+    if (cl)
+        return nfk_cl_launch(x, ldx, wpack, up_in, up_out, n_up, lo_in, lo_out, n_lo, hidden, z, ldz, logdet,
+                             logdet_mode, batch, K, tail_bound, inverse != 0, status, (hipStream_t)stream);
     const Layout L = pack_layout(n_lo, n_up, hidden, K);
     FusedArgs a = fused_args(x, ldx, wpack, up_in, up_out, lo_in, lo_out, L, z, ldz, logdet, logdet_mode, batch,
                              K, tail_bound, status);

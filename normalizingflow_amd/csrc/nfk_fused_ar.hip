@@ -352,12 +352,12 @@ struct ArArgs {
 // each ends the sub-record (barrier, next copy) and moves to the next slot.
 template <int NS, int KB, bool T1, int NT, int J, class SlotF, class EndF>
 __device__ __forceinline__ void ar_parts(const h8 (&bh)[KB], const h8 (&bl)[KB], h4 bt, int lane,
-                                         f32x4 (&acc)[NT], SlotF slot, EndF end) {
+                                         f32x4 (&acc)[NT], SlotF slot, EndF end, float bsc = 1.0f) {
     constexpr int T0 = J * NS;
     constexpr int N = (NT - T0) < NS ? (NT - T0) : NS;
-    gemm_h<KB, T1, N, NS, T0, NT, true, T0 + NS >= NT>(bh, bl, bt, slot(), lane, acc);
+    gemm_h<KB, T1, N, NS, T0, NT, true, T0 + NS >= NT>(bh, bl, bt, slot(), lane, acc, bsc);
     end();
-    if constexpr (T0 + NS < NT) ar_parts<NS, KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end);
+    if constexpr (T0 + NS < NT) ar_parts<NS, KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end, bsc);
 }
 
 // The same over a hidden width with a 16-feature tail (tail kind 2): the full
@@ -763,6 +763,334 @@ int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
     return e == hipSuccess ? 0 : (int)e;
 }
 
+// ---------------------------------------------------------------------------
+// NSF_CL with a wide conditioner (nf/flows.py:216-253 at the applications'
+// setup.py:59-62 sizes: hidden 354, nsplines 32), the NSF_AR machinery reused:
+// ONE conditioner FCNN(n_lo, n_up (3K-1), H) per layer, so layers 1 and 2 run
+// once per sample and the output layer streams as n_up records of NO tiles
+// (row j (3K-1) + p = parameter p of upper coordinate j, the reshape of
+// flows.py:231), each followed by its coordinate's spline (G per pass).  The
+// layer-1 B operands are the sample's lower coordinates, scaled per sample by
+// a power of two before the fp16 split (the bias scaled to match, the tanh
+// constant unscaled per lane), as in the other fused NSF kernels.  Both
+// directions share the structure (the upper coordinates do not condition each
+// other); lower columns pass through.  One status word per layer.
+// Pack: the AR header block, layer 1 (NH sub-records over KB1 = ceil(n_lo/32)
+// k-blocks), layer 2 (NH), then n_up x N3 output sub-records, each SB blocks.
+constexpr int kClKB1Max = 4;  // n_lo <= 128
+__host__ __device__ inline ArDims cl_dims(int hidden, int K, int n_lo) { return ar_dims(hidden, K, 16 * ((n_lo + 31) / 32) + 1); }
+__host__ __device__ inline int64_t cl_nsub(const ArDims& d, int n_up) { return 2 * (int64_t)d.NH + (int64_t)n_up * d.N3; }
+__host__ __device__ inline int64_t cl_pack_floats(const ArDims& d, int n_up) { return 256 + cl_nsub(d, n_up) * d.SB * 256; }
+
+// instantiated shapes (KBH, T1, K): the applications' H = 354, K = 32
+#define NFK_CL_SHAPES(X) X(11, 1, 32)
+
+inline bool cl_instance(const ArDims& d, int K) {
+#define NFK_CL_CHK(h, t, k) \
+    if (d.KBH == h && d.T1 == t && K == k) return true;
+    NFK_CL_SHAPES(NFK_CL_CHK)
+#undef NFK_CL_CHK
+    return false;
+}
+
+inline bool cl_ok(int n_lo, int n_up, int hidden, int K) {
+    if (n_lo < 1 || n_lo > 32 * kClKB1Max || n_up < 1 || hidden < 1 || K < 2) return false;
+    const ArDims d = cl_dims(hidden, K, n_lo);
+    if (!cl_instance(d, K)) return false;
+    return ar_lds_bytes(d, 2, false, 4) <= (size_t)kLdsBytes;
+}
+
+struct ClPackArgs {
+    const float *w0, *b0, *w2, *b2, *w4, *b4;  // FCNN: [H][n_lo], [H], [H][H], [H], [n_up P][H], [n_up P]
+    float* out;
+    int n_lo, n_up, H, K, kb1;
+    ArDims d;
+};
+
+__global__ __launch_bounds__(256) void k_cl_max(ClPackArgs a) {
+    const int64_t n1 = (int64_t)a.H * a.n_lo, n2 = (int64_t)a.H * a.H, n3 = (int64_t)a.n_up * a.d.P * a.H;
+    float m1 = 0.0f, m2 = 0.0f, m3 = 0.0f;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n1 + n2 + n3;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        if (g < n1)
+            m1 = fmaxf(m1, fabsf(a.w0[g]));
+        else if (g < n1 + n2)
+            m2 = fmaxf(m2, fabsf(a.w2[g - n1]));
+        else
+            m3 = fmaxf(m3, fabsf(a.w4[g - n1 - n2]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+        m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+        m3 = fmaxf(m3, __shfl_xor(m3, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        unsigned int* h = reinterpret_cast<unsigned int*>(a.out);
+        atomicMax(h, __float_as_uint(m1));
+        atomicMax(h + 1, __float_as_uint(m2));
+        atomicMax(h + 2, __float_as_uint(m3));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cl_pack(ClPackArgs a) {
+    const ArDims& d = a.d;
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+    const unsigned int* hdr = reinterpret_cast<const unsigned int*>(a.out);
+    const int s1 = ar_scale_exp(__uint_as_float(hdr[0])), s2 = ar_scale_exp(__uint_as_float(hdr[1])),
+              s3 = ar_scale_exp(__uint_as_float(hdr[2]));
+    const int64_t total = cl_pack_floats(d, a.n_up);
+    const int H = a.H, kbh = d.KBH, P = d.P, n_lo = a.n_lo;
+    auto hid = [&](int t, int r) { return (d.T1 == 2 && t == 2 * kbh) ? 32 * kbh + r : hid_feature(t, r, kbh); };
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        if (g < 256) {
+            if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -(s1 + 14)));
+            else if (g == 4) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
+            else if (g == 5) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
+            else if (g >= 6) out[g] = 0u;
+            continue;
+        }
+        const int64_t w = g - 256;
+        const int64_t s = w / ((int64_t)d.SB * 256);
+        const int blk = (int)((w >> 8) - s * d.SB), wl = (int)(w & 255);
+        uint32_t v;
+        if (s < d.NH) {  // layer 1: Linear(n_lo, H) on the lower coordinates in lo_in order
+            v = ar_sub_word(
+                d.NS, blk, wl, a.kb1, 0, d.HT, d.NS * (int)s, ldexpf(1.0f, s1), ldexpf(1.0f, s1 + 14),
+                [&](int t, int r, int k) -> float {
+                    const int f = hid(t, r);
+                    return (f < H && k < n_lo) ? a.w0[(int64_t)f * n_lo + k] : 0.0f;
+                },
+                [&](int t, int r) -> float {
+                    const int f = hid(t, r);
+                    return f < H ? a.b0[f] : 0.0f;
+                });
+        } else if (s < 2 * d.NH) {  // layer 2: Linear(H, H)
+            v = ar_sub_word(
+                d.NS, blk, wl, kbh, d.T1, d.HT, d.NS * (int)(s - d.NH), ldexpf(1.0f, s2), ldexpf(1.0f, s2 + 14),
+                [&](int t, int r, int k) -> float {
+                    const int f = hid(t, r);
+                    return (f < H && k < H) ? a.w2[(int64_t)f * H + k] : 0.0f;
+                },
+                [&](int t, int r) -> float {
+                    const int f = hid(t, r);
+                    return f < H ? a.b2[f] : 0.0f;
+                });
+        } else {  // output layer, coordinate j: rows j P + p of Linear(H, n_up P)
+            const int64_t u = s - 2 * d.NH;
+            const int j = (int)(u / d.N3), part = (int)(u - (int64_t)j * d.N3);
+            const int64_t r0 = (int64_t)j * P;
+            v = ar_sub_word(
+                d.NS, blk, wl, kbh, d.T1, d.NO, d.NS * part, ldexpf(1.0f, s3), ldexpf(1.0f, s3 + 14),
+                [&](int t, int r, int k) -> float {
+                    const int p = 16 * t + r;
+                    return (p < P && k < H) ? a.w4[(r0 + p) * H + k] : 0.0f;
+                },
+                [&](int t, int r) -> float {
+                    const int p = 16 * t + r;
+                    return p < P ? a.b4[r0 + p] : 0.0f;
+                });
+        }
+        out[g] = v;
+    }
+}
+
+struct ClArgs {
+    const float* x;
+    const float* pack;
+    float* z;
+    float* logdet;
+    int32_t* status;  // one word or null
+    const int32_t *up_in, *up_out, *lo_in, *lo_out;
+    int64_t ldx, ldz, batch;
+    int32_t n_lo, n_up, mode, sb, kb1;
+    int64_t nsr;
+    NfkSplineConst c;
+};
+
+template <int KBH, int TK, int K, bool INV>
+__global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
+    static_assert(TK != 2, "16-feature tails: not instanced for NSF_CL");
+    constexpr int NW = 4;
+    constexpr bool T1 = TK == 1;
+    constexpr int HT = 2 * KBH + (TK ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
+    constexpr int NS = ar_ns_for(KBH);
+    constexpr int NH = (HT + NS - 1) / NS;
+    constexpr int NTG = TK == 1 ? (NS + 1) / 2 : 0;
+    constexpr int PS = 16 * NO + 4, G = ar_group(false, PS);  // the upper coordinates are independent
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4, sl = lane & 15;
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    float4* const slot0 = lds4;
+    float4* const slot1 = lds4 + a.sb * 64;
+    float* const scr = reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + wid * (G * 16 * PS);
+    int* const cst = reinterpret_cast<int*>(reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + NW * G * 16 * PS);
+    const int64_t b0 = ((int64_t)blockIdx.x * NW + wid) * 16;
+    const bool row_ok = b0 + sl < a.batch;
+    const int64_t brow = row_ok ? b0 + sl : a.batch - 1;
+
+    int64_t st_s = 0;
+    auto stage_next = [&]() {
+        if (st_s >= a.nsr) return;
+        const int nblk = st_s < NH ? a.kb1 * NS * 2 + 1 : KBH * NS * 2 + NTG + 1;
+        stage_record<NW>(a.pack + 256 + st_s * a.sb * 256, nblk, (st_s & 1) ? slot1 : slot0, wid, lane);
+        ++st_s;
+    };
+
+    // ---- prologue: the status word, the lower coordinates (pass-through and
+    // the layer-1 operands, scaled per sample), the first two sub-records
+    if (threadIdx.x == 0) cst[0] = 0;
+    const float un1 = a.pack[3], un2 = a.pack[4], un3 = a.pack[5];
+    h8 xh[kClKB1Max], xl[kClKB1Max];
+    float c21, bsc1;
+    {
+        float v[kClKB1Max][8];
+        float mx = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < kClKB1Max; ++kb)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 32 * kb + 8 * q + j;
+                const bool ok = kb < a.kb1 && k < a.n_lo;
+                const float xv = ok ? a.x[brow * a.ldx + a.lo_in[ok ? k : 0]] : 0.0f;
+                v[kb][j] = xv;
+                mx = fmaxf(mx, fabsf(xv));
+                if (ok && row_ok) a.z[(b0 + sl) * a.ldz + a.lo_out[k]] = xv;  // flows.py:229-230
+            }
+        // per sample: the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 hold one sample
+        for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        int ex = 0;
+        if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
+        ex = ex < -64 ? -64 : ex;  // (a tiny sample: its bias scale stays finite)
+        const float sx = ldexpf(1.0f, 14 - ex);
+        bsc1 = ldexpf(1.0f, -ex);
+        c21 = -2.0f * kL2E * un1 * ldexpf(1.0f, ex);
+#pragma unroll
+        for (int kb = 0; kb < kClKB1Max; ++kb)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float t = v[kb][j] * sx;
+                const _Float16 hh = (_Float16)t;
+                xh[kb][j] = hh;
+                xl[kb][j] = (_Float16)(t - (float)hh);
+            }
+    }
+    stage_next();
+    stage_next();
+    dma_barrier();
+
+    int64_t s = 0;
+    auto slot = [&]() -> const float4* { return (s & 1) ? slot1 : slot0; };
+    auto end = [&]() {
+        gemm_fence();
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stage_next();
+        ++s;
+    };
+    const float c22 = -2.0f * kL2E * un2;
+    h8 bh[KBH], bl[KBH];
+    h4 btail = h4{0, 0, 0, 0};
+    {
+        f32x4 h[HT];
+        auto layer1 = [&](auto kbc) {
+            constexpr int KB = decltype(kbc)::value;
+            h8 mh[KB], ml[KB];
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) mh[kb] = xh[kb], ml[kb] = xl[kb];
+            ar_parts<NS, KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end, bsc1);
+        };
+        switch (a.kb1) {
+            case 1: layer1(std::integral_constant<int, 1>{}); break;
+            case 2: layer1(std::integral_constant<int, 2>{}); break;
+            case 3: layer1(std::integral_constant<int, 3>{}); break;
+            default: layer1(std::integral_constant<int, 4>{}); break;
+        }
+        act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
+    }
+    {
+        f32x4 h2[HT];
+        ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+        act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
+    }
+
+    // ---- the upper coordinates: output record j, then the spline pass of
+    // coordinates j - c .. j (lane group q takes coordinate j - c + q)
+    float ld_acc = 0.0f, xin = 0.0f;
+    bool any_in = false, any_nd = false;
+    for (int j = 0; j < a.n_up; ++j) {
+        const int c = j % G;
+        if (c == 0) {
+            const int col = j + (q < G ? q : 0);
+            xin = col < a.n_up ? a.x[brow * a.ldx + a.up_in[col]] : 0.0f;
+        }
+        float* const slab = scr + c * 16 * PS;
+        {
+            f32x4 o[NO];
+            ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+#pragma unroll
+            for (int t = 0; t < NO; ++t) {
+                const int p = 16 * t + 4 * q;
+                if (p < PS - 3)
+                    *reinterpret_cast<float4*>(slab + sl * PS + p) =
+                        make_float4(o[t][0] * un3, o[t][1] * un3, o[t][2] * un3, o[t][3] * un3);
+            }
+        }
+        if (!(c == G - 1 || j == a.n_up - 1)) continue;
+        const int cl = q < G ? q : 0;
+        const int col = j - c + q;
+        const bool act = q <= c;
+        float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
+        {
+            const float* row = scr + cl * 16 * PS + sl * PS;
+#pragma unroll
+            for (int p = 0; p < K; ++p) wr[p] = row[p];
+#pragma unroll
+            for (int p = 0; p < K; ++p) hr[p] = row[K + p];
+#pragma unroll
+            for (int p = 0; p < K - 1; ++p) dr[p] = row[2 * K + p];
+        }
+        float out, lad;
+        bool inside, nd;
+        nfk_rqs_element_lean<K, INV>(xin, wr, hr, dr, a.c, out, lad, inside, nd);
+        const bool live = act && row_ok;
+        if (live) a.z[(b0 + sl) * a.ldz + a.up_out[col]] = out;
+        const float lm = act ? lad : 0.0f;
+#pragma unroll
+        for (int g = 0; g < G; ++g) ld_acc = ld_acc + __shfl(lm, sl + 16 * g, 64);
+        any_in |= live && inside;
+        any_nd |= live && inside && nd;
+    }
+
+    // ---- log|det| of the layer (flows.py:238, 252), the status word
+    if (q == 0 && row_ok && a.mode != 0) {
+        float* ld = a.logdet + b0 + sl;
+        *ld = a.mode == 2 ? *ld + ld_acc : ld_acc;
+    }
+    const int bits = (__any(any_in) ? NFK_ST_INSIDE_SEEN : 0) | (__any(any_nd) ? NFK_ST_NEG_DISC : 0);
+    if (lane == 0 && bits != 0) atomicOr(cst, bits);
+    __syncthreads();
+    if (a.status != nullptr && threadIdx.x == 0) {
+        const int b = cst[0];
+        if (b != 0 && (a.status[0] & b) != b) atomicOr(a.status, b);
+    }
+}
+
+template <int KBH, int T1, int K>
+int launch_cl(const ClArgs& a, const ArDims& d, bool inv, hipStream_t st) {
+    const size_t lds = ar_lds_bytes(d, 2, false, 4);
+    const dim3 g((unsigned)((a.batch + 63) / 64)), b(256);
+    if (inv)
+        hipLaunchKernelGGL((k_fused_cl<KBH, T1, K, true>), g, b, lds, st, a);
+    else
+        hipLaunchKernelGGL((k_fused_cl<KBH, T1, K, false>), g, b, lds, st, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
 }  // namespace
 
 extern "C" int nfk_fused_ar_supported(int32_t dim, int32_t hidden, int32_t K) { return ar_ok(dim, hidden, K) ? 1 : 0; }
@@ -845,4 +1173,60 @@ extern "C" int nfk_fused_ar_ws(const float* x, int64_t ldx, const float* pack, i
     NFK_AR_SHAPES(NFK_AR_LAUNCH)
 #undef NFK_AR_LAUNCH
     return nfk_set_error("nfk_fused_ar: no kernel instance");
+}
+
+// NSF_CL layers with a wide conditioner, reached through nfk_fused_nsf_* (nfk_fused.hip)
+bool nfk_cl_ok(int n_lo, int n_up, int hidden, int K) { return cl_ok(n_lo, n_up, hidden, K); }
+
+int64_t nfk_cl_pack_floats(int n_lo, int n_up, int hidden, int K) {
+    return cl_ok(n_lo, n_up, hidden, K) ? cl_pack_floats(cl_dims(hidden, K, n_lo), n_up) : 0;
+}
+
+int nfk_cl_pack(const float* w0, const float* b0, const float* w2, const float* b2, const float* w4,
+                const float* b4, int n_lo, int n_up, int hidden, int K, float* pack, hipStream_t st) {
+    if (!cl_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf_pack: shape not supported");
+    const ArDims d = cl_dims(hidden, K, n_lo);
+    ClPackArgs a{w0, b0, w2, b2, w4, b4, pack, n_lo, n_up, hidden, K, (n_lo + 31) / 32, d};
+    hipError_t e = hipMemsetAsync(pack, 0, 3 * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_cl_max, dim3(256), dim3(256), 0, st, a);
+    int64_t g = (cl_pack_floats(d, n_up) + 255) / 256;
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL(k_cl_pack, dim3((unsigned)g), dim3(256), 0, st, a);
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int nfk_cl_launch(const float* x, int64_t ldx, const float* pack, const int32_t* up_in, const int32_t* up_out,
+                  int n_up, const int32_t* lo_in, const int32_t* lo_out, int n_lo, int hidden, float* z, int64_t ldz,
+                  float* logdet, int mode, int64_t batch, int K, double tail_bound, bool inv, int32_t* status,
+                  hipStream_t st) {
+    if (!cl_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
+    const ArDims d = cl_dims(hidden, K, n_lo);
+    ClArgs a;
+    a.x = x;
+    a.pack = pack;
+    a.z = z;
+    a.logdet = logdet;
+    a.status = status;
+    a.up_in = up_in;
+    a.up_out = up_out;
+    a.lo_in = lo_in;
+    a.lo_out = lo_out;
+    a.ldx = ldx;
+    a.ldz = ldz;
+    a.batch = batch;
+    a.n_lo = n_lo;
+    a.n_up = n_up;
+    a.mode = mode;
+    a.sb = d.SB;
+    a.kb1 = (n_lo + 31) / 32;
+    a.nsr = cl_nsub(d, n_up);
+    // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:236-237)
+    a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+#define NFK_CL_LAUNCH(h, t, k) \
+    if (d.KBH == h && d.T1 == t && K == k) return launch_cl<h, t, k>(a, d, inv, st);
+    NFK_CL_SHAPES(NFK_CL_LAUNCH)
+#undef NFK_CL_LAUNCH
+    return nfk_set_error("nfk_fused_nsf: no kernel instance");
 }

@@ -498,7 +498,7 @@ __device__ __forceinline__ void mfma_result_wait() {
 // sub-record): wait them out here (see kMfmaResultWait).
 template <int KBH, bool T1, int NT, int NS = NT, int T0 = 0, int NA = NT, bool BREL = false, bool WAIT = false>
 __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH], h4 btail,
-                                       const float4* slot, int lane, f32x4 (&acc)[NA]) {
+                                       const float4* slot, int lane, f32x4 (&acc)[NA], float bsc = 1.0f) {
     constexpr int NPR = (NT + 1) / 2;  // tile pairs (the last may be a single tile)
     constexpr int N = KBH * NPR;       // k-block steps; T1: then NPR tail steps
     constexpr int NI = N + (T1 ? NPR : 0);
@@ -507,7 +507,7 @@ __device__ __forceinline__ void gemm_h(const h8 (&bh)[KBH], const h8 (&bl)[KBH],
     const float4* tail = slot + KBH * NS * 2 * 64;
     const float4* bias = tail + NTG * 64;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[T0 + t] = as_f32x4(bias[((BREL ? 0 : T0) + t) * 4 + q]);
+    for (int t = 0; t < NT; ++t) acc[T0 + t] = as_f32x4(bias[((BREL ? 0 : T0) + t) * 4 + q]) * bsc;
 #ifdef NFK_DIAG_BIAS_NOP  // diagnostic: a wait between the bias initialisation and the first MFMA
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");

@@ -441,3 +441,30 @@ def test_c3_full_batch_properties(hip_device):
         xr, ld_i = pre.inverse(z)
     assert float((xr - xd).abs().max()) < 1e-3
     assert float((ld_f + ld_i).abs().max()) < 1e-3
+
+
+def test_applications_nsf_cl_branch_vs_oracle(hip_device):
+    """The applications' NSF_CL branch (applications/src/setup.py:59-62) at the
+    Einstein / LJ / Fe configs' sizes: 32 particles x 3 dims, nsplines 32,
+    hidden 354, B = (32 / (8 * 1.28))^(1/3), the six-mask cycle [0], [1], [2],
+    [0, 1], [1, 2], [0, 2]: a 6-layer model's log_prob vs the oracle, and the
+    sample round trip.  (K = 32 / H = 354 run the per-layer library-GEMM +
+    nfk_rqs_coupling path: no fused instance for that shape.)"""
+    torch.manual_seed(21)
+    B = (32 / (8 * 1.28)) ** (1.0 / 3.0)
+    masks = [[0], [1], [2], [0, 1], [1, 2], [0, 2]]
+    flows = [nff.NSF_CL(size=32, dim=3, K=32, B=B, hidden_dim=354, mask=m) for m in masks]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(96), torch.eye(96))
+    model = nfm.NormalizingFlowModel(prior, flows)
+    sd = cpu_sd(model)
+    specs = [dict(type="NSF_CL", prefix="flows.%d." % i, size=32, dim=3, K=32, B=B, mask=m)
+             for i, m in enumerate(masks)]
+    x = torch.randn(300, 96, generator=torch.Generator().manual_seed(4)) * 0.6
+    ref = orc.model_log_prob(specs, sd, x)
+    model = model.to(hip_device)
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(96, device=hip_device),
+                                                        torch.eye(96, device=hip_device))
+    lp = model.log_prob(x.to(hip_device))
+    close(lp, ref, 1e-5, 2e-4)
+    xs, lpx, zs = model.sample(500)
+    close(lpx, model.log_prob(xs), 1e-5, 2e-3)
