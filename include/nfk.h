@@ -251,6 +251,19 @@ int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t
                   const int32_t* lo_out, int32_t n_lo, int32_t hidden, float* z, int64_t ldz,
                   float* logdet, int32_t logdet_mode, int64_t batch, int32_t K,
                   double tail_bound, int32_t inverse, int32_t* status, nfk_stream_t stream);
+/* The same with a workspace of nfk_fused_nsf_workspace() floats: layers with a
+ * conditioner wider than the instanced NSF_CL kernels (the applications'
+ * H = 354, K = 32, setup.py:59-62) split their upper coordinates over
+ * workgroups when the batch alone cannot fill the GPU, the per-coordinate
+ * log|det| terms going through the workspace (summed in coordinate order:
+ * bitwise the unsplit result).  0 floats = no split for this call. */
+int64_t nfk_fused_nsf_workspace(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K, int64_t batch,
+                                int32_t inverse);
+int nfk_fused_nsf_ws(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
+                     const int32_t* up_out, int32_t n_up, const int32_t* lo_in, const int32_t* lo_out,
+                     int32_t n_lo, int32_t hidden, float* z, int64_t ldz, float* logdet,
+                     int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound, int32_t inverse,
+                     int32_t* status, float* workspace, int64_t workspace_floats, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Chain of fused NSF coupling layers in one launch: the layer loop of

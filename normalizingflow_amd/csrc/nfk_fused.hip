@@ -462,7 +462,8 @@ int nfk_cl_pack(const float* w0, const float* b0, const float* w2, const float* 
 int nfk_cl_launch(const float* x, int64_t ldx, const float* pack, const int32_t* up_in, const int32_t* up_out,
                   int n_up, const int32_t* lo_in, const int32_t* lo_out, int n_lo, int hidden, float* z, int64_t ldz,
                   float* logdet, int mode, int64_t batch, int K, double tail_bound, bool inv, int32_t* status,
-                  hipStream_t st);
+                  float* workspace, int64_t workspace_floats, hipStream_t st);
+int64_t nfk_cl_workspace(int n_lo, int n_up, int hidden, int K, int64_t batch);
 
 extern "C" int nfk_fused_nsf_supported(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K) {
     return (pack_ok(n_lo, n_up, hidden, K) || nfk_cl_ok(n_lo, n_up, hidden, K)) ? 1 : 0;
@@ -566,12 +567,34 @@ FusedArgs fused_args(const float* x, int64_t ldx, const float* wpack, const int3
 }
 }  // namespace
 
+extern "C" int64_t nfk_fused_nsf_workspace(int32_t n_lo, int32_t n_up, int32_t hidden, int32_t K, int64_t batch,
+                                           int32_t inverse) {
+    (void)inverse;
+    if (shape_ok(n_lo, n_up, hidden, K) || wide_ok(n_lo, n_up, hidden, K)) return 0;
+    return nfk_cl_workspace(n_lo, n_up, hidden, K, batch);
+}
+
+extern "C" int nfk_fused_nsf_ws(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
+                                const int32_t* up_out, int32_t n_up, const int32_t* lo_in, const int32_t* lo_out,
+                                int32_t n_lo, int32_t hidden, float* z, int64_t ldz, float* logdet,
+                                int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound, int32_t inverse,
+                                int32_t* status, float* workspace, int64_t workspace_floats, nfk_stream_t stream);
+
 extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
                              const int32_t* up_out, int32_t n_up, const int32_t* lo_in,
                              const int32_t* lo_out, int32_t n_lo, int32_t hidden, float* z,
                              int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
                              int32_t K, double tail_bound, int32_t inverse, int32_t* status,
                              nfk_stream_t stream) {
+    return nfk_fused_nsf_ws(x, ldx, wpack, up_in, up_out, n_up, lo_in, lo_out, n_lo, hidden, z, ldz, logdet,
+                            logdet_mode, batch, K, tail_bound, inverse, status, nullptr, 0, stream);
+}
+
+extern "C" int nfk_fused_nsf_ws(const float* x, int64_t ldx, const float* wpack, const int32_t* up_in,
+                                const int32_t* up_out, int32_t n_up, const int32_t* lo_in, const int32_t* lo_out,
+                                int32_t n_lo, int32_t hidden, float* z, int64_t ldz, float* logdet,
+                                int32_t logdet_mode, int64_t batch, int32_t K, double tail_bound, int32_t inverse,
+                                int32_t* status, float* workspace, int64_t workspace_floats, nfk_stream_t stream) {
     const bool narrow = shape_ok(n_lo, n_up, hidden, K);
     const bool cl = !narrow && !wide_ok(n_lo, n_up, hidden, K) && nfk_cl_ok(n_lo, n_up, hidden, K);
     if (!narrow && !cl && !wide_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
@@ -582,7 +605,8 @@ extern "C" int nfk_fused_nsf(const float* x, int64_t ldx, const float* wpack, co
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_nsf: null logdet");
     if (cl)
         return nfk_cl_launch(x, ldx, wpack, up_in, up_out, n_up, lo_in, lo_out, n_lo, hidden, z, ldz, logdet,
-                             logdet_mode, batch, K, tail_bound, inverse != 0, status, (hipStream_t)stream);
+                             logdet_mode, batch, K, tail_bound, inverse != 0, status, workspace, workspace_floats,
+                             (hipStream_t)stream);
     const Layout L = pack_layout(n_lo, n_up, hidden, K);
     FusedArgs a = fused_args(x, ldx, wpack, up_in, up_out, lo_in, lo_out, L, z, ldz, logdet, logdet_mode, batch,
                              K, tail_bound, status);

@@ -905,7 +905,9 @@ struct ClArgs {
     const int32_t *up_in, *up_out, *lo_in, *lo_out;
     int64_t ldx, ldz, batch;
     int32_t n_lo, n_up, mode, sb, kb1;
-    int64_t nsr;
+    int32_t csplit;   // upper-coordinate ranges (1: all per workgroup)
+    int64_t rblocks;  // row blocks of the batch
+    float* ld_cols;   // csplit > 1: per-coordinate log|det| terms [n_up][batch] (k_ar_ld_sum)
     NfkSplineConst c;
 };
 
@@ -916,7 +918,7 @@ __global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
     constexpr bool T1 = TK == 1;
     constexpr int HT = 2 * KBH + (TK ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
     constexpr int NS = ar_ns_for(KBH);
-    constexpr int NH = (HT + NS - 1) / NS;
+    constexpr int NH = (HT + NS - 1) / NS, N3 = (NO + NS - 1) / NS;
     constexpr int NTG = TK == 1 ? (NS + 1) / 2 : 0;
     constexpr int PS = 16 * NO + 4, G = ar_group(false, PS);  // the upper coordinates are independent
     const int lane = threadIdx.x & 63;
@@ -927,15 +929,30 @@ __global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
     float4* const slot1 = lds4 + a.sb * 64;
     float* const scr = reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + wid * (G * 16 * PS);
     int* const cst = reinterpret_cast<int*>(reinterpret_cast<float*>(lds4 + 2 * a.sb * 64) + NW * G * 16 * PS);
-    const int64_t b0 = ((int64_t)blockIdx.x * NW + wid) * 16;
+    // upper-coordinate range of this workgroup (a small batch splits them over
+    // workgroups; XCD-affine virtual ids as in k_fused_ar)
+    int sp = 0;
+    int64_t rbk = blockIdx.x;
+    if (a.csplit > 1) {
+        const int64_t v = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+        if (v >= a.rblocks * a.csplit) return;  // padding workgroup (uniform: before any barrier)
+        sp = (int)(v / a.rblocks);
+        rbk = v - (int64_t)sp * a.rblocks;
+    }
+    const int j_lo = (int)(((int64_t)sp * a.n_up) / a.csplit), j_hi = (int)(((int64_t)(sp + 1) * a.n_up) / a.csplit);
+    const int64_t b0 = (rbk * NW + wid) * 16;
     const bool row_ok = b0 + sl < a.batch;
     const int64_t brow = row_ok ? b0 + sl : a.batch - 1;
 
+    // the stream: layers 1 and 2 (2 NH sub-records), then the output records
+    // of coordinates j_lo .. j_hi - 1; st_s counts sub-records in stream order
+    const int64_t nsr = 2 * NH + (int64_t)(j_hi - j_lo) * N3;
     int64_t st_s = 0;
     auto stage_next = [&]() {
-        if (st_s >= a.nsr) return;
-        const int nblk = st_s < NH ? a.kb1 * NS * 2 + 1 : KBH * NS * 2 + NTG + 1;
-        stage_record<NW>(a.pack + 256 + st_s * a.sb * 256, nblk, (st_s & 1) ? slot1 : slot0, wid, lane);
+        if (st_s >= nsr) return;
+        const int64_t ps = st_s < 2 * NH ? st_s : st_s + (int64_t)j_lo * N3;
+        const int nblk = ps < NH ? a.kb1 * NS * 2 + 1 : KBH * NS * 2 + NTG + 1;
+        stage_record<NW>(a.pack + 256 + ps * a.sb * 256, nblk, (st_s & 1) ? slot1 : slot0, wid, lane);
         ++st_s;
     };
 
@@ -957,7 +974,7 @@ __global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
                 const float xv = ok ? a.x[brow * a.ldx + a.lo_in[ok ? k : 0]] : 0.0f;
                 v[kb][j] = xv;
                 mx = fmaxf(mx, fabsf(xv));
-                if (ok && row_ok) a.z[(b0 + sl) * a.ldz + a.lo_out[k]] = xv;  // flows.py:229-230
+                if (ok && row_ok && sp == 0) a.z[(b0 + sl) * a.ldz + a.lo_out[k]] = xv;  // flows.py:229-230
             }
         // per sample: the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 hold one sample
         for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
@@ -1021,8 +1038,8 @@ __global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
     // coordinates j - c .. j (lane group q takes coordinate j - c + q)
     float ld_acc = 0.0f, xin = 0.0f;
     bool any_in = false, any_nd = false;
-    for (int j = 0; j < a.n_up; ++j) {
-        const int c = j % G;
+    for (int j = j_lo; j < j_hi; ++j) {
+        const int c = (j - j_lo) % G;
         if (c == 0) {
             const int col = j + (q < G ? q : 0);
             xin = col < a.n_up ? a.x[brow * a.ldx + a.up_in[col]] : 0.0f;
@@ -1039,7 +1056,7 @@ __global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
                         make_float4(o[t][0] * un3, o[t][1] * un3, o[t][2] * un3, o[t][3] * un3);
             }
         }
-        if (!(c == G - 1 || j == a.n_up - 1)) continue;
+        if (!(c == G - 1 || j == j_hi - 1)) continue;
         const int cl = q < G ? q : 0;
         const int col = j - c + q;
         const bool act = q <= c;
@@ -1059,14 +1076,20 @@ __global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
         const bool live = act && row_ok;
         if (live) a.z[(b0 + sl) * a.ldz + a.up_out[col]] = out;
         const float lm = act ? lad : 0.0f;
+        if (a.ld_cols != nullptr) {
+            // split coordinates: each term to its coordinate's row, summed in
+            // coordinate order by k_ar_ld_sum (the additions of ld_acc below)
+            if (live) a.ld_cols[(int64_t)col * a.batch + b0 + sl] = lad;
+        } else {
 #pragma unroll
-        for (int g = 0; g < G; ++g) ld_acc = ld_acc + __shfl(lm, sl + 16 * g, 64);
+            for (int g = 0; g < G; ++g) ld_acc = ld_acc + __shfl(lm, sl + 16 * g, 64);
+        }
         any_in |= live && inside;
         any_nd |= live && inside && nd;
     }
 
     // ---- log|det| of the layer (flows.py:238, 252), the status word
-    if (q == 0 && row_ok && a.mode != 0) {
+    if (q == 0 && row_ok && a.mode != 0 && a.ld_cols == nullptr) {
         float* ld = a.logdet + b0 + sl;
         *ld = a.mode == 2 ? *ld + ld_acc : ld_acc;
     }
@@ -1079,14 +1102,34 @@ __global__ __launch_bounds__(256, 1) void k_fused_cl(ClArgs a) {
     }
 }
 
+// upper-coordinate ranges of a launch: enough workgroups for every CU (one
+// 4-wave workgroup per CU), at most one range per coordinate
+inline int cl_csplit(int n_up, int64_t batch) {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    if (batch <= 0) return 1;
+    const int64_t rb = (batch + 63) / 64;
+    if (rb >= cus) return 1;
+    const int64_t cs = (cus + rb - 1) / rb;
+    return (int)(cs < n_up ? cs : n_up);
+}
+
 template <int KBH, int T1, int K>
 int launch_cl(const ClArgs& a, const ArDims& d, bool inv, hipStream_t st) {
     const size_t lds = ar_lds_bytes(d, 2, false, 4);
-    const dim3 g((unsigned)((a.batch + 63) / 64)), b(256);
+    const int64_t nblk = a.csplit > 1 ? (a.rblocks * a.csplit + 7) / 8 * 8 : a.rblocks;
+    const dim3 g((unsigned)nblk), b(256);
     if (inv)
         hipLaunchKernelGGL((k_fused_cl<KBH, T1, K, true>), g, b, lds, st, a);
     else
         hipLaunchKernelGGL((k_fused_cl<KBH, T1, K, false>), g, b, lds, st, a);
+    if (a.csplit > 1 && a.mode != 0)
+        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, a.ld_cols,
+                           a.logdet, a.batch, a.n_up, a.mode);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -1197,10 +1240,15 @@ int nfk_cl_pack(const float* w0, const float* b0, const float* w2, const float* 
     return e == hipSuccess ? 0 : (int)e;
 }
 
+int64_t nfk_cl_workspace(int n_lo, int n_up, int hidden, int K, int64_t batch) {
+    if (!cl_ok(n_lo, n_up, hidden, K) || batch <= 0) return 0;
+    return cl_csplit(n_up, batch) > 1 ? (int64_t)n_up * batch : 0;
+}
+
 int nfk_cl_launch(const float* x, int64_t ldx, const float* pack, const int32_t* up_in, const int32_t* up_out,
                   int n_up, const int32_t* lo_in, const int32_t* lo_out, int n_lo, int hidden, float* z, int64_t ldz,
                   float* logdet, int mode, int64_t batch, int K, double tail_bound, bool inv, int32_t* status,
-                  hipStream_t st) {
+                  float* workspace, int64_t workspace_floats, hipStream_t st) {
     if (!cl_ok(n_lo, n_up, hidden, K)) return nfk_set_error("nfk_fused_nsf: shape not supported");
     const ArDims d = cl_dims(hidden, K, n_lo);
     ClArgs a;
@@ -1221,7 +1269,10 @@ int nfk_cl_launch(const float* x, int64_t ldx, const float* pack, const int32_t*
     a.mode = mode;
     a.sb = d.SB;
     a.kb1 = (n_lo + 31) / 32;
-    a.nsr = cl_nsub(d, n_up);
+    a.csplit = cl_csplit(n_up, batch);
+    if (a.csplit > 1 && (workspace == nullptr || workspace_floats < (int64_t)n_up * batch)) a.csplit = 1;
+    a.ld_cols = a.csplit > 1 ? workspace : nullptr;
+    a.rblocks = (batch + 63) / 64;
     // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:236-237)
     a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
 #define NFK_CL_LAUNCH(h, t, k) \

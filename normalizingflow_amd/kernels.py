@@ -537,10 +537,17 @@ def fused_nsf(x, wpack, up_in, up_out, lo_in, lo_out, hidden, z, *, logdet, logd
     B = x.shape[0]
     xp, ldx = _mat(x, "x")
     zp, ldz = _mat(z, "z")
-    _timed("nfk_fused_nsf", dev, "nfk_fused_nsf", xp, ldx, wpack.data_ptr(), up_in.data_ptr(), up_out.data_ptr(),
-              up_in.numel(), lo_in.data_ptr(), lo_out.data_ptr(), lo_in.numel(), hidden, zp, ldz,
-              _vec(logdet, B, "logdet"), logdet_mode, B, K, float(tail_bound),
-              1 if inverse else 0, _vec(status, 1, "status", torch.int32), _stream(dev))
+    # wide conditioners (k_fused_cl) on a small batch split their upper
+    # coordinates over workgroups; the per-coordinate log|det| terms go through
+    # a workspace (0 floats for every other shape)
+    nws = int(_lib.load().nfk_fused_nsf_workspace(lo_in.numel(), up_in.numel(), hidden, K, B,
+                                                  1 if inverse else 0))
+    ws = torch.empty(nws, dtype=F32, device=dev) if nws > 0 else None
+    _timed("nfk_fused_nsf", dev, "nfk_fused_nsf_ws", xp, ldx, wpack.data_ptr(), up_in.data_ptr(),
+           up_out.data_ptr(), up_in.numel(), lo_in.data_ptr(), lo_out.data_ptr(), lo_in.numel(), hidden, zp, ldz,
+           _vec(logdet, B, "logdet"), logdet_mode, B, K, float(tail_bound),
+           1 if inverse else 0, _vec(status, 1, "status", torch.int32),
+           None if ws is None else ws.data_ptr(), nws, _stream(dev))
 
 
 _VJP_ELEMS = {}

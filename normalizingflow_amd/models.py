@@ -365,6 +365,12 @@ class NormalizingFlowModel(nn.Module):
         if not (config.USE_FUSED and config.USE_CHAIN) or x.dim() != 2 or not x.is_cuda \
                 or x.dtype != torch.float32:
             return None
+        # only a model made entirely of NSF_CL (or of RealNVP) layers can be one
+        # chained run: skip the plan's parameter key (a walk of every parameter)
+        # for any other model
+        fl = self.flows
+        if len(fl) < 2 or not (all(isinstance(f, NSF_CL) for f in fl) or all(isinstance(f, RealNVP) for f in fl)):
+            return None
         plan = self._lp_plan(x)
         if plan is None:
             return None

@@ -74,9 +74,11 @@ def test_cl_wide_vs_oracle_and_unfused(mask, inverse, hip_device):
 
 
 def test_cl_wide_round_trip_and_modes(hip_device):
-    """inverse(forward(x)) = x, the two log|det| cancel; the kernel's
-    accumulate mode adds to the buffer; 1 and 64 + 1 rows."""
-    layer = _layer([0, 2], seed=5).to(hip_device)
+    """inverse(forward(x)) = x, the two log|det| cancel (a prefix mask: the
+    reference's inverse reads the lower coordinates at the mask positions of
+    its input, which the masked-first forward output holds only for prefix
+    masks); the kernel's accumulate mode adds to the buffer; 1, 65, 4,096 rows."""
+    layer = _layer([0, 1], seed=5).to(hip_device)
     for rows in (1, 65, 4096):
         x = torch.randn(rows, 96, device=hip_device) * 0.5
         with torch.no_grad():
@@ -127,3 +129,39 @@ def test_cl_wide_outlier_rows_bitwise(hip_device):
         zo, ldo = layer(xo)
     assert torch.equal(z[keep], zo[keep])
     assert torch.equal(ld[keep], ldo[keep])
+
+
+@pytest.mark.parametrize("rows", [1, 40, 333, 4096])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_cl_wide_coordinate_split_bitwise(rows, inverse, hip_device):
+    """Small batches split the upper coordinates over workgroups
+    (nfk_fused_nsf_ws + the per-coordinate log|det| workspace): z, log|det|
+    (modes 1 and 2) and the status word are bitwise the unsplit launch's."""
+    layer = _layer([1], seed=11).to(hip_device)
+    x = torch.randn(rows, 96, device=hip_device) * 0.6
+    maps = layer._maps(x.device)
+    pack = layer._fused_pack(x.device)
+    n_lo, n_up = maps.lo_in.numel(), maps.up_in.numel()
+    nws = K_._lib.load().nfk_fused_nsf_workspace(n_lo, n_up, 354, 32, rows, int(inverse))
+    if rows <= 333:
+        assert nws == n_up * rows
+    res = []
+    for split in (False, True):
+        out = []
+        for mode, init in ((K_.MODE_WRITE, 0.0), (K_.MODE_ACC, 1.5)):
+            z = torch.empty_like(x)
+            ld = torch.full((rows,), init, device=hip_device)
+            st = torch.zeros(1, dtype=torch.int32, device=hip_device)
+            if split:
+                K_.fused_nsf(x, pack, maps.up_in, maps.up_out, maps.lo_in, maps.lo_out, 354, z, logdet=ld,
+                             logdet_mode=mode, K=32, tail_bound=B_APP, inverse=inverse, status=st)
+            else:
+                K_._lib.call("nfk_fused_nsf", x.data_ptr(), 96, pack.data_ptr(), maps.up_in.data_ptr(),
+                             maps.up_out.data_ptr(), n_up, maps.lo_in.data_ptr(), maps.lo_out.data_ptr(), n_lo,
+                             354, z.data_ptr(), 96, ld.data_ptr(), mode, rows, 32, float(B_APP), int(inverse),
+                             st.data_ptr(), K_._stream(x.device))
+            out += [z, ld, st]
+        torch.cuda.synchronize()
+        res.append(out)
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

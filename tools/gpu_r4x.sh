@@ -9,7 +9,7 @@ timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k a
 tail -2 $O/pt_app.log
 timeout -k 10 200 python tools/time_cl354.py > $O/cl354.txt 2>&1 || { tail -5 $O/cl354.txt; exit 1; }
 cat $O/cl354.txt
-NFK_NO_FUSED=1 timeout -k 10 200 python -c "
+timeout -k 10 200 python -c "
 import normalizingflow_amd.config as c; c.USE_FUSED=False
 import runpy, sys; sys.argv=['t']; runpy.run_path('tools/time_cl354.py', run_name='__main__')" > $O/cl354_unfused.txt 2>&1 || { tail -5 $O/cl354_unfused.txt; exit 1; }
 sed 's/^/unfused /' $O/cl354_unfused.txt
