@@ -31,6 +31,11 @@ USE_FCNN_DH    training: the stock FCNN backward's input-gradient GEMMs (g W,
 USE_FCNN_FWD   training: the stock FCNN's recompute forward (Linear + bias +
                Tanh) on nfk_fcnn_linear, the same kernel in forward form;
                off: library GEMMs (addmm) + tanh.
+AR_BATCHED_VJP_BYTES  training: NSF_AR's forward-direction backward recomputes and
+               differentiates ALL its conditioners at once (batched GEMMs over
+               the dim - 1 conditioners, one spline-VJP launch for every column)
+               when its activations take at most this many bytes; above it,
+               one column at a time.  0: always per column.
 """
 STRICT_CHECKS = True
 USE_FUSED = True
@@ -39,3 +44,4 @@ USE_TRAIN_CHAIN = True
 USE_FUSED_VJP = True
 USE_FCNN_DH = True
 USE_FCNN_FWD = True
+AR_BATCHED_VJP_BYTES = 4 << 30

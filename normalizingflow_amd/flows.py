@@ -851,6 +851,12 @@ class NSF_AR(_HipFlow):
         columns last to first, each one's output gradient complete."""
         if not all(_is_stock_fcnn(n) for n in self.layers) or x.shape[1] != self.dim:
             return None
+        if not inverse and self.dim >= 2 and set(names) == set(self._ar_param_names()):
+            H = self.layers[0].network[0].out_features
+            n, P = self.dim - 1, 3 * self.K - 1
+            per = 4 * n * x.shape[0] * (4 * H + 2 * n + 2 * P)  # the batched activations
+            if all(l.network[0].out_features == H for l in self.layers) and per <= config.AR_BATCHED_VJP_BYTES:
+                return self._vjp_batched(x, names, params, gz, gld, need, H)
         p = {n: t.detach() for n, t in zip(names, params)}
         want = {n for n, r in zip(names, need[1:]) if r}
         x = x.detach()
@@ -878,6 +884,100 @@ class NSF_AR(_HipFlow):
             grads.update(gr)
             K_.trig_features_bwd(cond[:, :i], gfeat, gout if inverse else gx, b)
         return _vjp_out(names, need, gx, grads)
+
+    def _ar_param_names(self):
+        return ["init_param"] + ["layers.%d.network.%d.%s" % (i, j, k) for i in range(self.dim - 1)
+                                 for j in (0, 2, 4) for k in ("weight", "bias")]
+
+    def _w1_index(self, H, device):
+        """Flat positions, in the zero-padded [dim-1, H, 2 (dim-1)] stack of the
+        conditioners' first-Linear weights, of each conditioner's W1 [H, 2i]
+        elements in order: its cos column c -> padded column c, its sin column
+        i + c -> padded column (dim - 1) + c (trig_transform's cat(cos, sin),
+        flows.py:172-173, over all dim - 1 leading coordinates)."""
+        key = ("w1idx", H, str(device))
+        idx = self._cols.get(key)
+        if idx is None:
+            n = self.dim - 1
+            parts = []
+            for i in range(1, self.dim):
+                c = torch.arange(2 * i)
+                col = torch.where(c < i, c, (n - i) + c)  # sin column i + c' -> n + c'
+                rows = torch.arange(H)[:, None] * (2 * n) + col[None, :]
+                parts.append(((i - 1) * H * 2 * n + rows).reshape(-1))
+            idx = self._cols[key] = torch.cat(parts).to(device)
+        return idx
+
+    def _vjp_batched(self, x, names, params, gz, gld, need, H):
+        """Forward-direction backward of the whole layer at once.  The dim - 1
+        conditioners are independent given x (flows.py:182-189), so their
+        recompute and backward are batched GEMMs over a stack of the
+        conditioners' weights (the first Linear zero-padded to all 2 (dim - 1)
+        trig features, so conditioner i still sees only x[:, :i]); the spline
+        VJP of every column is one nfk_rqs_coupling_bwd launch; the trig
+        features' backward one nfk_trig_features_bwd over the summed feature
+        gradients.  A few dozen launches instead of ~20 per column: the
+        applications train this layer on 40-50 rows, where launches are the
+        cost.  Same values as the per-column path up to fp32 summation order."""
+        p = {nm: t.detach() for nm, t in zip(names, params)}
+        want = {nm for nm, r in zip(names, need[1:]) if r}
+        x = x.detach().contiguous()
+        B, D, n, P, b = x.shape[0], self.dim, self.dim - 1, 3 * self.K - 1, float(self.B)
+        pre = ["layers.%d.network." % i for i in range(n)]
+        W1 = torch.cat([p[q + "0.weight"].reshape(-1) for q in pre])
+        idx = self._w1_index(H, x.device)
+        W1p = torch.zeros(n * H * 2 * n, dtype=x.dtype, device=x.device)
+        W1p[idx] = W1
+        W1p = W1p.view(n, H, 2 * n)
+        b1 = torch.stack([p[q + "0.bias"] for q in pre])
+        W2 = torch.stack([p[q + "2.weight"] for q in pre])
+        b2 = torch.stack([p[q + "2.bias"] for q in pre])
+        W3 = torch.stack([p[q + "4.weight"] for q in pre])
+        b3 = torch.stack([p[q + "4.bias"] for q in pre])
+        feat = self.trig_transform(x[:, :n])                               # [B, 2n]
+        fb = feat.unsqueeze(0).expand(n, B, 2 * n)
+        h1 = torch.tanh(torch.baddbmm(b1.unsqueeze(1), fb, W1p.transpose(1, 2)))   # [n, B, H]
+        h2 = torch.tanh(torch.baddbmm(b2.unsqueeze(1), h1, W2.transpose(1, 2)))
+        out = torch.baddbmm(b3.unsqueeze(1), h2, W3.transpose(1, 2))              # [n, B, P]
+        prm = torch.cat([p["init_param"].to(x.dtype).expand(B, 1, P), out.transpose(0, 1)], dim=1).contiguous()
+        gprm = torch.empty_like(prm)
+        gx = torch.empty_like(x)
+        cols = self._col_range(x.device)
+        K_.rqs_coupling_bwd(x, prm, cols, cols, _dense(gz, x), None if gld is None else gld.contiguous(), gprm,
+                            gx, K=self.K, left=-b, right=b, bottom=-b, top=b, tails=True, param_mode=0,
+                            inverse=False)
+        grads = {}
+        if "init_param" in want:
+            grads["init_param"] = gprm[:, 0, :].sum(0)
+        g3 = gprm[:, 1:, :].transpose(0, 1).contiguous()                   # [n, B, P]
+        gW3, gb3 = torch.bmm(g3.transpose(1, 2), h2), g3.sum(1)
+        ga2 = torch.bmm(g3, W3) * (1 - h2 * h2)
+        gW2, gb2 = torch.bmm(ga2.transpose(1, 2), h1), ga2.sum(1)
+        ga1 = torch.bmm(ga2, W2) * (1 - h1 * h1)
+        gb1 = ga1.sum(1)
+        gW1 = torch.bmm(ga1.transpose(1, 2), fb).reshape(-1)[idx] if any(q + "0.weight" in want for q in pre) \
+            else None
+        off = 0
+        for i, q in enumerate(pre):
+            if q + "0.weight" in want:
+                sz = H * 2 * (i + 1)
+                grads[q + "0.weight"] = gW1[off:off + sz].view(H, 2 * (i + 1))
+            off += H * 2 * (i + 1)
+            for nm, g in ((q + "0.bias", gb1[i]), (q + "2.weight", gW2[i]), (q + "2.bias", gb2[i]),
+                          (q + "4.weight", gW3[i]), (q + "4.bias", gb3[i])):
+                if nm in want:
+                    grads[nm] = g
+        if need[0]:
+            gfeat = torch.bmm(ga1, W1p).sum(0)                             # [B, 2n]
+            K_.trig_features_bwd(x[:, :n], gfeat, gx, b)
+        return _vjp_out(names, need, gx, grads)
+
+    def _col_range(self, device):
+        key = ("all", str(device))
+        c = self._cols.get(key)
+        if c is None:
+            c = self._cols[key] = torch.arange(self.dim, dtype=torch.int32, device=device)
+        return c
 
     def forward(self, x):
         return self._call(x, False)

@@ -198,3 +198,49 @@ def test_fused_ar_column_split_bitwise(dim, K, H, B, rows, hip_device):
         z_ref, ld_ref = orc.nsf_ar(x.cpu(), _sd(layer), "", dim, K, B)
     close(res[True][0], z_ref, Z_RTOL, Z_ATOL)
     close(res[True][1], ld_ref, LD_RTOL, LD_ATOL * max(1.0, dim / 40.0))
+
+
+@pytest.mark.parametrize("dim,K,H,B,rows", [(96, 32, 354, 1.462, 40), (40, 10, 80, 4.0, 1000), (5, 4, 16, 3.0, 77)])
+def test_ar_batched_backward_vs_per_column(dim, K, H, B, rows, hip_device):
+    """The forward-direction NSF_AR backward batched over all conditioners
+    (NSF_AR._vjp_batched: stacked-weight GEMMs, one spline-VJP launch) against
+    the per-column backward (config.AR_BATCHED_VJP_BYTES = 0) and the oracle's
+    autograd: dL/dx and every parameter gradient, at the applications' shape
+    and batch among others."""
+    torch.manual_seed(31 + dim)
+    layer = nff.NSF_AR(dim=dim, K=K, B=B, hidden_dim=H)
+    sd = _sd(layer)
+    layer = layer.to(hip_device)
+    x = torch.randn(rows, dim, generator=torch.Generator().manual_seed(dim)) * 0.8
+    w = torch.randn(rows, dim, generator=torch.Generator().manual_seed(dim + 1))
+
+    def grads():
+        layer.zero_grad(set_to_none=True)
+        xd = x.to(hip_device).requires_grad_(True)
+        z, ld = layer(xd)
+        ((z * w.to(hip_device)).sum() + ld.sum()).backward()
+        return [xd.grad.detach().clone()] + [p.grad.detach().clone() for p in layer.parameters()]
+
+    prev = config.AR_BATCHED_VJP_BYTES
+    try:
+        g_batched = grads()
+        config.AR_BATCHED_VJP_BYTES = 0
+        g_col = grads()
+    finally:
+        config.AR_BATCHED_VJP_BYTES = prev
+    for a, c in zip(g_batched, g_col):
+        scale = float(c.abs().max()) + 1e-12
+        torch.testing.assert_close(a.cpu(), c.cpu(), rtol=1e-4, atol=1e-5 * scale)
+    # and the oracle's autograd (fp32 restatement) on the same inputs
+    xo = x.clone().requires_grad_(True)
+    po = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    zo, ldo = orc.nsf_ar(xo, po, "", dim, K, B)
+    ((zo * w).sum() + ldo.sum()).backward()
+    # (dL/dx sums the chain through up to dim - 1 conditioners: fp32 summation-order
+    # differences of a few 1e-4 relative in single elements, for the per-column path too)
+    torch.testing.assert_close(g_batched[0].cpu(), xo.grad, rtol=1e-3, atol=5e-5 * float(xo.grad.abs().max()))
+    names = [n for n, _ in layer.named_parameters()]
+    for n, g in zip(names, g_batched[1:]):
+        ref = po[n].grad
+        torch.testing.assert_close(g.cpu(), ref, rtol=1e-3, atol=1e-4 * (float(ref.abs().max()) + 1e-12))
+    flush_status_checks()
