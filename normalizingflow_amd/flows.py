@@ -254,6 +254,10 @@ class _HipFlow(nn.Module):
             if name in self.__dict__:
                 self.__dict__[name] = None
 
+    def _named_param_list(self):
+        """[(name, parameter)] for the autograd node (named_parameters order)."""
+        return list(self.named_parameters())
+
     def _run(self, x, inverse, logdet, mode, status):
         raise NotImplementedError
 
@@ -271,7 +275,7 @@ class _HipFlow(nn.Module):
         if st is None and self._n_status:
             st = torch.zeros(self._n_status, dtype=torch.int32, device=x.device)
         if _needs_grad(self, x):
-            named = list(self.named_parameters())
+            named = self._named_param_list()
             z, logdet = _LayerFn.apply(self, inverse, st, tuple(n for n, _ in named), x,
                                        *(t for _, t in named))
         else:
@@ -764,21 +768,7 @@ class NSF_AR(_HipFlow):
         than the whole launch at their 40-row batches."""
         if not config.USE_FUSED or self.dim < 2:
             return None
-        mods = []
-        for n in self.layers._modules.values():
-            net = n.__dict__["_modules"].get("network")
-            mods.append(n)
-            mods.append(net)
-            if net is not None:
-                mods.extend(net.__dict__["_modules"].values())
-        tree = tuple(map(id, mods))
-        lin = self._ar_tree[1] if self._ar_tree is not None and self._ar_tree[0] == tree else None
-        if lin is None:
-            if not all(_is_stock_fcnn(n) for n in self.layers):
-                self._ar_tree = (tree, [])
-                return None
-            lin = [n.network[j] for n in self.layers for j in (0, 2, 4)]
-            self._ar_tree = (tree, lin)
+        lin = self._stock_linears()
         if not lin:
             return None
         params = [self.init_param]
@@ -849,13 +839,15 @@ class NSF_AR(_HipFlow):
         into the gradient of the coordinates it read -- x[:, :i] forward, the
         output z[:, :i] inverse (flows.py:174-209), so the inverse runs the
         columns last to first, each one's output gradient complete."""
-        if not all(_is_stock_fcnn(n) for n in self.layers) or x.shape[1] != self.dim:
+        lin = self._stock_linears() if self.dim >= 2 else []
+        if (self.dim >= 2 and not lin) or x.shape[1] != self.dim:
             return None
-        if not inverse and self.dim >= 2 and set(names) == set(self._ar_param_names()):
-            H = self.layers[0].network[0].out_features
+        if not inverse and self.dim >= 2 and len(names) == 1 + 6 * (self.dim - 1) \
+                and set(names) == self._ar_name_set():
+            H = lin[0].out_features
             n, P = self.dim - 1, 3 * self.K - 1
             per = 4 * n * x.shape[0] * (4 * H + 2 * n + 2 * P)  # the batched activations
-            if all(l.network[0].out_features == H for l in self.layers) and per <= config.AR_BATCHED_VJP_BYTES:
+            if all(m.out_features == H for m in lin[0::3]) and per <= config.AR_BATCHED_VJP_BYTES:
                 return self._vjp_batched(x, names, params, gz, gld, need, H)
         p = {n: t.detach() for n, t in zip(names, params)}
         want = {n for n, r in zip(names, need[1:]) if r}
@@ -885,9 +877,54 @@ class NSF_AR(_HipFlow):
             K_.trig_features_bwd(cond[:, :i], gfeat, gout if inverse else gx, b)
         return _vjp_out(names, need, gx, grads)
 
-    def _ar_param_names(self):
-        return ["init_param"] + ["layers.%d.network.%d.%s" % (i, j, k) for i in range(self.dim - 1)
-                                 for j in (0, 2, 4) for k in ("weight", "bias")]
+    def _stock_linears(self):
+        """The conditioners' Linear modules in order (3 per conditioner) when
+        every conditioner is the stock FCNN, else []; cached on a fingerprint of
+        the module tree (object ids read from the modules' own dicts)."""
+        mods = []
+        for n in self.layers._modules.values():
+            net = n.__dict__["_modules"].get("network")
+            mods.append(n)
+            mods.append(net)
+            if net is not None:
+                mods.extend(net.__dict__["_modules"].values())
+        tree = tuple(map(id, mods))
+        if self._ar_tree is not None and self._ar_tree[0] == tree:
+            return self._ar_tree[1]
+        lin = [n.network[j] for n in self.layers for j in (0, 2, 4)] \
+            if all(_is_stock_fcnn(n) for n in self.layers) else []
+        self._ar_tree = (tree, lin)
+        return lin
+
+    def _named_param_list(self):
+        """named_parameters() of the layer, cached on the module tree and the
+        parameter objects (ids read from the modules' own dicts): at dim 96 a
+        walk through nn.Module's generators cost ~1.5 ms of host time per call."""
+        if self.__dict__["_parameters"].keys() != {"init_param"}:
+            return list(self.named_parameters())
+        fp = [id(self.__dict__["_parameters"]["init_param"])]
+        for n in self.layers._modules.values():
+            fp.append(id(n))
+            for m in n.__dict__["_modules"].values():
+                fp.append(id(m))
+                for sub in m.__dict__["_modules"].values():
+                    fp.append(id(sub))
+                    fp.extend(map(id, sub.__dict__["_parameters"].values()))
+                fp.extend(map(id, m.__dict__["_parameters"].values()))
+            fp.extend(map(id, n.__dict__["_parameters"].values()))
+        fp = tuple(fp)
+        c = self.__dict__.get("_named_cache")
+        if c is None or c[0] != fp:
+            c = self.__dict__["_named_cache"] = (fp, list(self.named_parameters()))
+        return c[1]
+
+    def _ar_name_set(self):
+        c = self.__dict__.get("_ar_names")
+        if c is None:
+            c = self.__dict__["_ar_names"] = frozenset(
+                ["init_param"] + ["layers.%d.network.%d.%s" % (i, j, k) for i in range(self.dim - 1)
+                                  for j in (0, 2, 4) for k in ("weight", "bias")])
+        return c
 
     def _w1_index(self, H, device):
         """Flat positions, in the zero-padded [dim-1, H, 2 (dim-1)] stack of the
