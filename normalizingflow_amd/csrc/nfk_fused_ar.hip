@@ -716,6 +716,11 @@ inline int ar_waves(const ArDims& d) {
 // one range per conditioner at most; the inverse is sequential (1)
 inline int ar_csplit(const ArDims& d, int dim, int64_t batch, bool inv) {
     if (inv || batch <= 0) return 1;
+    static const int forced = [] {  // diagnostic: NFK_AR_CSPLIT=n forces n column ranges (A/B runs)
+        const char* e = std::getenv("NFK_AR_CSPLIT");
+        return e != nullptr ? std::atoi(e) : 0;
+    }();
+    if (forced > 0) return forced < dim ? forced : dim;
     static const int cus = [] {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
