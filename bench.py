@@ -517,11 +517,24 @@ def roofline_ar(kw, B, per, n_launch, mean_ms, traffic, insts):
         floors["valu_issue_ms"] = round(t_valu, 4)
         if t_valu > t_mfma:
             bound, t_floor = "valu-issue", t_valu
-    achieved = flops / (mean_ms * 1e-3) / 1e12
-    peak = flops / (t_floor * 1e-3) / 1e12
     # x in, z and log|det| out, and every conditioner's weights once per launch
     # (fp16 hi + lo: 4 B per weight; a launch must read them at least once)
     alg = ((2 * dim * 4 + 8) * B + ar_weight_bytes(dim, K, H)) * per
+    # at small batches the weights dominate: reading them once at the HBM peak
+    # is then the binding floor (the applications' 40 rows: 73.6 MB per launch)
+    t_hbm = alg / (PEAK_HBM_GBS * 1e9) * 1e3
+    floors["hbm_ms"] = round(t_hbm, 4)
+    if t_hbm > t_floor:
+        achieved = alg / (mean_ms * 1e-3) / 1e9
+        return {"kernel": "nfk_fused_ar", "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "mfma_frac": round(t_mfma / mean_ms, 4),
+                "traffic": traffic,
+                **hbm_fields(traffic, alg, mean_ms), "launches": n_launch, "mean_ms": round(mean_ms, 4),
+                "floor_ms": round(t_hbm, 4), "floors": floors,
+                "per_launch": "%d samples x %g layers: %d B algorithmic (weights once + x, z, log|det|)"
+                              % (B, per, alg)}
+    achieved = flops / (mean_ms * 1e-3) / 1e12
+    peak = flops / (t_floor * 1e-3) / 1e12
     return {"kernel": "nfk_fused_ar", "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "mfma_frac": round(t_mfma / mean_ms, 4),
             "traffic": traffic,
