@@ -788,7 +788,8 @@ __host__ __device__ inline int64_t cl_nsub(const ArDims& d, int n_up) { return 2
 __host__ __device__ inline int64_t cl_pack_floats(const ArDims& d, int n_up) { return 256 + cl_nsub(d, n_up) * d.SB * 256; }
 
 // instantiated shapes (KBH, T1, K): the applications' H = 354, K = 32
-#define NFK_CL_SHAPES(X) X(11, 1, 32)
+// (Einstein / LJ / Fe_*.yaml) and config.py's defaults H = 100, K = 32
+#define NFK_CL_SHAPES(X) X(11, 1, 32) X(3, 1, 32)
 
 inline bool cl_instance(const ArDims& d, int K) {
 #define NFK_CL_CHK(h, t, k) \

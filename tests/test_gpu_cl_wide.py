@@ -165,3 +165,31 @@ def test_cl_wide_coordinate_split_bitwise(rows, inverse, hip_device):
         res.append(out)
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mask", [[0], [1, 2]])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_cl_config_defaults_vs_oracle(mask, inverse, hip_device):
+    """The applications' config.py defaults for the NSF_CL branch (nsplines 32,
+    hidden 100) on the same kernel (k_fused_cl's H = 100 instance): vs the
+    oracle and the unfused path, 1 and 333 rows."""
+    torch.manual_seed(17 + len(mask))
+    layer = nff.NSF_CL(size=32, dim=3, K=32, B=B_APP, hidden_dim=100, mask=mask)
+    n_lo, n_up = 32 * len(mask), 32 * (3 - len(mask))
+    assert K_.fused_nsf_supported(n_lo, n_up, 100, 32)
+    sd = _sd(layer)
+    layer = layer.to(hip_device)
+    for rows in (1, 333):
+        x = torch.randn(rows, 96, generator=torch.Generator().manual_seed(rows)) * 0.7
+        xd = x.to(hip_device)
+        with torch.no_grad():
+            assert layer._fused_pack(xd.device) is not None
+            z, ld = layer.inverse(xd) if inverse else layer(xd)
+            zu, ldu = _unfused(layer, xd, inverse)
+            if rows > 1:
+                z_ref, ld_ref = orc.nsf_cl(x, sd, "", 32, 3, 32, B_APP, mask, inverse=inverse)
+                close(z, z_ref, Z_RTOL, Z_ATOL)
+                close(ld, ld_ref, LD_RTOL, LD_ATOL)
+        close(z, zu, Z_RTOL, Z_ATOL)
+        close(ld, ldu, LD_RTOL, LD_ATOL)
+    flush_status_checks()
