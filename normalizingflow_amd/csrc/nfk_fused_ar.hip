@@ -128,6 +128,7 @@ inline size_t ar_lds_bytes(const ArDims& d, int dim, bool inv, int nw = kArWaves
     X(3, 1, 10, 4)  /* H = 100, K 10 */                                                           \
     X(3, 1, 32, 4)  /* config.py defaults: H = 100, K 32 (nsplines), dim <= 64 */                \
     X(11, 1, 32, 6) /* Einstein / LJ / Fe_*.yaml: H = 354 (11 k-blocks + 2), K 32, dim <= 96 */ \
+    X(3, 1, 32, 6)  /* config.py defaults (H = 100, K 32) at 32 particles x 3 dims: dim <= 97 */ \
     NFK_AR_DIAG_SHAPES(X)
 #ifndef NFK_AR_DIAG_SHAPES
 #define NFK_AR_DIAG_SHAPES(X)
@@ -144,13 +145,22 @@ inline bool ar_instance(const ArDims& d, int K, int* kbx) {
     return false;
 }
 
+// waves per workgroup of an instance (the wide conditioners: 4)
+inline int ar_waves(const ArDims& d) {
+    static const int nw_env = [] {
+        const char* e = std::getenv("NFK_AR_WAVES");
+        return (e != nullptr && e[0] == '8') ? 8 : 4;
+    }();
+    return ar_min_waves(d.KBH) == 1 ? 4 : nw_env;
+}
+
 inline bool ar_ok(int dim, int hidden, int K) {
     if (dim < 2 || dim > kArMaxDim || hidden < 1 || K < 2) return false;
     const ArDims d = ar_dims(hidden, K, dim);
     int kbx;
     if (!ar_instance(d, K, &kbx)) return false;
-    // both directions fit one workgroup per CU (at the most waves a workgroup may have)
-    const int nw = ar_min_waves(d.KBH) == 1 ? 4 : kArWavesMax;
+    // both directions fit one workgroup per CU at the waves a launch uses
+    const int nw = ar_waves(d);
     return ar_lds_bytes(d, dim, false, nw) <= (size_t)kLdsBytes && ar_lds_bytes(d, dim, true, nw) <= (size_t)kLdsBytes;
 }
 
@@ -702,14 +712,6 @@ __global__ __launch_bounds__(256) void k_ar_ld_sum(const float* cols, float* log
     logdet[r] = mode == 2 ? logdet[r] + acc : acc;
 }
 
-// waves per workgroup of an instance (the wide conditioners: 4)
-inline int ar_waves(const ArDims& d) {
-    static const int nw_env = [] {
-        const char* e = std::getenv("NFK_AR_WAVES");
-        return (e != nullptr && e[0] == '8') ? 8 : 4;
-    }();
-    return ar_min_waves(d.KBH) == 1 ? 4 : nw_env;
-}
 
 // column ranges of a forward launch: enough workgroups for every CU
 // (resident workgroups per CU: 1 for the wide conditioners, else 8 / waves),

@@ -70,7 +70,8 @@ def test_fused_ar_vs_reference_golden(name, hip_device):
 
 @pytest.mark.parametrize("dim,K,H,B,rows", [(40, 10, 80, 4.0, 3000), (17, 8, 100, 3.0, 1000),
                                            (64, 10, 100, 3.0, 2049), (2, 4, 16, 3.0, 77),
-                                           (33, 32, 100, 2.5, 640), (96, 32, 354, 1.462, 333)])
+                                           (33, 32, 100, 2.5, 640), (96, 32, 354, 1.462, 333),
+                                           (96, 32, 100, 1.462, 200)])
 def test_fused_ar_vs_oracle_and_unfused(dim, K, H, B, rows, hip_device):
     """Random weights and ragged batches: the fused layer vs the oracle, and
     the unfused per-column path (library GEMMs + nfk_rqs_coupling) vs the
@@ -160,7 +161,8 @@ def test_fused_ar_no_element_inside_raises(hip_device):
         config.STRICT_CHECKS = prev
 
 
-@pytest.mark.parametrize("dim,K,H,B", [(96, 32, 354, 1.462), (40, 10, 80, 4.0), (24, 32, 100, 3.0)])
+@pytest.mark.parametrize("dim,K,H,B", [(96, 32, 354, 1.462), (40, 10, 80, 4.0), (24, 32, 100, 3.0),
+                                       (96, 32, 100, 1.462)])
 @pytest.mark.parametrize("rows", [1, 40, 50, 333, 4096])
 def test_fused_ar_column_split_bitwise(dim, K, H, B, rows, hip_device):
     """The forward's column split (small batches: the conditioners spread over
