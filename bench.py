@@ -6,6 +6,9 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
+``--gpus N`` alone (no launcher, WORLD_SIZE unset) starts the N rank
+processes itself (spawn_ranks: torchrun's environment, one per GPU).
+
 A step = one NormalizingFlowModel.log_prob pass over this rank's rows of
 synthetic x ~ N(0, I), already resident in HBM (c3: 8 NSF_CL RQS coupling
 layers, D=64, K=8, H=100).  Sample sharding, replicated weights:
@@ -22,10 +25,14 @@ device in a test).  Status checks run deferred (config.STRICT_CHECKS =
 
 Rank 0 prints ONE JSON line with:
   roofline      the dominant kernel's time from HIP events recorded live on
-                its launch stream, against its binding floor: the larger of
-                the MFMA floor of its formulation and the VALU-issue floor
-                from its committed PMC instruction counts
-                (profiles/pmc_insts.json); traffic = PMC HBM bytes per launch
+                its launch stream, against a hardware roofline: the dense
+                f16 MFMA peak for the fused kernels (frac = the MFMA floor of
+                the kernel's formulation / the launch time), HBM for the
+                streaming ones (and for the fused NSF_AR at batches where
+                reading its weights once is the larger floor); the VALU-issue
+                floor from the committed PMC instruction counts
+                (profiles/pmc_insts.json) is a diagnostic entry of `floors`;
+                traffic = PMC HBM bytes per launch
   parity        the oracle's log_prob on the first --parity-rows rows of the
                 benched x and weights vs the values the timed kernel produced
                 (outside the timed region)
@@ -47,7 +54,6 @@ sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
-PEAK_FP16_TFLOPS = 16 * PEAK_FP32_TFLOPS  # MI355X_MICROARCH.md: F16/BF16 MFMA = 16x f32, ~2.5 PF dense
 
 WORKLOADS = {
     # name: (description, layer type, kwargs, D, flops/sample/layer, HBM bytes/sample/layer)
@@ -80,9 +86,11 @@ WORKLOADS = {
 # configs' own training batch (Einstein.yaml / LJ.yaml batch_size 40), where
 # the fused layer splits its conditioners over the GPU (nfk_fused_ar_ws)
 DEFAULT_BATCH = {"c1": 4096, "ar354": 40}
-# BASELINE.md's published figure for the same metric: c1 is quoted on the
-# reference's own CPU path (900,334 samples/s, 8-core Xeon); no GPU figures exist
-BASELINE_CPU = {"c1": 900334.0}  # c1 B = 4096; the others 2^20
+# BASELINE.md's figures for the same metric and config: the reference's own
+# CPU path measured in the survey container (8-core Xeon, 8 threads, fp32;
+# no GPU figures exist): c1 at B = 4096, c2 and c3 at B = 2^20 (c5 is quoted
+# there at B = 65,536 only, so it has none here)
+BASELINE_CPU = {"c1": 900334.0, "c2": 126376.0, "c3": 13918.0}
 
 
 def moons(n, noise=0.05, generator=None, device="cpu"):
@@ -372,30 +380,52 @@ def mfma_per_wave_layer(workload):
     return ((n_lo + 31) // 32) * HT * 3 + HT * per_tile + tiles * per_tile
 
 
-def _floors(flops_f16, flops_f32, B, per, insts, name, workload, n_steps):
-    """(bound, t_floor_ms, floors) of a fused kernel launch: the MFMA floor of
-    its formulation (mfma_per_wave_layer instructions per 16 samples and layer
-    at MFMA_CYC each on the 1024 SIMDs) and, when its PMC instruction counts
-    are committed, the VALU-issue floor; the binding floor is the larger."""
-    n_mfma = mfma_per_wave_layer(workload)
+# dense f16 MFMA peak: one 16x16x32 f16 MFMA (16,384 flop) per 16 cycles per
+# SIMD on 1024 SIMDs at 2.4 GHz = 2,516.6 TFLOP/s (MI355X_MICROARCH.md; AMD's
+# 2:1-sparsity figure is not used)
+MFMA_FLOP = 2 * 16 * 16 * 32
+PEAK_MFMA_F16_TFLOPS = MFMA_FLOP / 16.0 * 1024 * 2.4e9 / 1e12
+
+
+def _floors(B, per, insts, n_mfma):
+    """(t_mfma_ms, floors) of a fused kernel launch: the MFMA floor of its
+    formulation (n_mfma instructions per 16 samples and layer at MFMA_CYC
+    each on the 1024 SIMDs: the hardware roofline) and, as a diagnostic when
+    its PMC instruction counts are committed, the VALU-issue floor."""
     t_mfma = n_mfma * MFMA_CYC * (B / 16.0) * per / N_SIMD / (CLOCK_GHZ * 1e9) * 1e3
     floors = {"mfma_ms": round(t_mfma, 4),
               "mfma_basis": "%d MFMA per 16 samples and layer x %g cyc on 1024 SIMDs at %.1f GHz"
                             % (n_mfma, MFMA_CYC, CLOCK_GHZ)}
-    t_valu = None
     if insts:
         scale = (B / insts["batch"]) * (per / insts.get("layers", 1))
-        t_valu = valu_floor_ms(insts, scale)
-        floors["valu_issue_ms"] = round(t_valu, 4)
-        floors["valu_basis"] = ("%.0f VALU (%.0f transcendental) + %.0f MFMA per launch of %d samples x "
-                                "%g layers (%s); %g cyc per VALU, %g per transcendental, %g per MFMA "
-                                "issue hold, on 1024 SIMDs at %.1f GHz"
+        floors["valu_issue_ms"] = round(valu_floor_ms(insts, scale), 4)
+        floors["valu_basis"] = ("diagnostic, not the roofline: %.0f VALU (%.0f transcendental) + %.0f MFMA "
+                                "per launch of %d samples x %g layers (%s); %g cyc per VALU, %g per "
+                                "transcendental, %g per MFMA issue hold, on 1024 SIMDs at %.1f GHz"
                                 % (insts["valu"], insts["valu_trans"], insts["mfma"], insts["batch"],
                                    insts.get("layers", 1), insts.get("source", "PMC"), VALU_CYC,
                                    TRANS_CYC, MFMA_HOLD_CYC, CLOCK_GHZ))
-    if t_valu is not None and t_valu > t_mfma:
-        return "valu-issue", t_valu, floors
-    return "mfma", t_mfma, floors
+    return t_mfma, floors
+
+
+def _mfma_roofline(name, n_mfma, B, per, mean_ms, t_mfma, ref_flops, floors):
+    """The MFMA-bound roofline fields: achieved = the MFMA pipe's work of the
+    launch (its n_mfma instructions per 16 samples and layer, each one
+    16x16x32-f16 issue slot = 16,384 flop) / the launch time, peak = the dense
+    f16 MFMA peak, so frac = the MFMA floor / the launch time."""
+    mflops = n_mfma * MFMA_FLOP * (B / 16.0) * per
+    achieved = mflops / (mean_ms * 1e-3) / 1e12
+    return {"kernel": name, "bound": "mfma", "achieved": round(achieved, 2),
+            "peak": round(PEAK_MFMA_F16_TFLOPS, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_MFMA_F16_TFLOPS, 4),
+            "mfma_frac": round(t_mfma / mean_ms, 4),
+            "floor_ms": round(t_mfma, 4), "floors": floors,
+            "peak_basis": "dense f16 MFMA peak (16x16x32 f16: 16,384 flop per 16 cycles per SIMD, 1024 SIMDs, "
+                          "2.4 GHz); achieved = the launch's MFMA issue slots x 16,384 flop / launch time "
+                          "(the 16x16x16 tail MFMAs occupy a full slot)",
+            "ref_fp32_equiv_tflops": round(ref_flops / (mean_ms * 1e-3) / 1e12, 2),
+            "ref_fp32_equiv_basis": "the reference FCNN's fp32 flops (SURVEY 8(d)) / launch time",
+            "vs_fp32_mfma_peak": round(ref_flops / (mean_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4)}
 
 
 def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
@@ -425,21 +455,16 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
             f32 = 2.0 * tail * (H + n_up * P)
             f16 = 2.0 * (n_lo * H + H * H + H * n_up * P) - f32  # 173,600/sample/layer
         flops = (f16 + f32) * B * per
-        bound, t_floor, floors = _floors(f16, f32, B, per, insts, name, workload, n_steps)
-        achieved = flops / (mean_ms * 1e-3) / 1e12
-        peak = flops / (t_floor * 1e-3) / 1e12
+        n_mfma = mfma_per_wave_layer(workload)
+        t_mfma, floors = _floors(B, per, insts, n_mfma)
         alg = (D * 4 + 4) * B if name.endswith("_chain") else (2 * D * 4 + 8) * B  # x (+ z, log|det|) or log p
-        return {"kernel": name, "bound": bound, "achieved": round(achieved, 2),
-                "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "mfma_frac": round(floors["mfma_ms"] / mean_ms, 4),
-                "traffic": traffic, **hbm_fields(traffic, alg, mean_ms),
-                "launches": n_launch, "mean_ms": round(mean_ms, 4),
-                "floor_ms": round(t_floor, 4), "floors": floors,
-                "per_launch": "%d samples x %g layers x %.0f flop (fp32-equivalent)"
-                              % (B, per, flops / B / per),
-                "peak_basis": "fp32-equivalent flop per launch / the binding floor (the larger of "
-                              "the MFMA floor and the VALU-issue floor, see floors)",
-                "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
+        out = _mfma_roofline(name, n_mfma, B, per, mean_ms, t_mfma, flops, floors)
+        out.update({"traffic": traffic, **hbm_fields(traffic, alg, mean_ms),
+                    "launches": n_launch, "mean_ms": round(mean_ms, 4),
+                    "per_launch": "%d samples x %g layers: %d MFMA per 16 samples and layer; reference "
+                                  "%.0f flop per sample and layer (fp32-equivalent)"
+                                  % (B, per, n_mfma, flops / B / per)})
+        return out
     if name == "nfk_fused_ar":
         return roofline_ar(kw, B, L * n_steps / n_launch, n_launch, mean_ms, traffic, insts)
     if name == "nfk_rqs_coupling" and kind == "NSF_AR":
@@ -490,12 +515,13 @@ def ar_mfma_per_wave_layer(dim, K, H):
     nfk_fused_ar's formulation: conditioner i = 1 .. dim-1 runs layer 1 over
     ceil(2i / 32) k-blocks and HT hidden tiles (3 split products each), layer 2
     and the output layer (ceil((3K-1) / 16) tiles) over KBH k-blocks (+1 tail
-    MFMA per tile when H = 32 KBH + 1..4)."""
+    MFMA per tile when H = 32 KBH + 1..4, +2 when H = 32 KBH + 5..16: the
+    16-feature half tile, nfk_fused_ar.hip ar_dims)."""
     kbf, R = divmod(H, 32)
-    T1 = 1 if (0 < R <= 4 and kbf >= 1) else 0
-    KBH = kbf if (R == 0 or T1) else kbf + 1
-    HT, NO = 2 * KBH + T1, (3 * K - 1 + 15) // 16
-    per_tile = 3 * KBH + T1
+    TK = 0 if (R == 0 or kbf < 1) else (1 if R <= 4 else (2 if R <= 16 else 0))
+    KBH = kbf if (R == 0 or TK) else kbf + 1
+    HT, NO = 2 * KBH + (1 if TK else 0), (3 * K - 1 + 15) // 16
+    per_tile = 3 * KBH + TK
     return sum(((2 * i + 31) // 32) * HT * 3 + (HT + NO) * per_tile for i in range(1, dim))
 
 
@@ -507,16 +533,7 @@ def roofline_ar(kw, B, per, n_launch, mean_ms, traffic, insts):
     fl = sum(2.0 * (2 * i * H + H * H + H * (3 * K - 1)) for i in range(1, dim))
     flops = fl * B * per
     n_mfma = ar_mfma_per_wave_layer(dim, K, H)
-    t_mfma = n_mfma * MFMA_CYC * (B / 16.0) * per / N_SIMD / (CLOCK_GHZ * 1e9) * 1e3
-    floors = {"mfma_ms": round(t_mfma, 4),
-              "mfma_basis": "%d MFMA per 16 samples and layer x %g cyc on 1024 SIMDs at %.1f GHz"
-                            % (n_mfma, MFMA_CYC, CLOCK_GHZ)}
-    bound, t_floor = "mfma", t_mfma
-    if insts:
-        t_valu = valu_floor_ms(insts, (B / insts["batch"]) * (per / insts.get("layers", 1)))
-        floors["valu_issue_ms"] = round(t_valu, 4)
-        if t_valu > t_mfma:
-            bound, t_floor = "valu-issue", t_valu
+    t_mfma, floors = _floors(B, per, insts, n_mfma)
     # x in, z and log|det| out, and every conditioner's weights once per launch
     # (fp16 hi + lo: 4 B per weight; a launch must read them at least once)
     alg = ((2 * dim * 4 + 8) * B + ar_weight_bytes(dim, K, H)) * per
@@ -524,7 +541,7 @@ def roofline_ar(kw, B, per, n_launch, mean_ms, traffic, insts):
     # is then the binding floor (the applications' 40 rows: 73.6 MB per launch)
     t_hbm = alg / (PEAK_HBM_GBS * 1e9) * 1e3
     floors["hbm_ms"] = round(t_hbm, 4)
-    if t_hbm > t_floor:
+    if t_hbm > t_mfma:
         achieved = alg / (mean_ms * 1e-3) / 1e9
         return {"kernel": "nfk_fused_ar", "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "mfma_frac": round(t_mfma / mean_ms, 4),
@@ -533,16 +550,12 @@ def roofline_ar(kw, B, per, n_launch, mean_ms, traffic, insts):
                 "floor_ms": round(t_hbm, 4), "floors": floors,
                 "per_launch": "%d samples x %g layers: %d B algorithmic (weights once + x, z, log|det|)"
                               % (B, per, alg)}
-    achieved = flops / (mean_ms * 1e-3) / 1e12
-    peak = flops / (t_floor * 1e-3) / 1e12
-    return {"kernel": "nfk_fused_ar", "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
-            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "mfma_frac": round(t_mfma / mean_ms, 4),
-            "traffic": traffic,
-            **hbm_fields(traffic, alg, mean_ms), "launches": n_launch, "mean_ms": round(mean_ms, 4),
-            "floor_ms": round(t_floor, 4), "floors": floors,
-            "per_launch": "%d samples x %g layers x %.0f flop (reference FCNN flops, fp32-equivalent)"
-                          % (B, per, fl),
-            "vs_fp32_mfma_peak": round(achieved / PEAK_FP32_TFLOPS, 4)}
+    out = _mfma_roofline("nfk_fused_ar", n_mfma, B, per, mean_ms, t_mfma, flops, floors)
+    out.update({"traffic": traffic, **hbm_fields(traffic, alg, mean_ms), "launches": n_launch,
+                "mean_ms": round(mean_ms, 4),
+                "per_launch": "%d samples x %g layers: %d MFMA per 16 samples and layer; reference %.0f flop "
+                              "per sample and layer (FCNN flops, fp32-equivalent)" % (B, per, n_mfma, fl)})
+    return out
 
 
 def load_traffic(kernel, workload, batch=None):
@@ -567,6 +580,39 @@ def load_traffic(kernel, workload, batch=None):
         return None
     scale = 1.0 if batch is None else batch / float(rec.get("batch", 1 << 20))
     return int(rec["bytes_per_launch"] * scale)
+
+
+def spawn_ranks(n):
+    """``--gpus N`` (N > 1) started without a launcher (no WORLD_SIZE in the
+    environment): start the N rank processes of this same command line, one
+    per GPU, with torchrun's environment contract (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), before anything in
+    this process touches the GPU (child processes, no exec).  Rank 0 prints the
+    line.  If a rank fails the others are stopped (by their own PIDs) and its
+    exit code is returned."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for o in procs:  # a failed rank leaves the others waiting on a collective
+                    o.kill()
+    return rc
 
 
 def main():
@@ -601,6 +647,8 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="a process group and the NLL all-reduce even at N = 1 (RCCL on a one-GPU box)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     dflt = DEFAULT_BATCH.get(args.workload, 1 << 20)
     args.batch = dflt if args.batch is None else args.batch
     args.global_batch = dflt if args.global_batch is None else args.global_batch

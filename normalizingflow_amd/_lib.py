@@ -82,12 +82,12 @@ SIGNATURES = {
         P, P, I32,                      # up_in, up_out, n_up
         P, P, I32, I32,                 # lo_in, lo_out, n_lo, hidden
         P, I64, P, I32,                 # z, ldz, logdet, logdet_mode
-        I64, I32, F64, I32, P, P]),     "nfk_fused_nsf_workspace": (ctypes.c_int64, [I32, I32, I32, I32, I64, I32]),
+        I64, I32, F64, I32, P, P]),     # batch, K, tail_bound, inverse, status, stream
+    "nfk_fused_nsf_workspace": (ctypes.c_int64, [I32, I32, I32, I32, I64, I32]),
     "nfk_fused_nsf_ws": (ctypes.c_int, [
         P, I64, P, P, P, I32, P, P, I32, I32,   # x, ldx, wpack, up_in, up_out, n_up, lo_in, lo_out, n_lo, hidden
         P, I64, P, I32, I64, I32, F64, I32, P,  # z, ldz, logdet, mode, batch, K, tail_bound, inverse, status
         P, I64, P]),                            # workspace, workspace_floats, stream
-    # batch, K, tail_bound, inverse, status, stream
     "nfk_fused_nsf_chain_max": (ctypes.c_int, [I32, I32, I32, I32]),
     "nfk_fused_nsf_chain": (ctypes.c_int, [
         P, I64, P, P, I32,              # x, ldx, wpacks, cmaps, nlayers

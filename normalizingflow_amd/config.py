@@ -25,6 +25,10 @@ USE_TRAIN_CHAIN training (forward direction under autograd): consecutive fused
 USE_FUSED_VJP  training: NSF_CL's backward through nfk_fused_nsf_vjp (conditioner
                recompute on the matrix cores + spline VJP in one kernel) where
                the shape is supported; off: recompute GEMMs + nfk_rqs_coupling_bwd.
+FUSED_VJP_MAX_ROWS  training: the largest batch the fused VJP kernel takes (None:
+               any); larger batches run the unfused backward (recompute GEMMs +
+               nfk_rqs_coupling_bwd).  A switch, not a correctness gate: the fused
+               VJP is bitwise reproducible at every batch.
 USE_FCNN_DH    training: the stock FCNN backward's input-gradient GEMMs (g W,
                tanh's backward fused) on nfk_fcnn_dh (fp16-split MFMA) where
                the shape is supported; off: fp32 library GEMMs + tanh_backward.
@@ -42,6 +46,7 @@ USE_FUSED = True
 USE_CHAIN = True
 USE_TRAIN_CHAIN = True
 USE_FUSED_VJP = True
+FUSED_VJP_MAX_ROWS = None
 USE_FCNN_DH = True
 USE_FCNN_FWD = True
 AR_BATCHED_VJP_BYTES = 4 << 30

@@ -583,6 +583,11 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
                 case 4: if constexpr (KBX >= 4) layer1(std::integral_constant<int, 4>{}); break;
                 case 5: if constexpr (KBX >= 5) layer1(std::integral_constant<int, 5>{}); break;
                 case 6: if constexpr (KBX >= 6) layer1(std::integral_constant<int, 6>{}); break;
+                case 7: if constexpr (KBX >= 7) layer1(std::integral_constant<int, 7>{}); break;
+                case 8: if constexpr (KBX >= 8) layer1(std::integral_constant<int, 8>{}); break;
+                case 9: if constexpr (KBX >= 9) layer1(std::integral_constant<int, 9>{}); break;
+                case 10: if constexpr (KBX >= 10) layer1(std::integral_constant<int, 10>{}); break;
+                case 11: if constexpr (KBX >= 11) layer1(std::integral_constant<int, 11>{}); break;
                 default: break;
             }
             f32x4 o[NO];

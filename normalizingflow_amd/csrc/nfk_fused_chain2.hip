@@ -282,6 +282,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                 for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
                 int ex = 0;
                 if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
+                ex = ex < -64 ? -64 : ex;  // a tiny sample: its scale 2^(14 - ex) and bias scale stay finite
                 const float sx = ldexpf(1.0f, 14 - ex);
                 unx[s] = ldexpf(un1, ex - 14);
                 const float bsc = ldexpf(1.0f, 14 - ex) / un1;

@@ -1137,6 +1137,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
             for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
             int ex = 0;
             if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
+            ex = ex < -64 ? -64 : ex;  // a tiny sample: its scale 2^(14 - ex) and bias scale stay finite
             const float sx = ldexpf(1.0f, 14 - ex);
             unx = ldexpf(un1, ex - 14);
             // accumulators start at b1 2^(s1+sx) (exact power-of-two scaling), so the

@@ -168,6 +168,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void k_fused_rnvp(RArgs a) {
             for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
             int ex = 0;
             if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
+            ex = ex < -64 ? -64 : ex;  // a tiny sample: its scale 2^(14 - ex) and bias scale stay finite
             const float sx = ldexpf(1.0f, 14 - ex);
             h8 xh[KBI], xl[KBI];
 #pragma unroll
@@ -616,6 +617,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_rnvp_chain(RChainArgs a) 
 #pragma unroll
                 for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
                 if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
+                ex = ex < -64 ? -64 : ex;  // a tiny sample: its scale 2^(14 - ex) and bias scale stay finite
                 const float sx = ldexpf(1.0f, 14 - ex);
 #pragma unroll
                 for (int kb = 0; kb < KBI; ++kb) {

@@ -86,6 +86,13 @@ __device__ __forceinline__ void store_act(const f32x4 (&h)[HT], float* row, int 
     if (q == 1) row[H] = 1.0f;
 }
 
+#ifdef NFK_VJP_DIAG_SAVE  // diagnostic: every element backward's inputs, [B][n_up][3K + 2] floats
+__device__ float* g_vjp_dbg;
+extern "C" int nfk_vjp_diag_set(float* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_vjp_dbg), &p, sizeof(p), 0, hipMemcpyHostToDevice);
+}
+#endif
+
 template <int KBH, bool T1, int K, bool INV>
 __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
     constexpr VjpDims d = vjp_dims(KBH, T1 ? 1 : 0, K);
@@ -177,6 +184,7 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
         for (int off = 16; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));  // per sample: the 4 lanes of column sl
         int ex = 0;
         if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);
+        ex = ex < -64 ? -64 : ex;  // a tiny sample: its scale 2^(14 - ex) and bias scale stay finite
         const float sx = ldexpf(1.0f, 14 - ex);
         h8 xh[1], xl[1];
 #pragma unroll
@@ -239,6 +247,20 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
             }
             const float xv = tile[sl * XS + m_up_in[j]];
             const float go = (a.gz != nullptr) ? a.gz[b * a.ldgz + m_up_out[j]] : 0.0f;
+#ifdef NFK_VJP_DIAG_SAVE
+            if (row_ok) {
+                float* sv = g_vjp_dbg + (b * n_up + j) * (3 * K + 2);
+#pragma unroll
+                for (int i = 0; i < K; ++i) sv[i] = wr[i];
+#pragma unroll
+                for (int i = 0; i < K; ++i) sv[K + i] = hr[i];
+#pragma unroll
+                for (int i = 0; i < K - 1; ++i) sv[2 * K + i] = dr[i];
+                sv[3 * K - 1] = xv;
+                sv[3 * K] = go;
+                sv[3 * K + 1] = gl;
+            }
+#endif
 #ifdef NFK_VJP_DUMP  // diagnostic: the element backward's inputs instead of its outputs
             const float gxv = xv + 1000.0f * go + 1.0e6f * gl;
 #else

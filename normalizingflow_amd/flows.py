@@ -648,7 +648,8 @@ class NSF_CL(_HipFlow):
         # weight gradients); any other conditioner through autograd
         manual = _is_stock_fcnn(self.psi) and set(names) == set(
             "psi.network.%d.%s" % (i, k) for i in (0, 2, 4) for k in ("weight", "bias"))
-        vpack = self._vjp_pack(x.device) if manual else None
+        rows_ok = config.FUSED_VJP_MAX_ROWS is None or x.shape[0] <= config.FUSED_VJP_MAX_ROWS
+        vpack = self._vjp_pack(x.device) if manual and rows_ok else None
         if vpack is not None:
             # fused: the conditioner recomputed on the matrix cores and the
             # spline VJP in one kernel (nfk_fused_nsf_vjp); it hands over
@@ -846,7 +847,11 @@ class NSF_AR(_HipFlow):
                 and set(names) == self._ar_name_set():
             H = lin[0].out_features
             n, P = self.dim - 1, 3 * self.K - 1
-            per = 4 * n * x.shape[0] * (4 * H + 2 * n + 2 * P)  # the batched activations
+            # peak bytes of the batched backward per (conditioner, row): h1, h2,
+            # the tanh-derivative temporaries and ga1/ga2 with theirs (8 H), the
+            # logits, their gradient and its transposed copy (3 P), the expanded
+            # trig features bmm materialises and the feature-gradient product (4 n)
+            per = 4 * n * x.shape[0] * (8 * H + 3 * P + 4 * n)
             if all(m.out_features == H for m in lin[0::3]) and per <= config.AR_BATCHED_VJP_BYTES:
                 return self._vjp_batched(x, names, params, gz, gld, need, H)
         p = {n: t.detach() for n, t in zip(names, params)}
@@ -893,7 +898,9 @@ class NSF_AR(_HipFlow):
             return self._ar_tree[1]
         lin = [n.network[j] for n in self.layers for j in (0, 2, 4)] \
             if all(_is_stock_fcnn(n) for n in self.layers) else []
-        self._ar_tree = (tree, lin)
+        # the fingerprinted modules are kept alive with it, so none of their ids
+        # can be reused by a replacement module while the entry stands
+        self._ar_tree = (tree, lin, mods)
         return lin
 
     def _named_param_list(self):

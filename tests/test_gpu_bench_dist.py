@@ -91,6 +91,28 @@ def test_bench_world2_single_mode_nll_vs_oracle(hip_device, scaling, rows):
     assert abs(line["nll"] - ref) <= 1e-5 * abs(ref), (line["nll"], ref)
 
 
+def test_bench_gpus2_without_launcher_spawns_ranks(hip_device):
+    """`python bench.py --gpus 2` with no launcher (WORLD_SIZE unset) starts its
+    own two ranks (bench.spawn_ranks, torchrun's environment contract): ONE
+    line with n_gpus 2 whose all-reduced NLL equals the oracle's over both
+    ranks' rows -- however the driver invokes the N-GPU run, it measures N ranks."""
+    rows = 12288
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--scaling", "weak", "--batch", str(rows), "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--parity-rows", "1024"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 2 * rows
+    assert line["config"]["backend"] == "gloo" and line["parity"]["pass"]
+    ref = _nll_ref(hip_device, [rows, rows])
+    assert abs(line["nll"] - ref) <= 1e-5 * abs(ref), (line["nll"], ref)
+
+
 def test_bench_rccl_world1_nll_vs_oracle(hip_device):
     """The RCCL leg of the same path: one rank under torchrun with a real
     "nccl" (RCCL) process group (--dist keeps the group and the NLL

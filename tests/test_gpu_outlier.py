@@ -126,6 +126,82 @@ def test_outlier_rows_leave_other_rows_bitwise(kind, n_layers, rows, chain, inve
         torch.testing.assert_close(zb[k].cpu(), z_ref, rtol=Z_RTOL, atol=Z_ATOL)
 
 
+TINY = (1e-35, 3e-30, 2e-33)
+
+
+@pytest.mark.parametrize("kind,n_layers,rows,chain", [
+    ("c3", 4, 2048, True), ("c3", 4, 2048, False), ("c5", 4, 1024, True), ("c2", 4, 2048, True)])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_tiny_rows_vs_oracle(kind, n_layers, rows, chain, inverse, hip_device, lax_checks):
+    """A row whose coordinates are all nonzero but below ~1e-29: its per-sample
+    layer-1 scale 2^(14 - ex) is clamped (ex >= -64), so its bias scale stays
+    finite.  That row matches the oracle and the other rows stay bitwise
+    those of the batch without it (without the clamp the row was NaN)."""
+    config.USE_CHAIN = chain
+    model, D = _model(kind, n_layers)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    specs = _specs(model)
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(rows, D, generator=g)
+    rws = _outlier_rows(rows)
+    xt = x.clone()
+    for i, r in enumerate(rws.tolist()):
+        xt[r] = TINY[i % len(TINY)] * torch.sign(torch.randn(D, generator=g))
+    keep = torch.ones(rows, dtype=torch.bool)
+    keep[rws] = False
+    model = _to_dev(model, D, hip_device)
+    with torch.no_grad():
+        if inverse:
+            a, _ = model.inverse(x.to(hip_device))
+            b, ldb = model.inverse(xt.to(hip_device))
+        else:
+            a = model.log_prob(x.to(hip_device))
+            b = model.log_prob(xt.to(hip_device))
+    k = keep.to(hip_device)
+    assert torch.isfinite(b).all(), "a tiny row came out non-finite"
+    assert torch.equal(a[k], b[k]), "a tiny row changed another row's result"
+    tiny = xt[rws]
+    if inverse:
+        x_ref, ld_ref = orc.model_inverse(specs, sd, tiny)
+        torch.testing.assert_close(b[~k].cpu(), x_ref, rtol=Z_RTOL, atol=1e-4)
+        torch.testing.assert_close(ldb[~k].cpu(), ld_ref, rtol=1e-5, atol=2e-4)
+    else:
+        torch.testing.assert_close(b[~k].cpu(), orc.model_log_prob(specs, sd, tiny), rtol=LP_RTOL, atol=LP_ATOL)
+
+
+def test_tiny_rows_fused_vjp(hip_device, lax_checks):
+    """The fused VJP kernel on rows of ~1e-35: finite dL/dx and dL/dparams that
+    match the unfused backward's (the same clamp as the forward kernels)."""
+    model, D = _model("c3", 1)
+    model = _to_dev(model, D, hip_device)
+    layer = model.flows[0]
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(1024, D, generator=g)
+    rws = _outlier_rows(1024)
+    for i, r in enumerate(rws.tolist()):
+        x[r] = TINY[i % len(TINY)] * torch.sign(torch.randn(D, generator=g))
+    gz = torch.randn(1024, D, generator=g).to(hip_device) * 1e-3
+    grads = []
+    for fused in (True, False):
+        old = config.USE_FUSED_VJP
+        config.USE_FUSED_VJP = fused
+        try:
+            xd = x.to(hip_device).requires_grad_(True)
+            z, ld = layer(xd)
+            ((z * gz).sum() + ld.sum()).backward()
+            grads.append((xd.grad.clone(), [p.grad.clone() for p in layer.parameters()]))
+            layer.zero_grad()
+        finally:
+            config.USE_FUSED_VJP = old
+    (gx_f, gp_f), (gx_u, gp_u) = grads
+    assert torch.isfinite(gx_f).all() and all(torch.isfinite(p).all() for p in gp_f)
+    # the tiny rows themselves (elsewhere the two backwards differ only on
+    # knife-edge rows, tests/test_gpu_vjp.py)
+    torch.testing.assert_close(gx_f[rws], gx_u[rws], rtol=1e-4, atol=1e-5)
+    for a, b in zip(gp_f, gp_u):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+
+
 def test_outlier_rows_training_kernels(hip_device, lax_checks):
     """Training: the saved-input chain forward and the fused VJP kernel give the
     clean rows bitwise the same z, log|det|, dL/dx and dL/dparams rows."""
