@@ -81,11 +81,21 @@ WORKLOADS = {
     "ar354": ("96-dim synthetic Gaussian, NSF_AR autoregressive RQS (Einstein.yaml: K=32, H=354, "
               "B=1.462, 2 layers), log_prob", "NSF_AR",
               dict(dim=96, K=32, B=(32 / (8 * 1.28)) ** (1.0 / 3.0), hidden_dim=354), 96, 2),
+    # the Fe configs' flow (applications/input/Fe_100K.yaml; Fe_400K / Fe_700K the
+    # same): 54 particles x 3 dims = 162 coordinates, nsplines 32, hidden 354,
+    # nlayers 2, B = ncellx * cell_len / 2 = 3 * 2.8841 / 2 (setup.py:44-58)
+    "fe162": ("162-dim synthetic Gaussian, NSF_AR autoregressive RQS (Fe_*.yaml: K=32, H=354, "
+              "B=4.326, 2 layers), log_prob", "NSF_AR", dict(dim=162, K=32, B=3 * 2.8841 / 2, hidden_dim=354),
+              162, 2),
+    # Polymer.yaml's flow: 2048 particles x 1 dim, nsplines 32, hidden_dim from
+    # config.py:40 (100), nlayers 2, B = ncellx * cell_len / 2 = 0.5
+    "poly2048": ("2048-dim synthetic Gaussian, NSF_AR autoregressive RQS (Polymer.yaml: K=32, H=100, "
+                 "B=0.5, 2 layers), log_prob", "NSF_AR", dict(dim=2048, K=32, B=0.5, hidden_dim=100), 2048, 2),
 }
 # default per-GPU rows: c1 is BASELINE's 4,096-row case; ar354 runs at its
 # configs' own training batch (Einstein.yaml / LJ.yaml batch_size 40), where
 # the fused layer splits its conditioners over the GPU (nfk_fused_ar_ws)
-DEFAULT_BATCH = {"c1": 4096, "ar354": 40}
+DEFAULT_BATCH = {"c1": 4096, "ar354": 40, "fe162": 50, "poly2048": 40}
 # BASELINE.md's figures for the same metric and config: the reference's own
 # CPU path measured in the survey container (8-core Xeon, 8 threads, fp32;
 # no GPU figures exist): c1 at B = 4096, c2 and c3 at B = 2^20 (c5 is quoted
@@ -123,6 +133,8 @@ METRICS = {
     "c1": "samples/sec log_prob (4096×2 two moons, 4 RealNVP affine coupling layers)",
     "ar": "samples/sec log_prob (1M×40, 1 NSF_AR autoregressive RQS layer, K=10, H=80)",
     "ar354": "samples/sec log_prob (96-dim rows, 2 NSF_AR autoregressive RQS layers, K=32, H=354; rows per step = config.global_batch, default the applications' 40)",
+    "fe162": "samples/sec log_prob (162-dim rows, 2 NSF_AR autoregressive RQS layers, K=32, H=354; rows per step = config.global_batch, default the Fe configs' 50)",
+    "poly2048": "samples/sec log_prob (2048-dim rows, 2 NSF_AR autoregressive RQS layers, K=32, H=100; rows per step = config.global_batch, default Polymer.yaml's 40)",
 }
 
 
@@ -137,6 +149,9 @@ ARITH = {
     "ar": _SPLIT + " (nfk_fused_ar.hip; layer 1 on the fp16-split trig features)",
     "ar354": _SPLIT + "; the 2 tail features of H=354 as one 16x16x16 f16 MFMA per tile"
              " (nfk_fused_ar.hip, one wave per SIMD; layer 1 on the fp16-split trig features)",
+    "fe162": _SPLIT + "; the 2 tail features of H=354 as one 16x16x16 f16 MFMA per tile"
+             " (nfk_fused_ar.hip, one wave per SIMD; layer 1 on the fp16-split trig features)",
+    "poly2048": _SPLIT + _TAIL + " (nfk_fused_ar.hip; layer 1 on the fp16-split trig features)",
 }
 # the line's dtype: what the path computes in (fp32 values and outputs; the
 # conditioner's products on the fp16 matrix cores as a two-way split)
@@ -680,11 +695,11 @@ def main():
         """auto: a HIP graph replay where launches are a visible part of the
         step -- the small-batch workloads (c1) and per-rank batches of at most
         2^17 rows (the 8-GPU strong-scaling shard), where the host-side launch
-        and status-copy overhead is ~2 % of a step.  Not ar354, whose step is
-        milliseconds at any batch (and whose roofline needs the kernel timer)."""
+        and status-copy overhead is ~2 % of a step.  Not the NSF_AR workloads
+        (ar354, fe162, poly2048), whose roofline needs the kernel timer."""
         if args.graph != "auto":
             return args.graph == "on"
-        return args.workload == "c1" or (B <= (1 << 17) and args.workload != "ar354")
+        return args.workload == "c1" or (B <= (1 << 17) and WORKLOADS[args.workload][1] != "NSF_AR")
 
     def run(mode):
         """One mode's timed loop: W warm-up steps, then K steps bracketed by a

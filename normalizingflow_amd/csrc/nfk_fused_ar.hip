@@ -80,7 +80,7 @@ __host__ __device__ constexpr int ar_min_waves(int kbh) { return kbh <= 4 ? 2 : 
 // or 8 (one workgroup per CU; half the weight stream per sample, but its two
 // waves per SIMD run every phase in lockstep); NFK_AR_WAVES selects
 constexpr int kArWavesMax = 8;
-constexpr int kArMaxDim = 128;
+constexpr int kArMaxDim = 256;  // (the instances' layer-1 capacity KBX bounds it further)
 
 // T1 = the hidden width's tail kind: 0 none (H = 32 KBH), 1 = 1..4 features
 // (the NSF_CL kernels' f16 tail step), 2 = 5..16 features (a 16-row half tile:
@@ -127,7 +127,8 @@ inline size_t ar_lds_bytes(const ArDims& d, int dim, bool inv, int nw = kArWaves
     X(3, 1, 8, 4)   /* H = 100 (config.py:40), K 8, dim <= 64 */                                 \
     X(3, 1, 10, 4)  /* H = 100, K 10 */                                                           \
     X(3, 1, 32, 4)  /* config.py defaults: H = 100, K 32 (nsplines), dim <= 64 */                \
-    X(11, 1, 32, 6) /* Einstein / LJ / Fe_*.yaml: H = 354 (11 k-blocks + 2), K 32, dim <= 96 */ \
+    X(11, 1, 32, 6) /* Einstein / LJ.yaml: H = 354 (11 k-blocks + 2), K 32, 32 x 3 = 96 coords */ \
+    X(11, 1, 32, 11) /* Fe_*.yaml: H = 354, K 32, 54 particles x 3 = 162 coordinates (<= 177) */ \
     X(3, 1, 32, 6)  /* config.py defaults (H = 100, K 32) at 32 particles x 3 dims: dim <= 97 */ \
     NFK_AR_DIAG_SHAPES(X)
 #ifndef NFK_AR_DIAG_SHAPES

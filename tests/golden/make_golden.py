@@ -493,11 +493,23 @@ def case_layer_seeded(name, ctor, kwargs, x, seed=1234):
         arrays.update(rt_x=xi, rt_ld=ldi)
         xa, lda = layer.inverse(x.clone())
         arrays.update(inv_x=xa, inv_ld=lda)
-    for k, v in layer.state_dict().items():
-        v64 = v.detach().double().flatten()
-        arrays["sdsum." + k] = torch.stack([v64.sum(), v64.square().sum()])
-        arrays["sdhead." + k] = v.detach().flatten()[:8].clone()
+    sd = layer.state_dict()
+    sums = [torch.stack([v.detach().double().flatten().sum(), v.detach().double().flatten().square().sum()])
+            for v in sd.values()]
+    heads = [torch.nn.functional.pad(v.detach().flatten()[:8], (0, max(0, 8 - v.numel()))) for v in sd.values()]
     meta = dict(kind="layer", type=ctor.__name__, kwargs=kwargs, seed=seed, sd_from_seed=True)
+    if len(sd) > 1000:
+        # thousands of tensors (Polymer's 2,047 conditioners): one array each of
+        # sums and heads in state_dict order (per-entry arrays cost ~0.5 KB of
+        # zip headers apiece)
+        arrays["sdsum_all"] = torch.stack(sums)
+        arrays["sdhead_all"] = torch.stack(heads)
+        meta["sd_keys"] = list(sd.keys())
+        meta["sd_numel"] = [int(v.numel()) for v in sd.values()]
+    else:
+        for (k, v), sm in zip(sd.items(), sums):
+            arrays["sdsum." + k] = sm
+            arrays["sdhead." + k] = v.detach().flatten()[:8].clone()
     _save(name, meta, arrays)
 
 
@@ -524,8 +536,35 @@ def ar_app_cases():
     case_layer_seeded("nsfar_d96_k32_h354", rflows.NSF_AR, dict(dim=96, K=32, B=B, hidden_dim=354), x)
 
 
+def ar_fe_cases():
+    """NSF_AR at the Fe configs' shape (applications/input/Fe_100K.yaml:8,18-20;
+    Fe_400K / Fe_700K the same): nparticles 54 x dim 3 (config.py:14) = 162
+    coordinates (setup.py:48), nsplines 32, hidden_dim 354, B = ncellx *
+    cell_len / 2 = 3 * 2.8841 / 2 (setup.py:44-45), at the configs' training
+    batch of 50 rows (Fe_*.yaml batch_size)."""
+    B = 3 * 2.8841 / 2
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(50, 162, generator=g) * (0.6 * B)
+    case_layer_seeded("nsfar_d162_k32_h354", rflows.NSF_AR, dict(dim=162, K=32, B=B, hidden_dim=354), x)
+
+
+def ar_polymer_cases():
+    """NSF_AR at Polymer.yaml's shape (applications/input/Polymer.yaml:8-9,
+    17-18): nparticles 2048 x dim 1 = 2048 coordinates, nsplines 32,
+    hidden_dim commented out (:21) so config.py:40's 100, B = ncellx *
+    cell_len / 2 = 0.5, at the config's 40-row batch.  2,047 conditioners
+    FCNN(2i, 95, 100): 0.42 G weights, rebuilt from the seed."""
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(40, 2048, generator=g) * 0.3
+    case_layer_seeded("nsfar_d2048_k32_h100", rflows.NSF_AR, dict(dim=2048, K=32, B=0.5, hidden_dim=100), x)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["ar"]:
+    if sys.argv[1:] == ["ar_fe"]:
+        ar_fe_cases()
+    elif sys.argv[1:] == ["ar_polymer"]:
+        ar_polymer_cases()
+    elif sys.argv[1:] == ["ar"]:
         ar_cases()
     elif sys.argv[1:] == ["ar_app"]:
         ar_app_cases()

@@ -33,8 +33,15 @@ def _rebuild_sd(meta, data):
     torch.manual_seed(meta["seed"])
     layer = getattr(nff, meta["type"])(**meta["kwargs"])
     sd = {k: v.detach().clone() for k, v in layer.state_dict().items()}
-    for k, v in sd.items():
-        sums, head = data.pop("sdsum." + k), data.pop("sdhead." + k)
+    packed = "sd_keys" in meta
+    if packed:
+        assert list(sd.keys()) == meta["sd_keys"], "state_dict keys differ from the fixture's"
+        all_sums, all_heads = data.pop("sdsum_all"), data.pop("sdhead_all")
+    for i, (k, v) in enumerate(sd.items()):
+        if packed:
+            sums, head = all_sums[i], all_heads[i][:min(8, v.numel())]
+        else:
+            sums, head = data.pop("sdsum." + k), data.pop("sdhead." + k)
         v64 = v.double().flatten()
         got = torch.stack([v64.sum(), v64.square().sum()])
         if not (torch.equal(v.flatten()[:8], head) and torch.allclose(got, sums, rtol=1e-12, atol=1e-12)):
