@@ -215,6 +215,10 @@ int nfk_trig_features(const float* x, int64_t ldx, float* feat, int64_t ldf, int
  * Supported shapes: nfk_fused_ar_supported() != 0.
  * ------------------------------------------------------------------------- */
 int nfk_fused_ar_supported(int32_t dim, int32_t hidden, int32_t K);
+/* The inverse fused too (NSF_AR.inverse, flows.py:191-209)?  0 for the shapes
+ * only the streamed forward covers (Polymer.yaml's 2048 coordinates): their
+ * inverse runs per column. */
+int nfk_fused_ar_inverse_supported(int32_t dim, int32_t hidden, int32_t K);
 int64_t nfk_fused_ar_pack_elems(int32_t dim, int32_t hidden, int32_t K);
 int nfk_fused_ar_pack(const float* const* weights, const float* init_param, int32_t dim, int32_t hidden,
                       int32_t K, float* pack, nfk_stream_t stream);
@@ -225,7 +229,9 @@ int nfk_fused_ar(const float* x, int64_t ldx, const float* pack, int32_t dim, in
  * GPU splits the conditioners over workgroups (they are independent given x,
  * flows.py:182-189) when workspace holds nfk_fused_ar_workspace() floats (the
  * per-column log|det| terms, summed in column order: results bitwise those of
- * nfk_fused_ar).  A null or short workspace runs unsplit; 0 = none needed. */
+ * nfk_fused_ar).  A null or short workspace runs unsplit; 0 = none needed.
+ * The shapes only the streamed forward covers (nfk_fused_ar_inverse_supported()
+ * == 0) always need it: it also holds their trig operands. */
 int64_t nfk_fused_ar_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch, int32_t inverse);
 int nfk_fused_ar_ws(const float* x, int64_t ldx, const float* pack, int32_t dim, int32_t hidden, int32_t K,
                     double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,

@@ -62,6 +62,7 @@ SIGNATURES = {
     "nfk_normal_logprob": (ctypes.c_int, [P, I64, P, P, I64, I32, F32, F32, I32, P, P]),
     "nfk_trig_features": (ctypes.c_int, [P, I64, P, I64, I64, I32, F64, P]),
     "nfk_fused_ar_supported": (ctypes.c_int, [I32, I32, I32]),
+    "nfk_fused_ar_inverse_supported": (ctypes.c_int, [I32, I32, I32]),
     "nfk_fused_ar_pack_elems": (ctypes.c_int64, [I32, I32, I32]),
     "nfk_fused_ar_pack": (ctypes.c_int, [P, P, I32, I32, I32, P, P]),
     "nfk_fused_ar": (ctypes.c_int, [

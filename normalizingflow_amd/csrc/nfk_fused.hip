@@ -7,9 +7,11 @@
 // computed transposed, h^T[feature][sample] = W . act^T:
 //   A operand = weights (from an LDS slot), B operand = activations (registers),
 //   D: lane l, register r = output row 4*(l>>4)+r of sample l&15.
-// Layer 1 (inputs x, any magnitude) runs on v_mfma_f32_16x16x4_f32, an exact
-// fp32 fma chain.  Layer 2 and the output layer run as a two-way fp16 split on
-// v_mfma_f32_16x16x32_f16: v = hi + lo with hi = f16(v), lo = f16(v - hi)
+// Every layer runs as a two-way fp16 split on v_mfma_f32_16x16x32_f16 (layer
+// 1 too, since round 4: x, of any magnitude, is first scaled per SAMPLE by a
+// power of two 2^(14 - e), e from the max |x| over that sample's lower
+// coordinates, clamped at e >= -64, the accumulators unscaled by the same
+// factor): v = hi + lo with hi = f16(v), lo = f16(v - hi)
 // (22 significant bits), product = lo.hi + hi.lo + hi.hi accumulated in fp32,
 // dropping lo.lo (2^-22 relative).  Weights are pre-scaled by a power of two
 // so that max|W| lies in [2^14, 2^15) and activations (tanh outputs) by 2^14,

@@ -1148,24 +1148,479 @@ int launch_cl(const ClArgs& a, const ArDims& d, bool inv, hipStream_t st) {
     return e == hipSuccess ? 0 : (int)e;
 }
 
+
+// ---------------------------------------------------------------------------
+// NSF_AR with STREAMED layer-1 operands (k_fused_ar_s, forward): the wide
+// layers the register instances above cannot hold -- Polymer.yaml's 2048
+// coordinates (applications/input/Polymer.yaml:8-9: 2,047 conditioners
+// FCNN(2i, 95, 100), flows.py:165-166, 0.42 G weights per layer).  Conditioner
+// i's layer 1 reads ceil(2i / 32) k-blocks of trig features (up to 128): they
+// are not kept in registers but computed once per launch into a workspace
+// (k_ars_trig, in the MFMA B-operand lane layout, fp16 hi/lo of 2^14 x
+// cos / sin) and streamed through the LDS slots with the weights, two k-blocks
+// per sub-record (layer 1 in k-block-major order: every hidden tile of the
+// k-blocks, then their trig operands for the workgroup's four waves), so each
+// accumulator sees the same products in the same order as the register form
+// (gemm_h: per k-block lo.hi, hi.lo, hi.hi).  Layers 2 and 3 and the spline
+// are the register form's.  Given x the conditioners are independent
+// (flows.py:182-189), so the launch splits them over workgroups: conditioner
+// pairs (p, dim - p), whose layer-1 sizes sum to a constant, in contiguous
+// ranges (balanced weight streams), the XCD-affine grid of the column split;
+// every weight byte is read from HBM once per row block.  Per-column log|det|
+// terms go to the workspace and k_ar_ld_sum adds them in column order
+// (bitwise any partition).  The inverse is sequential through the outputs
+// and stays on the per-column path.
+constexpr int kArsKBS = 2;  // layer-1 k-blocks per sub-record
+constexpr int kArsNW = 4;   // waves per workgroup (16 rows each)
+
+struct ArsDims {
+    ArDims d;
+    int SB2;  // blocks of a layer-2 / output sub-record (the register form's)
+    int TB0;  // first trig block of a layer-1 sub-record in the slot
+    int SBS;  // slot blocks
+    int KB1M;
+};
+
+__host__ __device__ inline ArsDims ars_dims(int hidden, int K, int dim) {
+    ArsDims a{};
+    a.d = ar_dims(hidden, K, dim);
+    a.SB2 = a.d.KBH * a.d.NS * 2 + a.d.NTG + 1;
+    a.TB0 = 1 + kArsKBS * a.d.HT * 2;
+    const int s1 = a.TB0 + kArsKBS * kArsNW * 2;
+    a.SBS = s1 > a.SB2 ? s1 : a.SB2;
+    a.KB1M = a.d.KB1M;
+    return a;
+}
+// sum_{j=1}^{m} ceil(j / 16): layer-1 k-blocks of conditioners 1 .. m
+__host__ __device__ inline int64_t ars_kb_sum(int m) {
+    const int64_t q = m / 16, r = m % 16;
+    return 16 * q * (q + 1) / 2 + r * (q + 1);
+}
+__host__ __device__ inline int ars_kb1(int i) { return (2 * i + 31) / 32; }
+// pack block of conditioner i's stream (block 0 = the header): its bias block,
+// kb1(i) x HT x {hi, lo} layer-1 blocks, then NH + N3 sub-records of SB2 blocks
+__host__ __device__ inline int64_t ars_cond_off(const ArsDims& a, int i) {
+    return 1 + (int64_t)(i - 1) * (1 + (int64_t)(a.d.NH + a.d.N3) * a.SB2) + (int64_t)a.d.HT * 2 * ars_kb_sum(i - 1);
+}
+__host__ __device__ inline int64_t ars_pack_floats(const ArsDims& a, int dim) { return ars_cond_off(a, dim) * 256; }
+inline int64_t ars_trig_floats(const ArsDims& a, int64_t rblocks) { return rblocks * a.KB1M * kArsNW * 2 * 256; }
+__host__ __device__ constexpr int ars_group(int ps) { return ps <= 52 ? 4 : 2; }
+inline size_t ars_lds_bytes(const ArsDims& a, int dim) {
+    return (size_t)2 * a.SBS * 1024 + (size_t)kArsNW * ars_group(a.d.PS) * 16 * a.d.PS * sizeof(float) +
+           (size_t)(dim + 3) / 4 * 16;
+}
+
+// instantiated (KBH, T1, K): Polymer.yaml's conditioners (config.py:40's
+// hidden 100, nsplines 32)
+#define NFK_ARS_SHAPES(X) X(3, 1, 32)
+
+inline bool ars_ok(int dim, int hidden, int K) {
+    if (dim < 2 || dim > 16384 || hidden < 1 || K < 2) return false;
+    const ArsDims a = ars_dims(hidden, K, dim);
+    bool inst = false;
+#define NFK_ARS_CHK(h, t, k) inst |= (a.d.KBH == h && a.d.T1 == t && K == k);
+    NFK_ARS_SHAPES(NFK_ARS_CHK)
+#undef NFK_ARS_CHK
+    return inst && ars_lds_bytes(a, dim) <= (size_t)kLdsBytes;
+}
+
+__global__ __launch_bounds__(256) void k_ars_pack(ArPackArgs a) {
+    const ArsDims A = ars_dims(a.H, a.K, a.dim);
+    const ArDims& d = A.d;
+    const int i = 1 + (int)blockIdx.y;  // conditioner
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+    const unsigned int* hdr = reinterpret_cast<const unsigned int*>(a.out);
+    const int s1 = ar_scale_exp(__uint_as_float(hdr[0])), s2 = ar_scale_exp(__uint_as_float(hdr[1])),
+              s3 = ar_scale_exp(__uint_as_float(hdr[2]));
+    if (i == 1 && blockIdx.x == 0) {  // the header block
+        for (int g = threadIdx.x; g < 256; g += blockDim.x) {
+            if (g == 3) out[g] = __float_as_uint(ldexpf(1.0f, -(s1 + 14)));
+            else if (g == 4) out[g] = __float_as_uint(ldexpf(1.0f, -(s2 + 14)));
+            else if (g == 5) out[g] = __float_as_uint(ldexpf(1.0f, -(s3 + 14)));
+            else if (g >= 8 && g < 8 + d.P) out[g] = __float_as_uint(a.init[g - 8]);
+            else if (g >= 6) out[g] = 0u;
+        }
+    }
+    const int H = a.H, kbh = d.KBH, HT = d.HT, kb1 = ars_kb1(i);
+    const float* const* pw = a.w + (int64_t)(i - 1) * 6;
+    const float *W1 = pw[0], *b1 = pw[1], *W2 = pw[2], *b2 = pw[3], *W3 = pw[4], *b3 = pw[5];
+    auto hid = [&](int t, int r) { return (d.T1 == 2 && t == 2 * kbh) ? 32 * kbh + r : hid_feature(t, r, kbh); };
+    const int64_t base = ars_cond_off(A, i) * 256;
+    const int64_t l1w = (int64_t)(1 + kb1 * HT * 2) * 256;
+    const int64_t nw = l1w + (int64_t)(d.NH + d.N3) * A.SB2 * 256;
+    const float sc1 = ldexpf(1.0f, s1), bsc1 = ldexpf(1.0f, s1 + 14);
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const int blk = (int)(w >> 8), wl = (int)(w & 255);
+        uint32_t v;
+        if (blk == 0) {  // layer-1 bias block [tile][row]
+            const int tt = wl >> 4, r = wl & 15;
+            const int f = tt < HT ? hid(tt, r) : H;
+            v = __float_as_uint(f < H ? b1[f] * bsc1 : 0.0f);
+        } else if (w < l1w) {  // layer 1, k-block-major: (kb, tile, {hi, lo}), canonical trig order
+            const int e = blk - 1, part = e & 1, t = (e >> 1) % HT, kb = (e >> 1) / HT;
+            const int lane = wl >> 2, j = 2 * (wl & 3), k0 = 32 * kb + 8 * (lane >> 4) + j, f = hid(t, lane & 15);
+            auto val = [&](int k) -> float {
+                if (f >= H || k >= 2 * i) return 0.0f;
+                return W1[(int64_t)f * 2 * i + (k & 1) * i + (k >> 1)] * sc1;  // cat(cos, sin) columns
+            };
+            v = nfk_f16_part_pair(val(k0), val(k0 + 1), part);
+        } else {
+            const int rel = (int)((w - l1w) >> 8), sub = rel / A.SB2, b = rel - sub * A.SB2;
+            if (sub < d.NH) {  // layer 2: Linear(H, H)
+                v = ar_sub_word(
+                    d.NS, b, wl, kbh, d.T1, d.HT, d.NS * sub, ldexpf(1.0f, s2), ldexpf(1.0f, s2 + 14),
+                    [&](int t, int r, int k) -> float {
+                        const int f = hid(t, r);
+                        return (f < H && k < H) ? W2[(int64_t)f * H + k] : 0.0f;
+                    },
+                    [&](int t, int r) -> float {
+                        const int f = hid(t, r);
+                        return f < H ? b2[f] : 0.0f;
+                    });
+            } else {  // output layer: Linear(H, 3K-1)
+                const int P = d.P;
+                v = ar_sub_word(
+                    d.NS, b, wl, kbh, d.T1, d.NO, d.NS * (sub - d.NH), ldexpf(1.0f, s3), ldexpf(1.0f, s3 + 14),
+                    [&](int t, int r, int k) -> float {
+                        const int p = 16 * t + r;
+                        return (p < P && k < H) ? W3[(int64_t)p * H + k] : 0.0f;
+                    },
+                    [&](int t, int r) -> float {
+                        const int p = 16 * t + r;
+                        return p < P ? b3[p] : 0.0f;
+                    });
+            }
+        }
+        out[base + w] = v;
+    }
+}
+
+// the trig features of every row block in the MFMA B-operand layout: block
+// ((rb KB1M + kb) NW + w) 2 + {hi, lo}, lane l = (q, sl): features
+// 32 kb + 8 q + j (feature 2c = cos, 2c + 1 = sin of column c < dim - 1) of
+// row (rb NW + w) 16 + sl (rows past the batch repeat the last row, as the
+// register form's brow), x 2^14, fp16 hi and lo
+__global__ __launch_bounds__(256) void k_ars_trig(const float* x, int64_t ldx, float* trig, int64_t batch, int dim,
+                                                  int kb1m, int64_t rblocks, float pi, float bnd) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nrec = rblocks * kb1m * kArsNW;
+    if (g >= nrec * 64) return;
+    const int lane = (int)(g & 63);
+    const int64_t rec = g >> 6;  // (rb, kb, w)
+    const int w = (int)(rec % kArsNW), kb = (int)((rec / kArsNW) % kb1m);
+    const int64_t rb = rec / ((int64_t)kArsNW * kb1m);
+    const int q = lane >> 4, sl = lane & 15;
+    int64_t row = (rb * kArsNW + w) * 16 + sl;
+    row = row < batch ? row : batch - 1;
+    h8 hi, lo;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int col = 16 * kb + 4 * q + t;
+        _Float16 ch = 0, cl = 0, sh = 0, s2 = 0;
+        if (col < dim - 1) trig_split(x[row * ldx + col], pi, bnd, ch, cl, sh, s2);
+        hi[2 * t] = ch;
+        hi[2 * t + 1] = sh;
+        lo[2 * t] = cl;
+        lo[2 * t + 1] = s2;
+    }
+    float4* dst = reinterpret_cast<float4*>(trig + rec * 2 * 256);
+    dst[lane] = __builtin_bit_cast(float4, hi);
+    dst[64 + lane] = __builtin_bit_cast(float4, lo);
+}
+
+struct ArsArgs {
+    const float* x;
+    const float* pack;
+    const float* trig;
+    float* out;
+    float* ld_cols;   // [dim][batch] per-column log|det| terms
+    int32_t* status;  // [dim] or null
+    int64_t ldx, ldo, batch, rblocks;
+    int32_t dim, sbs, kb1m, csplit, npair;
+    NfkSplineConst c;
+};
+
+template <int KBH, int TK, int K>
+__global__ __launch_bounds__(64 * kArsNW, 1) void k_fused_ar_s(ArsArgs a) {
+    constexpr int NW = kArsNW;
+    constexpr bool T1 = TK == 1;
+    static_assert(TK != 2, "16-feature tails: not instanced for the streamed form");
+    constexpr int HT = 2 * KBH + (TK ? 1 : 0), P = 3 * K - 1, NO = (P + 15) / 16;
+    constexpr int NS = ar_ns_for(KBH);
+    constexpr int NH = (HT + NS - 1) / NS, N3 = (NO + NS - 1) / NS;
+    constexpr int NTG = TK == 1 ? (NS + 1) / 2 : 0;
+    constexpr int SB2 = KBH * NS * 2 + NTG + 1;
+    constexpr int TB0 = 1 + kArsKBS * HT * 2;
+    constexpr int PS = 16 * NO + 4, G = ars_group(PS);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4, sl = lane & 15;
+    const int D = a.dim;
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    float4* const slot0 = lds4;
+    float4* const slot1 = lds4 + a.sbs * 64;
+    float* const scr = reinterpret_cast<float*>(lds4 + 2 * a.sbs * 64) + wid * (G * 16 * PS);
+    int* const cst = reinterpret_cast<int*>(reinterpret_cast<float*>(lds4 + 2 * a.sbs * 64) + NW * G * 16 * PS);
+    // XCD-affine grid (k_fused_ar): the row blocks of one conditioner range share an XCD
+    const int64_t v = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    if (v >= a.rblocks * a.csplit) return;  // padding workgroup (uniform: before any barrier)
+    const int sp = (int)(v / a.rblocks);
+    const int64_t rbk = v - (int64_t)sp * a.rblocks;
+    const int p_lo = 1 + (int)(((int64_t)sp * a.npair) / a.csplit), p_hi = 1 + (int)(((int64_t)(sp + 1) * a.npair) / a.csplit);
+    const int64_t b0 = (rbk * NW + wid) * 16;
+    const bool row_ok = b0 + sl < a.batch;
+    const int64_t brow = row_ok ? b0 + sl : a.batch - 1;
+    // the conditioners of pair p: p, then dim - p (one when they coincide)
+    auto cond_of = [&](int p, int m) { return m == 0 ? p : D - p; };
+    auto members = [&](int p) { return D - p != p ? 2 : 1; };
+
+    // sub-record cursor in stream order: pair st_p, member st_m, part st_u
+    // (layer-1 parts 0 .. NU1 - 1, then NH layer-2 and N3 output parts)
+    int st_p = p_lo, st_m = 0, st_u = 0, st_n = 0;
+    const ArsDims AD = ars_dims(32 * KBH + (TK == 1 ? 4 : 0), K, D);  // (only the block offsets are used)
+    auto stage_next = [&]() {
+        if (st_p >= p_hi) return;
+        const int i = cond_of(st_p, st_m), kb1 = ars_kb1(i), nu1 = (kb1 + kArsKBS - 1) / kArsKBS;
+        float4* const dst = (st_n & 1) ? slot1 : slot0;
+        const float* cb = a.pack + ars_cond_off(AD, i) * 256;
+        const uint32_t base = lds_addr(dst);
+        if (st_u < nu1) {
+            const int kb0 = st_u * kArsKBS, nk = kb1 - kb0 < kArsKBS ? kb1 - kb0 : kArsKBS;
+            // weights (with the bias block in front of part 0), then the trig operands
+            const int wb0 = st_u == 0 ? 0 : 1, nwb = (st_u == 0 ? 1 : 0) + nk * HT * 2;
+            const float* wsrc = cb + (int64_t)(st_u == 0 ? 0 : 1 + kb0 * HT * 2) * 256;
+            for (int b = wid; b < nwb; b += NW) dma_blk(wsrc + (int64_t)b * 256, lane, base + (wb0 + b) * 1024);
+            const float* tsrc = a.trig + ((rbk * a.kb1m + kb0) * NW) * 2 * 256;
+            for (int b = wid; b < nk * NW * 2; b += NW) dma_blk(tsrc + (int64_t)b * 256, lane, base + (TB0 + b) * 1024);
+        } else {
+            const int k = st_u - nu1;
+            const float* src = cb + (int64_t)(1 + kb1 * HT * 2 + k * SB2) * 256;
+            for (int b = wid; b < SB2; b += NW) dma_blk(src + (int64_t)b * 256, lane, base + b * 1024);
+        }
+        ++st_n;
+        if (++st_u == nu1 + NH + N3) {
+            st_u = 0;
+            if (++st_m == members(st_p)) {
+                st_m = 0;
+                ++st_p;
+            }
+        }
+    };
+
+    // ---- prologue: status words, the first two sub-records
+    for (int i = threadIdx.x; i < D; i += 64 * NW) cst[i] = 0;
+    const float un1 = a.pack[3], un2 = a.pack[4], un3 = a.pack[5];
+    stage_next();
+    stage_next();
+    dma_barrier();
+
+    int64_t s = 0;  // sub-records consumed
+    auto slot = [&]() -> const float4* { return (s & 1) ? slot1 : slot0; };
+    auto end = [&]() {
+        gemm_fence();
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stage_next();
+        ++s;
+    };
+    const float c21 = -2.0f * kL2E * un1, c22 = -2.0f * kL2E * un2;
+    h8 bh[KBH], bl[KBH];
+    h4 btail = h4{0, 0, 0, 0};
+    int cols[G];   // the slabs' columns (uniform)
+    int nc = 0;    // slabs filled
+    bool any = false;
+
+    // the spline pass over the nc filled slabs: lane group g < nc takes column cols[g]
+    auto spline_pass = [&]() {
+        const bool act = q < nc;
+        const int col = cols[q < nc ? q : 0];
+        const float xin = a.x[brow * a.ldx + col];
+        float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
+        const float* row = scr + (q < nc ? q : 0) * 16 * PS + sl * PS;
+#pragma unroll
+        for (int p = 0; p < K; ++p) wr[p] = row[p];
+#pragma unroll
+        for (int p = 0; p < K; ++p) hr[p] = row[K + p];
+#pragma unroll
+        for (int p = 0; p < K - 1; ++p) dr[p] = row[2 * K + p];
+        float out, lad;
+        bool inside, nd;
+        nfk_rqs_element_lean<K, false>(xin, wr, hr, dr, a.c, out, lad, inside, nd);
+        const bool live = act && row_ok;
+        if (live) {
+            a.out[(b0 + sl) * a.ldo + col] = out;
+            a.ld_cols[(int64_t)col * a.batch + b0 + sl] = lad;
+        }
+        const uint64_t m_in = __ballot(live && inside), m_nd = __ballot(live && inside && nd);
+        if (lane == 0) {
+            for (int g = 0; g < nc; ++g) {
+                const int bits = (((m_in >> (16 * g)) & 0xFFFFull) ? NFK_ST_INSIDE_SEEN : 0) |
+                                 (((m_nd >> (16 * g)) & 0xFFFFull) ? NFK_ST_NEG_DISC : 0);
+                if (bits) atomicOr(cst + cols[g], bits);
+            }
+        }
+        nc = 0;
+    };
+
+    // column 0: init_param (flows.py:178-180), by the first range
+    if (sp == 0) {
+        for (int e = lane; e < 16 * P; e += 64) {
+            const int r = e / P;
+            scr[r * PS + (e - r * P)] = a.pack[8 + (e - r * P)];
+        }
+        cols[0] = 0;
+        nc = 1;
+        any = true;
+    }
+    for (int p = p_lo; p < p_hi; ++p) {
+        for (int m = 0; m < members(p); ++m) {
+            const int i = cond_of(p, m), kb1 = ars_kb1(i);
+            f32x4 h[HT];
+            // ---- layer 1, k-block-major over the streamed sub-records
+            for (int kb0 = 0; kb0 < kb1; kb0 += kArsKBS) {
+                const float4* sl4 = slot();
+                if (kb0 == 0) {
+#pragma unroll
+                    for (int t = 0; t < HT; ++t) h[t] = as_f32x4(sl4[t * 4 + q]);
+                }
+                const int nk = kb1 - kb0 < kArsKBS ? kb1 - kb0 : kArsKBS;
+                for (int kl = 0; kl < nk; ++kl) {
+                    h8 th = __builtin_bit_cast(h8, sl4[(TB0 + (kl * NW + wid) * 2) * 64 + lane]);
+                    h8 tl = __builtin_bit_cast(h8, sl4[(TB0 + (kl * NW + wid) * 2 + 1) * 64 + lane]);
+                    if (kb0 + kl == kb1 - 1) {  // the k-block past feature 2i: masked (x[:, :i])
+                        const int lim = 2 * i - 32 * (kb1 - 1) - 8 * q;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            th[j] = j < lim ? th[j] : (_Float16)0.0f;
+                            tl[j] = j < lim ? tl[j] : (_Float16)0.0f;
+                        }
+                    }
+#pragma unroll
+                    for (int t = 0; t < HT; ++t) {
+                        const h8 ahi = __builtin_bit_cast(h8, sl4[(1 + (kl * HT + t) * 2) * 64 + lane]);
+                        const h8 alo = __builtin_bit_cast(h8, sl4[(1 + (kl * HT + t) * 2 + 1) * 64 + lane]);
+                        h[t] = mfma16(alo, th, h[t]);
+                        h[t] = mfma16(ahi, tl, h[t]);
+                        h[t] = mfma16(ahi, th, h[t]);
+                    }
+                }
+                mfma_result_wait();
+                end();
+            }
+            act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
+            {
+                f32x4 h2[HT];
+                ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+                act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
+            }
+            f32x4 o[NO];
+            ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+            float* const slab = scr + nc * 16 * PS;
+#pragma unroll
+            for (int t = 0; t < NO; ++t) {
+                const int pp = 16 * t + 4 * q;
+                if (pp < PS - 3)
+                    *reinterpret_cast<float4*>(slab + sl * PS + pp) =
+                        make_float4(o[t][0] * un3, o[t][1] * un3, o[t][2] * un3, o[t][3] * un3);
+            }
+            cols[nc++] = i;
+            any = true;
+            if (nc == G) spline_pass();
+        }
+    }
+    if (nc > 0) spline_pass();
+    __syncthreads();
+    if (a.status != nullptr && any) {
+        for (int i = threadIdx.x; i < D; i += 64 * NW) {
+            const int bits = cst[i];
+            if (bits != 0 && (a.status[i] & bits) != bits) atomicOr(a.status + i, bits);
+        }
+    }
+}
+
+// conditioner-pair ranges of a launch: enough workgroups for every CU (one
+// per CU), at most one pair each
+inline int ars_csplit(int npair, int64_t rblocks) {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int64_t cs = rblocks >= cus ? 1 : (cus + rblocks - 1) / rblocks;
+    return (int)(cs < npair ? cs : npair);
+}
+
+template <int KBH, int T1, int K>
+int launch_ars(ArsArgs a, const ArsDims& ad, float* logdet, int mode, float pi, float bnd, hipStream_t st) {
+    const int64_t ntrig = a.rblocks * a.kb1m * kArsNW * 64;
+    hipLaunchKernelGGL(k_ars_trig, dim3((unsigned)((ntrig + 255) / 256)), dim3(256), 0, st, a.x, a.ldx,
+                       const_cast<float*>(a.trig), a.batch, a.dim, a.kb1m, a.rblocks, pi, bnd);
+    const size_t lds = ars_lds_bytes(ad, a.dim);
+    const int64_t nblk = (a.rblocks * a.csplit + 7) / 8 * 8;
+    hipLaunchKernelGGL((k_fused_ar_s<KBH, T1, K>), dim3((unsigned)nblk), dim3(64 * kArsNW), lds, st, a);
+    if (mode != 0)
+        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, a.ld_cols, logdet,
+                           a.batch, a.dim, mode);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
 }  // namespace
 
-extern "C" int nfk_fused_ar_supported(int32_t dim, int32_t hidden, int32_t K) { return ar_ok(dim, hidden, K) ? 1 : 0; }
+// the streamed form (k_fused_ar_s) for shapes beyond the register instances;
+// NFK_AR_STREAM=1 or nfk_debug_ar_stream(1) (diagnostic) selects it for every
+// shape it has, so it can be checked bitwise against the register form
+static int g_ar_stream = -1;
+static bool ar_use_stream(int dim, int hidden, int K) {
+    static const bool env = [] {
+        const char* e = std::getenv("NFK_AR_STREAM");
+        return e != nullptr && e[0] == '1';
+    }();
+    if (!ars_ok(dim, hidden, K)) return false;
+    const bool force = g_ar_stream < 0 ? env : g_ar_stream == 1;
+    return force || !ar_ok(dim, hidden, K);
+}
+
+// Diagnostic: -1 automatic, 1 = the streamed form wherever it is instanced
+// (packs built before a change must be rebuilt).  Returns the previous
+// setting.  Not part of include/nfk.h.
+extern "C" int nfk_debug_ar_stream(int on) {
+    const int prev = g_ar_stream;
+    g_ar_stream = on < 0 ? -1 : (on ? 1 : 0);
+    return prev;
+}
+
+extern "C" int nfk_fused_ar_supported(int32_t dim, int32_t hidden, int32_t K) {
+    return (ar_ok(dim, hidden, K) || ars_ok(dim, hidden, K)) ? 1 : 0;
+}
+
+extern "C" int nfk_fused_ar_inverse_supported(int32_t dim, int32_t hidden, int32_t K) {
+    return (ar_ok(dim, hidden, K) && !ar_use_stream(dim, hidden, K)) ? 1 : 0;
+}
 
 extern "C" int64_t nfk_fused_ar_pack_elems(int32_t dim, int32_t hidden, int32_t K) {
+    if (ar_use_stream(dim, hidden, K)) return ars_pack_floats(ars_dims(hidden, K, dim), dim);
     if (!ar_ok(dim, hidden, K)) return 0;
     return ar_pack_floats(ar_dims(hidden, K, dim), dim);
 }
 
 extern "C" int nfk_fused_ar_pack(const float* const* weights, const float* init_param, int32_t dim,
                                  int32_t hidden, int32_t K, float* pack, nfk_stream_t stream) {
-    if (!ar_ok(dim, hidden, K)) return nfk_set_error("nfk_fused_ar_pack: shape not supported");
+    const bool strm = ar_use_stream(dim, hidden, K);
+    if (!strm && !ar_ok(dim, hidden, K)) return nfk_set_error("nfk_fused_ar_pack: shape not supported");
     if (!weights || !init_param || !pack) return nfk_set_error("nfk_fused_ar_pack: null pointer");
     ArPackArgs a{weights, init_param, pack, dim, hidden, K, ar_dims(hidden, K, dim)};
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(pack, 0, 3 * sizeof(float), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_ar_max, dim3(16, (unsigned)(dim - 1)), dim3(256), 0, st, a);
+    if (strm) {  // conditioner by conditioner (grid y), the streamed layout
+        hipLaunchKernelGGL(k_ars_pack, dim3(16, (unsigned)(dim - 1)), dim3(256), 0, st, a);
+        e = hipGetLastError();
+        return e == hipSuccess ? 0 : (int)e;
+    }
     int64_t g = (ar_pack_floats(a.d, dim) + 255) / 256;
     if (g > 16384) g = 16384;
     hipLaunchKernelGGL(k_ar_pack, dim3((unsigned)g), dim3(256), 0, st, a);
@@ -1174,7 +1629,13 @@ extern "C" int nfk_fused_ar_pack(const float* const* weights, const float* init_
 }
 
 extern "C" int64_t nfk_fused_ar_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch, int32_t inverse) {
-    if (!ar_ok(dim, hidden, K) || batch <= 0) return 0;
+    if (batch <= 0) return 0;
+    if (ar_use_stream(dim, hidden, K)) {
+        if (inverse) return 0;
+        const ArsDims ad = ars_dims(hidden, K, dim);
+        return (int64_t)dim * batch + ars_trig_floats(ad, (batch + 16 * kArsNW - 1) / (16 * kArsNW));
+    }
+    if (!ar_ok(dim, hidden, K)) return 0;
     return ar_csplit(ar_dims(hidden, K, dim), dim, batch, inverse != 0) > 1 ? (int64_t)dim * batch : 0;
 }
 
@@ -1189,12 +1650,45 @@ extern "C" int nfk_fused_ar_ws(const float* x, int64_t ldx, const float* pack, i
                                double tail_bound, float* out, int64_t ldo, float* logdet, int32_t logdet_mode,
                                int64_t batch, int32_t inverse, int32_t* status, float* workspace,
                                int64_t workspace_floats, nfk_stream_t stream) {
-    if (!ar_ok(dim, hidden, K)) return nfk_set_error("nfk_fused_ar: shape not supported");
+    const bool strm = ar_use_stream(dim, hidden, K);
+    if (!strm && !ar_ok(dim, hidden, K)) return nfk_set_error("nfk_fused_ar: shape not supported");
     if (batch < 0) return nfk_set_error("nfk_fused_ar: bad batch");
     if (batch == 0) return 0;
     if (!x || !pack || !out) return nfk_set_error("nfk_fused_ar: null pointer");
     if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_fused_ar: null logdet");
     if (ldx < dim || ldo < dim) return nfk_set_error("nfk_fused_ar: bad leading dimension");
+    if (strm) {
+        if (inverse) return nfk_set_error("nfk_fused_ar: the inverse of this shape is not fused "
+                                          "(nfk_fused_ar_inverse_supported)");
+        const ArsDims ad = ars_dims(hidden, K, dim);
+        ArsArgs s;
+        s.rblocks = (batch + 16 * kArsNW - 1) / (16 * kArsNW);
+        const int64_t need = (int64_t)dim * batch + ars_trig_floats(ad, s.rblocks);
+        if (workspace == nullptr || workspace_floats < need)
+            return nfk_set_error("nfk_fused_ar: this shape needs nfk_fused_ar_workspace() floats of workspace");
+        s.x = x;
+        s.pack = pack;
+        s.ld_cols = workspace;
+        s.trig = workspace + (int64_t)dim * batch;
+        s.out = out;
+        s.status = status;
+        s.ldx = ldx;
+        s.ldo = ldo;
+        s.batch = batch;
+        s.dim = dim;
+        s.sbs = ad.SBS;
+        s.kb1m = ad.KB1M;
+        s.npair = dim / 2;
+        s.csplit = ars_csplit(s.npair, s.rblocks);
+        s.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+        hipStream_t st = (hipStream_t)stream;
+#define NFK_ARS_LAUNCH(h, t, k) \
+    if (ad.d.KBH == h && ad.d.T1 == t && K == k) \
+        return launch_ars<h, t, k>(s, ad, logdet, logdet_mode, (float)M_PI, (float)tail_bound, st);
+        NFK_ARS_SHAPES(NFK_ARS_LAUNCH)
+#undef NFK_ARS_LAUNCH
+        return nfk_set_error("nfk_fused_ar: no kernel instance");
+    }
     const ArDims d = ar_dims(hidden, K, dim);
     ArArgs a;
     a.x = x;

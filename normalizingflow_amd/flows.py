@@ -812,6 +812,8 @@ class NSF_AR(_HipFlow):
             raise RuntimeError("NSF_AR(dim=%d) got %d features" % (self.dim, x.shape[1]))
         n = x.shape[0]
         pack = self._fused_pack(x.device)
+        if pack is not None and inverse and not K_.fused_ar_inverse_supported(self.dim, self._pack_cache[2], self.K):
+            pack = None  # (a streamed-forward shape: the inverse runs per column)
         if pack is not None:
             z = torch.empty_like(x, memory_format=torch.contiguous_format)
             K_.fused_ar(x, pack, self.dim, self._pack_cache[2], self.K, float(self.B), z, logdet=logdet,
@@ -852,6 +854,7 @@ class NSF_AR(_HipFlow):
             # logits, their gradient and its transposed copy (3 P), the expanded
             # trig features bmm materialises and the feature-gradient product (4 n)
             per = 4 * n * x.shape[0] * (8 * H + 3 * P + 4 * n)
+            per += 2 * 4 * n * H * 2 * n  # the zero-padded first-Linear stack and its gradient
             if all(m.out_features == H for m in lin[0::3]) and per <= config.AR_BATCHED_VJP_BYTES:
                 return self._vjp_batched(x, names, params, gz, gld, need, H)
         p = {n: t.detach() for n, t in zip(names, params)}

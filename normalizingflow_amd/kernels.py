@@ -477,6 +477,12 @@ def fused_ar_supported(dim, hidden, K):
     return bool(_lib.load().nfk_fused_ar_supported(dim, hidden, K))
 
 
+def fused_ar_inverse_supported(dim, hidden, K):
+    """False for the shapes only the streamed forward covers (their inverse,
+    sequential through the outputs, runs per column)."""
+    return bool(_lib.load().nfk_fused_ar_inverse_supported(dim, hidden, K))
+
+
 def fused_ar_pack(weights, init_param, dim, hidden, K):
     """The fused NSF_AR pack from the conditioners' Linear parameters:
     ``weights`` = [(W1, b1, W2, b2, W3, b3) for conditioner 1 .. dim-1].

@@ -312,3 +312,84 @@ def test_polymer2048_vs_reference_golden(hip_device):
         close(xa, data["inv_x"], 1e-5, 1e-4)
         close(lda, data["inv_ld"], 1e-5, 2e-3)
     flush_status_checks()
+
+
+@pytest.mark.parametrize("dim,rows", [(96, 40), (96, 333), (64, 1000), (23, 64)])
+def test_streamed_ar_bitwise_vs_register_form(dim, rows, hip_device):
+    """The streamed-layer-1 forward (k_fused_ar_s: the trig operands and the
+    layer-1 weights through the LDS slots, k-block-major; the Polymer form)
+    forced on shapes the register form also covers (config.py's hidden 100,
+    nsplines 32): z, log|det| (modes 1, 2) and the status words bitwise those
+    of the register form -- the same products in the same order."""
+    lib = K_._lib.load()
+    torch.manual_seed(dim + rows)
+    layer = nff.NSF_AR(dim=dim, K=32, B=1.5, hidden_dim=100).to(hip_device)
+    x = torch.randn(rows, dim, device=hip_device)
+    x[0, dim // 3] = 40.0  # one element outside [-B, B]: the identity tail
+    res = []
+    for force in (0, 1):
+        prev = lib.nfk_debug_ar_stream(force)
+        try:
+            layer.invalidate_caches()
+            pack = layer._fused_pack(x.device)
+            assert pack is not None
+            assert K_.fused_ar_inverse_supported(dim, 100, 32) == (force == 0)
+            z = torch.empty_like(x)
+            ld1 = torch.full((rows,), 7.0, device=hip_device)
+            ld2 = torch.linspace(-3.0, 3.0, rows, device=hip_device)
+            st = torch.zeros(dim, dtype=torch.int32, device=hip_device)
+            K_.fused_ar(x, pack, dim, 100, 32, 1.5, z, logdet=ld1, logdet_mode=1, status=st)
+            z2 = torch.empty_like(x)
+            K_.fused_ar(x, pack, dim, 100, 32, 1.5, z2, logdet=ld2, logdet_mode=2)
+            torch.cuda.synchronize()
+            assert torch.equal(z, z2)
+            res.append((z, ld1, ld2, st))
+        finally:
+            lib.nfk_debug_ar_stream(prev)
+            layer.invalidate_caches()
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+
+
+def test_polymer2048_forward_one_launch_and_speed(hip_device):
+    """Polymer.yaml's layer at its 40-row batch: the forward is ONE streamed
+    launch (plus the trig pre-pass and the column-order log|det| sum), matches
+    the oracle, and is far faster than the per-column path (2,047 conditioners
+    x ~8 launches)."""
+    import time
+    torch.manual_seed(2048)
+    layer = nff.NSF_AR(dim=2048, K=32, B=0.5, hidden_dim=100)
+    sd = _sd(layer)
+    layer = layer.to(hip_device)
+    x = torch.randn(40, 2048, generator=torch.Generator().manual_seed(5)) * 0.3
+    xd = x.to(hip_device)
+    assert K_.fused_ar_supported(2048, 100, 32) and not K_.fused_ar_inverse_supported(2048, 100, 32)
+    with torch.no_grad():
+        (z, ld), n = _launches(lambda: layer(xd))
+        assert n == {"nfk_fused_ar": 1}, n
+        z_ref, ld_ref = orc.nsf_ar(x, sd, "", 2048, 32, 0.5)
+        close(z, z_ref, Z_RTOL, Z_ATOL)
+        close(ld, ld_ref, LD_RTOL, 2e-3)
+
+        def timed(fn, reps):
+            fn()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps
+
+        t_fused = timed(lambda: layer(xd), 10)
+        prev = config.USE_FUSED
+        config.USE_FUSED = False
+        try:
+            layer.invalidate_caches()
+            t_col = timed(lambda: layer(xd), 1)
+        finally:
+            config.USE_FUSED = prev
+            layer.invalidate_caches()
+    print("poly2048 forward at 40 rows: fused %.3f ms, per-column %.3f ms (%.1fx)"
+          % (t_fused * 1e3, t_col * 1e3, t_col / t_fused))
+    assert t_col >= 10 * t_fused, (t_fused, t_col)
+    flush_status_checks()

@@ -40,7 +40,11 @@ def test_layer_fixture(name):
     meta, d, sd = gio.load(name)
     spec = gio.layer_spec(meta)
     z, ld = orc.apply_layer(spec, d["x"], sd)
-    _close(z, d["z"]); _close(ld.expand_as(d["ld"]), d["ld"])
+    # NSF_AR's log|det| sums dim fp32 terms whose logits come from library
+    # GEMMs (their blocking, hence rounding, follows the thread count): its
+    # slack grows with dim (the default 2e-6 up to 24 columns)
+    ld_at = AT * max(1.0, meta["kwargs"].get("dim", 0) / 24.0) if meta["type"] == "NSF_AR" else AT
+    _close(z, d["z"]); _close(ld.expand_as(d["ld"]), d["ld"], atol=ld_at)
     if "rt_x" in d:
         # NSF_AR's inverse is sequential (each inverted coordinate conditions the
         # next ones, flows.py:191-209): ulp-level spline differences propagate
