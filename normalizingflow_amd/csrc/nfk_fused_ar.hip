@@ -709,13 +709,31 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
 }
 
 // log|det| of a column-split forward: the per-column terms summed in column
-// order from 0 (bitwise the single-range kernel's ld_acc), then mode 1/2
+// order from 0 (bitwise the single-range kernel's ld_acc), then mode 1/2.
+// A workgroup takes 64 rows: its four waves load 128-column chunks of the
+// [dim][batch] terms into LDS (coalesced over the rows, every load in flight
+// at once), then wave 0 adds each row's chunk in column order.  (One thread
+// per row walking the columns had each add wait for its strided load: 0.78 ms
+// at Polymer's 2048 columns, 36 us at dim 96.)
+constexpr int kLdRows = 64, kLdCols = 128;
 __global__ __launch_bounds__(256) void k_ar_ld_sum(const float* cols, float* logdet, int64_t batch, int dim, int mode) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= batch) return;
+    __shared__ float tile[kLdRows][kLdCols + 1];
+    const int t = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * kLdRows;
+    const int nr = batch - r0 < kLdRows ? (int)(batch - r0) : kLdRows;
     float acc = 0.0f;
-    for (int c = 0; c < dim; ++c) acc = acc + cols[(int64_t)c * batch + r];
-    logdet[r] = mode == 2 ? logdet[r] + acc : acc;
+    for (int c0 = 0; c0 < dim; c0 += kLdCols) {
+        const int nc = dim - c0 < kLdCols ? dim - c0 : kLdCols;
+        for (int e = t; e < kLdCols * kLdRows; e += 256) {
+            const int c = e / kLdRows, r = e - c * kLdRows;
+            if (c < nc && r < nr) tile[r][c] = cols[(int64_t)(c0 + c) * batch + r0 + r];
+        }
+        __syncthreads();
+        if (t < nr)
+            for (int c = 0; c < nc; ++c) acc = acc + tile[t][c];
+        __syncthreads();
+    }
+    if (t < nr) logdet[r0 + t] = mode == 2 ? logdet[r0 + t] + acc : acc;
 }
 
 
@@ -770,7 +788,7 @@ int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
             hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, false, 4>), g, b, lds, st, a);
     }
     if (a.csplit > 1 && a.mode != 0)
-        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, a.ld_cols,
+        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + kLdRows - 1) / kLdRows)), dim3(256), 0, st, a.ld_cols,
                            a.logdet, a.batch, a.dim, a.mode);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -1142,7 +1160,7 @@ int launch_cl(const ClArgs& a, const ArDims& d, bool inv, hipStream_t st) {
     else
         hipLaunchKernelGGL((k_fused_cl<KBH, T1, K, false>), g, b, lds, st, a);
     if (a.csplit > 1 && a.mode != 0)
-        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, a.ld_cols,
+        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + kLdRows - 1) / kLdRows)), dim3(256), 0, st, a.ld_cols,
                            a.logdet, a.batch, a.n_up, a.mode);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -1561,7 +1579,7 @@ int launch_ars(ArsArgs a, const ArsDims& ad, float* logdet, int mode, float pi, 
     const int64_t nblk = (a.rblocks * a.csplit + 7) / 8 * 8;
     hipLaunchKernelGGL((k_fused_ar_s<KBH, T1, K>), dim3((unsigned)nblk), dim3(64 * kArsNW), lds, st, a);
     if (mode != 0)
-        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, a.ld_cols, logdet,
+        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + kLdRows - 1) / kLdRows)), dim3(256), 0, st, a.ld_cols, logdet,
                            a.batch, a.dim, mode);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;

@@ -92,6 +92,17 @@ extern "C" int nfk_vjp_diag_set(float* p) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_vjp_dbg), &p, sizeof(p), 0, hipMemcpyHostToDevice);
 }
 #endif
+#ifdef NFK_VJP_DIAG_TWICE  // diagnostic: per-lane counts of elements whose two evaluations differed
+__device__ int g_vjp_cnt[64];
+extern "C" int nfk_vjp_diag_counts(int* host, int reset) {
+    int rc = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_vjp_cnt), sizeof(g_vjp_cnt), 0, hipMemcpyDeviceToHost);
+    if (reset) {
+        static const int zero[64] = {0};
+        rc |= (int)hipMemcpyToSymbol(HIP_SYMBOL(g_vjp_cnt), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+    }
+    return rc;
+}
+#endif
 
 template <int KBH, bool T1, int K, bool INV>
 __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
@@ -260,11 +271,40 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
                 sv[3 * K] = go;
                 sv[3 * K + 1] = gl;
             }
+#ifdef NFK_VJP_DIAG_RELOAD  // diagnostic: the element backward runs on the values just stored, re-read
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            {
+                volatile const float* rv = g_vjp_dbg + (b * n_up + j) * (3 * K + 2);
+#pragma unroll
+                for (int i = 0; i < K; ++i) wr[i] = rv[i];
+#pragma unroll
+                for (int i = 0; i < K; ++i) hr[i] = rv[K + i];
+#pragma unroll
+                for (int i = 0; i < K - 1; ++i) dr[i] = rv[2 * K + i];
+            }
+#endif
 #endif
 #ifdef NFK_VJP_DUMP  // diagnostic: the element backward's inputs instead of its outputs
             const float gxv = xv + 1000.0f * go + 1.0e6f * gl;
 #else
+#ifdef NFK_VJP_DIAG_TWICE  // diagnostic: the element backward twice on the same registers; mismatches counted
+            float w2[K], h2[K], d2[K - 1];
+#pragma unroll
+            for (int i = 0; i < K; ++i) w2[i] = wr[i], h2[i] = hr[i];
+#pragma unroll
+            for (int i = 0; i < K - 1; ++i) d2[i] = dr[i];
+            const float gx2 = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, w2, h2, d2, cc, go, gl);
+            asm volatile("" ::: "memory");
+#endif
             const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, wr, hr, dr, cc, go, gl);
+#ifdef NFK_VJP_DIAG_TWICE
+            {
+                bool same = __float_as_uint(gx2) == __float_as_uint(gxv);
+#pragma unroll
+                for (int i = 0; i < K; ++i) same = same && __float_as_uint(w2[i]) == __float_as_uint(wr[i]);
+                if (!same && row_ok) atomicAdd(g_vjp_cnt + lane, 1);
+            }
+#endif
 #endif
             if (row_ok) {
                 a.gx[b * a.ldgx + m_up_in[j]] = gxv;

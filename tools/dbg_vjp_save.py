@@ -90,8 +90,17 @@ def main():
             c_gp, c_gx, c_in = run(False)
             print("inv=%d B=%d clean: gp nan %d, inputs nan %d" % (inverse, B, int(torch.isnan(c_gp).sum()),
                                                                     int(torch.isnan(c_in).sum())), flush=True)
+            counts = getattr(lib, "nfk_vjp_diag_counts", None)
+            if counts is not None:
+                counts.argtypes = [ctypes.c_void_p, ctypes.c_int]
+                cbuf = (ctypes.c_int * 64)()
+                counts(ctypes.cast(cbuf, ctypes.c_void_p), 1)
             for rep in range(reps):
                 r_gp, r_gx, r_in = run(True)
+                if counts is not None:
+                    counts(ctypes.cast(cbuf, ctypes.c_void_p), 1)
+                    print("  twice: per-lane mismatches of the two evaluations: total %d, lanes 0-47 %d, "
+                          "48-63 %d" % (sum(cbuf), sum(cbuf[:48]), sum(cbuf[48:])), flush=True)
                 in_diff = (r_in != c_in) & ~(torch.isnan(r_in) & torch.isnan(c_in))
                 out_diff = (r_gp != c_gp) & ~(torch.isnan(r_gp) & torch.isnan(c_gp))
                 el_in = in_diff.any(1)
