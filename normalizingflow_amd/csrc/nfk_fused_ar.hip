@@ -498,12 +498,15 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
     for (int i = threadIdx.x; i < D; i += 64 * kArWaves) cst[i] = 0;
     const float un1 = a.pack[3], un2 = a.pack[4], un3 = a.pack[5];
     h8 th[KBX], tl[KBX];  // layer-1 B operands: features 32 kb + 8 q + j of sample sl
+    // the k-blocks this workgroup's conditioners read (a column range of a
+    // split launch: conditioners < i_hi read features < 2 (i_hi - 1))
+    const int kb_need = i_hi > 1 ? (2 * (i_hi - 1) + 31) / 32 : 0;
 #pragma unroll
     for (int kb = 0; kb < KBX; ++kb) {
         th[kb] = h8{0, 0, 0, 0, 0, 0, 0, 0};
         tl[kb] = th[kb];
         if constexpr (!INV) {
-            if (kb < a.kb1m) {
+            if (kb < kb_need && kb < a.kb1m) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const int col = 16 * kb + 4 * q + t;

@@ -93,11 +93,11 @@ extern "C" int nfk_vjp_diag_set(float* p) {
 }
 #endif
 #ifdef NFK_VJP_DIAG_TWICE  // diagnostic: per-lane counts of elements whose two evaluations differed
-__device__ int g_vjp_cnt[64];
+__device__ int g_vjp_cnt[64 + 80];  // per-lane mismatches, then per first-differing probe slot
 extern "C" int nfk_vjp_diag_counts(int* host, int reset) {
     int rc = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_vjp_cnt), sizeof(g_vjp_cnt), 0, hipMemcpyDeviceToHost);
     if (reset) {
-        static const int zero[64] = {0};
+        static const int zero[64 + 80] = {0};
         rc |= (int)hipMemcpyToSymbol(HIP_SYMBOL(g_vjp_cnt), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
     }
     return rc;
@@ -293,16 +293,37 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_nsf_vjp(VjpArgs a) {
             for (int i = 0; i < K; ++i) w2[i] = wr[i], h2[i] = hr[i];
 #pragma unroll
             for (int i = 0; i < K - 1; ++i) d2[i] = dr[i];
-            const float gx2 = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, w2, h2, d2, cc, go, gl);
+#ifdef NFK_BWD_PROBE
+            float pr1[nfk_bwd::kProbeSlots], pr2[nfk_bwd::kProbeSlots];
+#pragma unroll
+            for (int i = 0; i < nfk_bwd::kProbeSlots; ++i) pr1[i] = pr2[i] = 0.0f;
+#define NFK_PA1 , pr1
+#define NFK_PA2 , pr2
+#else
+#define NFK_PA1
+#define NFK_PA2
+#endif
+            const float gx2 = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, w2, h2, d2, cc, go, gl NFK_PA2);
             asm volatile("" ::: "memory");
 #endif
-            const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, wr, hr, dr, cc, go, gl);
+#ifndef NFK_PA1
+#define NFK_PA1
+#endif
+            const float gxv = nfk_bwd::rqs_element_bwd<K, INV, true, false, NFK_VJP_FAST>(xv, wr, hr, dr, cc, go, gl NFK_PA1);
 #ifdef NFK_VJP_DIAG_TWICE
             {
                 bool same = __float_as_uint(gx2) == __float_as_uint(gxv);
 #pragma unroll
                 for (int i = 0; i < K; ++i) same = same && __float_as_uint(w2[i]) == __float_as_uint(wr[i]);
                 if (!same && row_ok) atomicAdd(g_vjp_cnt + lane, 1);
+#ifdef NFK_BWD_PROBE
+                // the first intermediate (in computation order) where the two evaluations part
+                int first = -1;
+#pragma unroll
+                for (int i = nfk_bwd::kProbeSlots - 1; i >= 0; --i)
+                    first = __float_as_uint(pr1[i]) != __float_as_uint(pr2[i]) ? i : first;
+                if (first >= 0 && row_ok) atomicAdd(g_vjp_cnt + 64 + first, 1);
+#endif
             }
 #endif
 #endif

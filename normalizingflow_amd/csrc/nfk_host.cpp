@@ -1,0 +1,110 @@
+// nfk_host.cpp -- host-side cache validation for the layers with thousands of
+// parameter tensors (CPython extension, CPU only; no device work).
+//
+// A fused layer's weight pack is valid while every parameter keeps its storage
+// and version counter and the conditioner modules are the same objects
+// (normalizingflow_amd/flows.py: the caches are keyed on exactly that).  At
+// Polymer.yaml's NSF_AR (applications/input/Polymer.yaml: 2,047 conditioners,
+// 6,142 parameter tensors per layer) computing that key in Python took ~23 ms
+// per call -- forty times the layer's kernel.  ar_state() walks the same module
+// tree in C++ (~1 ms) and returns a 64-bit hash of it, or -1 when a
+// conditioner is not the stock FCNN (flows.py:20-35).
+#include <torch/csrc/autograd/python_variable.h>
+#include <torch/csrc/utils/pybind.h>
+
+#include <cstdint>
+
+namespace {
+
+struct Hash {
+    uint64_t h = 1469598103934665603ull;
+    void mix(uint64_t v) {
+        h = (h ^ v) * 1099511628211ull;
+        h ^= h >> 29;
+    }
+};
+
+// interned keys (PyDict_GetItemString would build a string object per lookup)
+struct Keys {
+    PyObject *modules, *network, *parameters, *weight, *bias;
+    Keys()
+        : modules(PyUnicode_InternFromString("_modules")), network(PyUnicode_InternFromString("network")),
+          parameters(PyUnicode_InternFromString("_parameters")), weight(PyUnicode_InternFromString("weight")),
+          bias(PyUnicode_InternFromString("bias")) {}
+};
+const Keys& keys() {
+    static const Keys k;
+    return k;
+}
+
+PyObject* inst_dict_item(PyObject* obj, PyObject* key) {
+    PyObject** dp = _PyObject_GetDictPtr(obj);
+    if (dp == nullptr || *dp == nullptr) return nullptr;
+    return PyDict_GetItem(*dp, key);  // borrowed
+}
+
+bool mix_tensor(Hash& h, PyObject* t) {
+    if (t == nullptr || !THPVariable_Check(t)) return false;
+    const at::Tensor& v = THPVariable_Unpack(t);
+    h.mix((uint64_t)(uintptr_t)v.unsafeGetTensorImpl()->data());
+    h.mix((uint64_t)v._version());
+    return true;
+}
+
+// (data_ptr, version) of every tensor of a list
+int64_t fingerprint(py::list ts) {
+    Hash h;
+    for (py::handle o : ts)
+        if (!mix_tensor(h, o.ptr())) throw py::type_error("fingerprint: not a tensor");
+    return (int64_t)h.h;
+}
+
+// NSF_AR's conditioner tree: layers._modules (an ordered dict of FCNN), each
+// FCNN's network._modules = {Linear, Tanh, Linear, Tanh, Linear}; the hash of
+// every module's identity and every Linear's (weight, bias) state, plus
+// init_param's; -1 when the tree is not that shape
+int64_t ar_state(py::handle layers_modules, py::handle init_param, py::handle fcnn_t, py::handle linear_t,
+                 py::handle tanh_t) {
+    Hash h;
+    if (!mix_tensor(h, init_param.ptr())) return -1;
+    PyObject* d = layers_modules.ptr();
+    if (!PyDict_Check(d)) return -1;
+    PyObject *key, *cond;
+    Py_ssize_t pos = 0;
+    PyTypeObject* lin = (PyTypeObject*)linear_t.ptr();
+    PyTypeObject* tnh = (PyTypeObject*)tanh_t.ptr();
+    while (PyDict_Next(d, &pos, &key, &cond)) {
+        if ((PyObject*)Py_TYPE(cond) != fcnn_t.ptr()) return -1;
+        h.mix((uint64_t)(uintptr_t)cond);
+        const Keys& K = keys();
+        PyObject* cm = inst_dict_item(cond, K.modules);
+        PyObject* net = (cm != nullptr && PyDict_Check(cm)) ? PyDict_GetItem(cm, K.network) : nullptr;
+        if (net == nullptr) return -1;
+        h.mix((uint64_t)(uintptr_t)net);
+        PyObject* nm = inst_dict_item(net, K.modules);
+        if (nm == nullptr || !PyDict_Check(nm) || PyDict_Size(nm) != 5) return -1;
+        PyObject *k2, *sub;
+        Py_ssize_t p2 = 0;
+        int idx = 0;
+        while (PyDict_Next(nm, &p2, &k2, &sub)) {
+            const bool want_lin = (idx % 2) == 0;
+            if (!PyObject_TypeCheck(sub, want_lin ? lin : tnh)) return -1;
+            h.mix((uint64_t)(uintptr_t)sub);
+            if (want_lin) {
+                PyObject* pm = inst_dict_item(sub, K.parameters);
+                if (pm == nullptr || !PyDict_Check(pm)) return -1;
+                if (!mix_tensor(h, PyDict_GetItem(pm, K.weight))) return -1;
+                if (!mix_tensor(h, PyDict_GetItem(pm, K.bias))) return -1;
+            }
+            ++idx;
+        }
+    }
+    return (int64_t)(h.h & 0x7fffffffffffffffull);  // (never -1)
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_nfk_host, m) {
+    m.def("fingerprint", &fingerprint);
+    m.def("ar_state", &ar_state);
+}

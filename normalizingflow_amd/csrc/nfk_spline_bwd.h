@@ -8,6 +8,18 @@
 
 namespace nfk_bwd {
 
+// Diagnostic probes (NFK_BWD_PROBE builds only: tools/dbg_vjp_save.py's
+// "probe" variant): rqs_element_bwd stores its intermediates at fixed slots of
+// a caller array so two evaluations can be compared stage by stage.
+#ifdef NFK_BWD_PROBE
+#define NFK_PROBE_PARAM , float* nfk_probe
+#define NFK_PROBE(i, v) (nfk_probe[(i)] = (float)(v))
+#else
+#define NFK_PROBE_PARAM
+#define NFK_PROBE(i, v) ((void)0)
+#endif
+constexpr int kProbeSlots = 80;
+
 // d softplus(v) / dv as torch's softplus_backward (beta 1, threshold 20)
 template <bool FAST = false>
 __device__ __forceinline__ float softplus_grad(float v) {
@@ -104,7 +116,7 @@ __device__ __forceinline__ float sel(const float (&a)[K], int k) { return nfk_se
 template <int K, bool INV, bool PRE, bool DFULL, bool FAST = false>
 __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float (&hr)[K],
                                                  float (&dr)[NfkDN<K, DFULL>::n],
-                                                 const NfkSplineConst& c, float gout, float gl) {
+                                                 const NfkSplineConst& c, float gout, float gl NFK_PROBE_PARAM) {
     constexpr int DN = NfkDN<K, DFULL>::n;
     const bool inside = !c.tails || ((x >= c.lo) && (x <= c.hi));
     if (!inside) {
@@ -118,6 +130,17 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
     W.build(wr, c.scale2b, c.lo, c.hi, c.span, c.min_w, c.fw);
     H.build(hr, c.scale2b, c.ylo, c.yhi, c.yspan, c.min_h, c.fh);
     const int k = nfk_bin<K>(INV ? H.edge : W.edge, x, c.knot_eps);
+#pragma unroll
+    for (int j = 0; j < K && j < 8; ++j) {
+        NFK_PROBE(j, W.s1[j]);
+        NFK_PROBE(17 + j, H.s1[j]);
+    }
+#pragma unroll
+    for (int j = 0; j <= K && j < 9; ++j) {
+        NFK_PROBE(8 + j, W.edge[j]);
+        NFK_PROBE(25 + j, H.edge[j]);
+    }
+    NFK_PROBE(34, k);
     float cw_k = W.edge[0], w_k = W.edge[1] - W.edge[0], ch_k = H.edge[0], h_k = H.edge[1] - H.edge[0];
 #pragma unroll
     for (int j = 1; j < K; ++j) {
@@ -155,6 +178,9 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
     const float d1 = c.min_d + nfk_splus<FAST>(v1);
     const float delta = nfk_div<FAST>(h_k, w_k);
     const float gap = (d0 + d1) - 2.0f * delta;
+    NFK_PROBE(35, d0);
+    NFK_PROBE(36, d1);
+    NFK_PROBE(37, delta);
 
     float th;
     if (INV) {
@@ -189,6 +215,13 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
     const float l_t = M_t * iM - 2.0f * Dn_t * iDn, l_dl = M_dl * iM - 2.0f * Dn_dl * iDn;
     const float l_d0 = M_d0 * iM - 2.0f * Dn_d0 * iDn, l_d1 = M_d1 * iM - 2.0f * Dn_d1 * iDn;
     const float iw = nfk_div<FAST>(1.0f, w_k);
+    NFK_PROBE(38, th);
+    NFK_PROBE(39, Dn);
+    NFK_PROBE(40, N);
+    NFK_PROBE(41, M);
+    NFK_PROBE(42, iDn);
+    NFK_PROBE(43, iM);
+    NFK_PROBE(44, iw);
 
     float a, b, gx;  // g_bin = a * f_bin + b * lad_bin
     if (INV) {
@@ -209,6 +242,10 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
     const float g_h = a * f_h + G_dl * iw;
     const float g_d0 = a * f_d0 + b * l_d0;
     const float g_d1 = a * f_d1 + b * l_d1;
+    NFK_PROBE(45, G_t);
+    NFK_PROBE(46, G_dl);
+    NFK_PROBE(47, g_w);
+    NFK_PROBE(48, g_h);
 
     W.backward(k, g_cw, g_w, c.span, c.fw, c.scale2b, wr);
     H.backward(k, g_ch, g_h, c.yspan, c.fh, c.scale2b, hr);
@@ -225,6 +262,14 @@ __device__ __forceinline__ float rqs_element_bwd(float x, float (&wr)[K], float 
         if (j == i1) g += gv1;
         dr[j] = g;
     }
+#pragma unroll
+    for (int j = 0; j < K && j < 8; ++j) {
+        NFK_PROBE(49 + j, wr[j]);
+        NFK_PROBE(57 + j, hr[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < DN && j < 7; ++j) NFK_PROBE(65 + j, dr[j]);
+    NFK_PROBE(72, gx);
     return gx;
 }
 

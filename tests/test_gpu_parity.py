@@ -100,17 +100,23 @@ def test_layer_vs_reference_golden(name, hip_device):
     layer = build_layer(meta)
     gio.load_into(layer, sd)
     layer = layer.to(hip_device)
+    # NSF_AR sums dim log|det| terms (the slack grows with dim: 5e-5 up to 40
+    # columns) and its inverse conditions on its own outputs through dim - 1
+    # conditioners (test_gpu_nsfar_fused.py's 1e-4)
+    ar = meta["type"] == "NSF_AR"
+    ld_atol = LD_ATOL * max(1.0, meta["kwargs"].get("dim", 0) / 40.0) if ar else LD_ATOL
+    inv_atol = 1e-4 if ar else 5e-5
     with torch.no_grad():
         z, ld = layer(d["x"].to(hip_device))
         close(z, d["z"], Z_RTOL, Z_ATOL)
-        close(ld, d["ld"], LD_RTOL, LD_ATOL)
+        close(ld, d["ld"], LD_RTOL, ld_atol)
         if "rt_x" in d:
             xi, ldi = layer.inverse(d["z"].to(hip_device))
-            close(xi, d["rt_x"], Z_RTOL, 5e-5)
-            close(ldi, d["rt_ld"], LD_RTOL, LD_ATOL)
+            close(xi, d["rt_x"], Z_RTOL, inv_atol)
+            close(ldi, d["rt_ld"], LD_RTOL, ld_atol)
             xa, lda = layer.inverse(d["x"].to(hip_device))
-            close(xa, d["inv_x"], Z_RTOL, 5e-5)
-            close(lda, d["inv_ld"], LD_RTOL, LD_ATOL)
+            close(xa, d["inv_x"], Z_RTOL, inv_atol)
+            close(lda, d["inv_ld"], LD_RTOL, ld_atol)
 
 
 def _golden_model(meta, sd, device):

@@ -1,0 +1,68 @@
+"""CPU: the host helper (normalizingflow_amd/csrc/nfk_host.cpp) that validates
+the fused NSF_AR pack of layers with thousands of parameter tensors: its key
+changes exactly when the Python key (module identities, every Linear's
+storage + version counter) would, and it rejects non-stock conditioners."""
+import time
+
+import pytest
+import torch
+from torch import nn
+
+import nf.flows as nff
+
+
+@pytest.fixture(scope="module")
+def hs():
+    from normalizingflow_amd import _hostbuild
+    _hostbuild.build()
+    from normalizingflow_amd import _nfk_host
+    return _nfk_host
+
+
+def _state(hs, layer):
+    return hs.ar_state(layer.layers._modules, layer.init_param, nff.FCNN, nn.Linear, nn.Tanh)
+
+
+def test_ar_state_tracks_every_change(hs):
+    torch.manual_seed(0)
+    layer = nff.NSF_AR(dim=12, K=4, B=3.0, hidden_dim=16)
+    s0 = _state(hs, layer)
+    assert s0 >= 0 and _state(hs, layer) == s0
+    with torch.no_grad():
+        layer.layers[5].network[2].bias.add_(1.0)            # in-place update: version bump
+    s1 = _state(hs, layer)
+    assert s1 != s0
+    with torch.no_grad():
+        layer.init_param.mul_(1.0)
+    s2 = _state(hs, layer)
+    assert s2 != s1
+    layer.layers[3].network[0] = nn.Linear(8, 16)            # a replaced Linear
+    s3 = _state(hs, layer)
+    assert s3 != s2
+    layer.layers[7].network[1] = nn.Tanh()                   # a replaced activation object
+    s4 = _state(hs, layer)
+    assert s4 != s3 and _state(hs, layer) == s4
+    layer.layers[7].network[1] = nn.ReLU()                   # not the stock FCNN any more
+    assert _state(hs, layer) == -1
+
+
+def test_fingerprint_tracks_versions(hs):
+    ts = [torch.zeros(3) for _ in range(5)]
+    f0 = hs.fingerprint(ts)
+    ts[2].add_(1)
+    assert hs.fingerprint(ts) != f0
+    with pytest.raises(TypeError):
+        hs.fingerprint([1, 2])
+
+
+def test_ar_state_fast_at_polymer_size(hs):
+    """Polymer.yaml's layer (2,047 conditioners): the C++ key in a few ms (the
+    Python key took ~23 ms; the walk touches ~20 K Python objects)."""
+    torch.manual_seed(0)
+    layer = nff.NSF_AR(dim=2048, K=32, B=0.5, hidden_dim=100)
+    _state(hs, layer)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        _state(hs, layer)
+    dt = (time.perf_counter() - t0) / 5
+    assert dt < 15e-3, dt

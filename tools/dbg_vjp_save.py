@@ -93,14 +93,17 @@ def main():
             counts = getattr(lib, "nfk_vjp_diag_counts", None)
             if counts is not None:
                 counts.argtypes = [ctypes.c_void_p, ctypes.c_int]
-                cbuf = (ctypes.c_int * 64)()
+                cbuf = (ctypes.c_int * (64 + 80))()
                 counts(ctypes.cast(cbuf, ctypes.c_void_p), 1)
             for rep in range(reps):
                 r_gp, r_gx, r_in = run(True)
                 if counts is not None:
                     counts(ctypes.cast(cbuf, ctypes.c_void_p), 1)
                     print("  twice: per-lane mismatches of the two evaluations: total %d, lanes 0-47 %d, "
-                          "48-63 %d" % (sum(cbuf), sum(cbuf[:48]), sum(cbuf[48:])), flush=True)
+                          "48-63 %d" % (sum(cbuf[:64]), sum(cbuf[:48]), sum(cbuf[48:64])), flush=True)
+                    firsts = {i: cbuf[64 + i] for i in range(80) if cbuf[64 + i]}
+                    if firsts:
+                        print("  probe: first differing intermediate slot -> count %s" % firsts, flush=True)
                 in_diff = (r_in != c_in) & ~(torch.isnan(r_in) & torch.isnan(c_in))
                 out_diff = (r_gp != c_gp) & ~(torch.isnan(r_gp) & torch.isnan(c_gp))
                 el_in = in_diff.any(1)

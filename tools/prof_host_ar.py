@@ -1,5 +1,6 @@
-"""Host-side profile (cProfile) of the ar354 log_prob step at the applications'
-40-row batch: where the time between kernel launches goes."""
+"""Host-side profile (cProfile) of an NSF_AR log_prob step at its workload's
+default batch (ar354: the applications' 40 rows; fe162: 50; poly2048: 40):
+where the time between kernel launches goes.  usage: prof_host_ar354.py [WORKLOAD]"""
 import cProfile
 import pstats
 import sys
@@ -11,8 +12,9 @@ sys.path.insert(0, ".")
 import bench  # noqa: E402
 
 dev = torch.device("cuda", 0)
-model, sd, _ = bench.build_model("ar354", dev)
-x = torch.randn(40, 96, device=dev)
+wl = sys.argv[1] if len(sys.argv) > 1 else "ar354"
+model, sd, _ = bench.build_model(wl, dev)
+x = torch.randn(bench.DEFAULT_BATCH[wl], bench.WORKLOADS[wl][3], device=dev)
 with torch.no_grad():
     for _ in range(5):
         model.log_prob(x)
@@ -25,4 +27,4 @@ with torch.no_grad():
     pr.disable()
     torch.cuda.synchronize()
     print("ms per step", (time.perf_counter() - t) / 50 * 1e3)
-pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
