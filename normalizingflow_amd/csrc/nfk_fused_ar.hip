@@ -713,30 +713,71 @@ __global__ __launch_bounds__(64 * NW, ar_min_waves(KBH)) void k_fused_ar(ArArgs 
 
 // log|det| of a column-split forward: the per-column terms summed in column
 // order from 0 (bitwise the single-range kernel's ld_acc), then mode 1/2.
-// A workgroup takes 64 rows: its four waves load 128-column chunks of the
-// [dim][batch] terms into LDS (coalesced over the rows, every load in flight
-// at once), then wave 0 adds each row's chunk in column order.  (One thread
-// per row walking the columns had each add wait for its strided load: 0.78 ms
-// at Polymer's 2048 columns, 36 us at dim 96.)
-constexpr int kLdRows = 64, kLdCols = 128;
-__global__ __launch_bounds__(256) void k_ar_ld_sum(const float* cols, float* logdet, int64_t batch, int dim, int mode) {
-    __shared__ float tile[kLdRows][kLdCols + 1];
+// A workgroup takes 64 rows: waves 1-15 load 256-column chunks of the
+// [dim][batch] terms into one of two LDS buffers (coalesced over the rows,
+// all of a chunk's loads in flight at once) while wave 0 adds the previous
+// chunk of each row in column order (16-B LDS reads, row stride 260 floats:
+// conflict-free); one barrier per chunk.  (One thread per row walking the
+// columns had each add wait for its strided load: 0.78 ms at Polymer's 2048
+// columns; one 128-column buffer filled and summed in turn: 0.23 ms.)  The
+// sum itself is the dependent chain of dim additions per row.
+constexpr int kLdRows = 64, kLdCols = 256, kLdStride = kLdCols + 4, kLdThreads = 1024;
+constexpr int kLdPer = (kLdRows * kLdCols + kLdThreads - 64 - 1) / (kLdThreads - 64);  // loads per loader thread
+constexpr size_t kLdLds = (size_t)2 * kLdRows * kLdStride * sizeof(float);
+
+__device__ __forceinline__ void ld_load_chunk(const float* cols, float* buf, int64_t batch, int64_t r0, int nr,
+                                              int c0, int nc, int t) {
+    float v[kLdPer];
+#pragma unroll
+    for (int i = 0; i < kLdPer; ++i) {
+        const int e = t + i * (kLdThreads - 64), c = e >> 6, r = e & 63;
+        v[i] = (c < nc && r < nr) ? cols[(int64_t)(c0 + c) * batch + r0 + r] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < kLdPer; ++i) {
+        const int e = t + i * (kLdThreads - 64), c = e >> 6, r = e & 63;
+        if (c < nc) buf[r * kLdStride + c] = v[i];
+    }
+}
+
+__global__ __launch_bounds__(kLdThreads) void k_ar_ld_sum(const float* cols, float* logdet, int64_t batch, int dim,
+                                                         int mode) {
+    extern __shared__ __attribute__((aligned(16))) float ldt[];
     const int t = threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.x * kLdRows;
     const int nr = batch - r0 < kLdRows ? (int)(batch - r0) : kLdRows;
+    const int nch = (dim + kLdCols - 1) / kLdCols;
+    if (t >= 64) ld_load_chunk(cols, ldt, batch, r0, nr, 0, dim < kLdCols ? dim : kLdCols, t - 64);
+    __syncthreads();
     float acc = 0.0f;
-    for (int c0 = 0; c0 < dim; c0 += kLdCols) {
-        const int nc = dim - c0 < kLdCols ? dim - c0 : kLdCols;
-        for (int e = t; e < kLdCols * kLdRows; e += 256) {
-            const int c = e / kLdRows, r = e - c * kLdRows;
-            if (c < nc && r < nr) tile[r][c] = cols[(int64_t)(c0 + c) * batch + r0 + r];
+    for (int k = 0; k < nch; ++k) {
+        const int c0 = k * kLdCols, nc = dim - c0 < kLdCols ? dim - c0 : kLdCols;
+        if (t >= 64) {
+            if (k + 1 < nch) {
+                const int c1 = c0 + kLdCols;
+                ld_load_chunk(cols, ldt + ((k + 1) & 1) * kLdRows * kLdStride, batch, r0, nr, c1,
+                              dim - c1 < kLdCols ? dim - c1 : kLdCols, t - 64);
+            }
+        } else if (t < nr) {
+            const float* row = ldt + (k & 1) * kLdRows * kLdStride + t * kLdStride;
+            const int n4 = nc >> 2;
+            for (int c = 0; c < n4; ++c) {
+                const float4 v = reinterpret_cast<const float4*>(row)[c];
+                acc = acc + v.x;
+                acc = acc + v.y;
+                acc = acc + v.z;
+                acc = acc + v.w;
+            }
+            for (int c = 4 * n4; c < nc; ++c) acc = acc + row[c];
         }
-        __syncthreads();
-        if (t < nr)
-            for (int c = 0; c < nc; ++c) acc = acc + tile[t][c];
         __syncthreads();
     }
     if (t < nr) logdet[r0 + t] = mode == 2 ? logdet[r0 + t] + acc : acc;
+}
+
+inline void launch_ld_sum(const float* cols, float* logdet, int64_t batch, int dim, int mode, hipStream_t st) {
+    hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((batch + kLdRows - 1) / kLdRows)), dim3(kLdThreads), kLdLds, st,
+                       cols, logdet, batch, dim, mode);
 }
 
 
@@ -791,8 +832,7 @@ int launch_ar(const ArArgs& a, const ArDims& d, bool inv, hipStream_t st) {
             hipLaunchKernelGGL((k_fused_ar<KBH, T1, K, KBX, false, 4>), g, b, lds, st, a);
     }
     if (a.csplit > 1 && a.mode != 0)
-        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + kLdRows - 1) / kLdRows)), dim3(256), 0, st, a.ld_cols,
-                           a.logdet, a.batch, a.dim, a.mode);
+        launch_ld_sum(a.ld_cols, a.logdet, a.batch, a.dim, a.mode, st);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -1163,8 +1203,7 @@ int launch_cl(const ClArgs& a, const ArDims& d, bool inv, hipStream_t st) {
     else
         hipLaunchKernelGGL((k_fused_cl<KBH, T1, K, false>), g, b, lds, st, a);
     if (a.csplit > 1 && a.mode != 0)
-        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + kLdRows - 1) / kLdRows)), dim3(256), 0, st, a.ld_cols,
-                           a.logdet, a.batch, a.n_up, a.mode);
+        launch_ld_sum(a.ld_cols, a.logdet, a.batch, a.n_up, a.mode, st);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -1582,8 +1621,7 @@ int launch_ars(ArsArgs a, const ArsDims& ad, float* logdet, int mode, float pi, 
     const int64_t nblk = (a.rblocks * a.csplit + 7) / 8 * 8;
     hipLaunchKernelGGL((k_fused_ar_s<KBH, T1, K>), dim3((unsigned)nblk), dim3(64 * kArsNW), lds, st, a);
     if (mode != 0)
-        hipLaunchKernelGGL(k_ar_ld_sum, dim3((unsigned)((a.batch + kLdRows - 1) / kLdRows)), dim3(256), 0, st, a.ld_cols, logdet,
-                           a.batch, a.dim, mode);
+        launch_ld_sum(a.ld_cols, logdet, a.batch, a.dim, mode, st);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

@@ -719,7 +719,21 @@ __device__ __forceinline__ void knot_phase(const f32x4 (&acc)[K], const float (&
             kb[r] = k;
         }
         const int kk = kb[r];
-        if (NFK_LUT) {
+        if (NFK_LUT == 2 && SEARCH) {
+            // (diagnostic A/B) the searched phase without the table: the
+            // prefixes are strictly increasing from pre[0] = 0, so pre[kk] is
+            // the largest prefix <= xi and pre[kk + 1] the smallest > xi, each
+            // an unsigned minimum of differences (negative ones wrap high)
+            const int xi = __float2int_rd(__builtin_fmaf(xv[r], c.inv30, -c.lo * c.inv30));
+            uint32_t m0 = (uint32_t)xi, m1 = 0xffffffffu;
+#pragma unroll
+            for (int j = 1; j < K; ++j) {
+                m0 = min(m0, (uint32_t)xi - (uint32_t)pre[j]);
+                m1 = min(m1, (uint32_t)pre[j] - (uint32_t)xi - 1u);
+            }
+            p0 = (int)((uint32_t)xi - m0);
+            p1 = (int)((uint32_t)xi + 1u + m1);
+        } else if (NFK_LUT) {
             // rows 0..K-1; p1 is unused when kk = K - 1 (e1 = hi below)
 #pragma unroll
             for (int j = 0; j < K; ++j) scr[j * 64 + lane] = pre[j];

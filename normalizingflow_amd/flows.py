@@ -132,16 +132,17 @@ def raise_on_status(status, n_slots=None, prior=None):
     support check in prior.log_prob, models.py:19), after every layer."""
     if status is None or (n_slots == 0 and not _validates(prior)):
         return  # nothing this word set can raise: no device->host read
-    st = status.cpu().tolist()
+    st = status.cpu().numpy()
     n = len(st) if n_slots is None else n_slots
-    for w in st[:n]:
-        if not w & ST_INSIDE_SEEN:
+    # the first word (in execution order) that raises decides which error
+    bad = np.flatnonzero(((st[:n] & ST_INSIDE_SEEN) == 0) | ((st[:n] & ST_NEG_DISC) != 0))
+    if bad.size:
+        if not st[bad[0]] & ST_INSIDE_SEEN:
             raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0. "
                                "(no element inside the spline interval [-B, B], nf/utils.py:63)")
-        if w & ST_NEG_DISC:
-            raise AssertionError("negative discriminant in the inverse rational-quadratic spline "
-                                 "(nf/utils.py:121)")
-    if _validates(prior) and any(w & ST_NAN_Z for w in st):
+        raise AssertionError("negative discriminant in the inverse rational-quadratic spline "
+                             "(nf/utils.py:121)")
+    if _validates(prior) and bool((st & ST_NAN_Z).any()):
         raise ValueError("Expected value argument to be within the support (IndependentConstraint("
                          "Real(), 1)) of the distribution %s, but found invalid values (NaN in z)"
                          % type(prior).__name__)
@@ -785,13 +786,19 @@ class NSF_AR(_HipFlow):
         if not config.USE_FUSED or self.dim < 2:
             return None
         hs = _host_helper()
-        if hs is not None and self._pack_cache is not None:
-            # the same key computed in C++ (module identities and every
-            # Linear's storage + version): ~1 ms instead of ~23 ms at Polymer's
-            # 2,047 conditioners (csrc/nfk_host.cpp)
-            st = hs.ar_state(self.layers._modules, self.init_param, FCNN, nn.Linear, nn.Tanh)
-            if st >= 0 and self._pack_cache[4] == (device, st):
-                return self._pack_cache[1]
+        if hs is not None and self._pack_cache is not None and self._pack_cache[4] is not None:
+            # the same key kept in C++ (csrc/nfk_host.cpp): a watch over every
+            # dict of the module tree (CPython's dict version tags) and every
+            # parameter (storage, version) -- ~20 us at Polymer's 2,047
+            # conditioners, where recomputing the key in Python took ~23 ms --
+            # else the key's hash recomputed in C++ (~1 ms)
+            hdev, hw = self._pack_cache[4]
+            if hdev == device:
+                if isinstance(hw, int):
+                    if hw == hs.ar_state(self.layers._modules, self.init_param, FCNN, nn.Linear, nn.Tanh):
+                        return self._pack_cache[1]
+                elif hw.valid():
+                    return self._pack_cache[1]
         lin = self._stock_linears()
         if not lin:
             return None
@@ -814,8 +821,12 @@ class NSF_AR(_HipFlow):
         pack, keep = K_.fused_ar_pack(ws, self.init_param, self.dim, hidden, self.K)
         hkey = None
         if hs is not None:
-            st = hs.ar_state(self.layers._modules, self.init_param, FCNN, nn.Linear, nn.Tanh)
-            hkey = (device, st) if st >= 0 else None
+            hw = hs.ar_watch(self.__dict__["_parameters"], self.layers._modules, self.init_param, FCNN, nn.Linear,
+                             nn.Tanh)
+            if hw is None:
+                hw = hs.ar_state(self.layers._modules, self.init_param, FCNN, nn.Linear, nn.Tanh)
+                hw = hw if hw >= 0 else None
+            hkey = (device, hw) if hw is not None else None
         self._pack_cache = (key, pack, hidden, keep, hkey)
         return pack
 

@@ -66,3 +66,61 @@ def test_ar_state_fast_at_polymer_size(hs):
         _state(hs, layer)
     dt = (time.perf_counter() - t0) / 5
     assert dt < 15e-3, dt
+
+
+def _watch(hs, layer):
+    return hs.ar_watch(layer.__dict__["_parameters"], layer.layers._modules, layer.init_param, nff.FCNN, nn.Linear,
+                       nn.Tanh)
+
+
+@pytest.mark.parametrize("change", ["inplace", "init_inplace", "init_replaced", "linear_replaced", "tanh_replaced",
+                                    "param_replaced", "data_assigned", "cond_replaced", "cond_appended"])
+def test_ar_watch_invalidated_by_every_change(hs, change):
+    """The watch (dict version tags + parameter storage/version) turns invalid
+    on each change that alters the pack key, and stays valid otherwise."""
+    torch.manual_seed(0)
+    layer = nff.NSF_AR(dim=12, K=4, B=3.0, hidden_dim=16)
+    w = _watch(hs, layer)
+    assert w is not None and w.valid() and w.valid()
+    if change == "inplace":
+        with torch.no_grad():
+            layer.layers[5].network[2].bias.add_(1.0)
+    elif change == "init_inplace":
+        with torch.no_grad():
+            layer.init_param.mul_(1.0)
+    elif change == "init_replaced":
+        layer.init_param = nn.Parameter(layer.init_param.detach().clone())
+    elif change == "linear_replaced":
+        layer.layers[3].network[0] = nn.Linear(8, 16)
+    elif change == "tanh_replaced":
+        layer.layers[7].network[1] = nn.Tanh()
+    elif change == "param_replaced":
+        layer.layers[2].network[4].weight = nn.Parameter(torch.zeros(11, 16))
+    elif change == "data_assigned":
+        layer.layers[4].network[0].weight.data = torch.zeros(16, 10)
+    elif change == "cond_replaced":
+        layer.layers[6] = nff.FCNN(14, 11, 16)
+    elif change == "cond_appended":
+        layer.layers.append(nff.FCNN(24, 11, 16))
+    assert not w.valid()
+
+
+def test_ar_watch_rejects_non_stock(hs):
+    torch.manual_seed(0)
+    layer = nff.NSF_AR(dim=6, K=4, B=3.0, hidden_dim=16)
+    layer.layers[2].network[1] = nn.ReLU()
+    assert _watch(hs, layer) is None
+
+
+def test_ar_watch_fast_at_polymer_size(hs):
+    """valid() compares the cached words only (~20 K at Polymer's 2,047
+    conditioners): well under the key's recomputation."""
+    torch.manual_seed(0)
+    layer = nff.NSF_AR(dim=2048, K=32, B=0.5, hidden_dim=100)
+    w = _watch(hs, layer)
+    w.valid()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        assert w.valid()
+    dt = (time.perf_counter() - t0) / 10
+    assert dt < 5e-3, dt
