@@ -378,6 +378,39 @@ __device__ __forceinline__ void dma4(const float* gsrc, uint32_t lds) {
 }
 
 // every DMA and LDS access of this wave retired, then the workgroup barrier
+// Kernels that issue MFMAs and can share a SIMD with other waves are
+// code-generated without packed-FP32 VALU instructions (v_pk_{add,mul,fma}_f32):
+// DESIGN.md section 10.5 -- with dependent MFMA accumulate chains in flight on
+// the SIMD, packed-FP32 results in lanes 48-63 of a co-resident wave were
+// intermittently wrong (tools/ubench_elem_twice.hip reproduces it; the same
+// source without packed FP32 never does).  The MFMA translation units are built
+// without the feature (Makefile NOPK); a kernel that runs one wave per SIMD
+// (512 registers) may take it back with NFK_PK_FP32.  (The other way round --
+// a per-kernel "no-packed-fp32-ops" in a packed unit -- stops the inliner:
+// lambdas keep the unit's features and became calls.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define NFK_PK_FP32 __attribute__((target("packed-fp32-ops")))
+#else
+#define NFK_PK_FP32  // (a device feature: the host pass does not know it)
+#endif
+
+// s_waitcnt vmcnt(n) for a wave-uniform n known only at run time (the field is
+// an immediate): a branch to the matching wait; n >= 63 waits for 63
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    switch (n < 63 ? n : 63) {
+#define NFK_VMW(k) \
+    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+#define NFK_VMW8(k) NFK_VMW(k) NFK_VMW(k + 1) NFK_VMW(k + 2) NFK_VMW(k + 3) NFK_VMW(k + 4) NFK_VMW(k + 5) \
+    NFK_VMW(k + 6) NFK_VMW(k + 7)
+        NFK_VMW8(0) NFK_VMW8(8) NFK_VMW8(16) NFK_VMW8(24) NFK_VMW8(32) NFK_VMW8(40) NFK_VMW8(48)
+        NFK_VMW(56) NFK_VMW(57) NFK_VMW(58) NFK_VMW(59) NFK_VMW(60) NFK_VMW(61) NFK_VMW(62)
+        default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+#undef NFK_VMW8
+#undef NFK_VMW
+    }
+}
+
 __device__ __forceinline__ void dma_barrier() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
