@@ -160,13 +160,15 @@ PARITY_RTOL = 1e-5   # BASELINE.json north star: log_prob within 1e-5 relative (
 PARITY_ATOL = 1e-5   # ... with this absolute floor for values near 0 (tests/test_gpu_parity.py)
 CLOCK_GHZ = 2.4      # MI355X_MICROARCH.md: max engine clock
 N_SIMD = 1024        # 256 CUs x 4 SIMDs
-# VALU issue cost per wave64 instruction on one SIMD-32 with several waves
-# resident: measured by tools/ubench_valu.hip (profiles/r2_ubench_valu.txt:
-# each added co-resident wave adds 2 cycles per v_fma_f32 / v_add_f32 and 4
-# per v_exp_f32 to every wave's per-instruction time, i.e. the SIMD retires
-# one VALU per 2 cycles and one transcendental per 4), and
-# MI355X_MICROARCH.md: an MFMA holds the SIMD's vector issue for 8 cycles
-VALU_CYC, TRANS_CYC, MFMA_HOLD_CYC = 2.0, 4.0, 8.0
+# VALU issue cost per wave64 instruction on one SIMD with several waves
+# resident, calibrated on wall-clock time (tools/ubench_valu.hip,
+# profiles/r2_ubench_valu.txt: at 2-4 waves per SIMD one v_add_f32 / v_fma_f32
+# takes 1.77-2.02 ns of the SIMD, one v_exp_f32 3.48-3.56 ns, i.e. 4.2-4.9 and
+# 8.4-8.6 cycles at 2.4 GHz -- MI355X_MICROARCH.md's issue table says 4 and 8),
+# and MI355X_MICROARCH.md: an MFMA holds the SIMD's vector issue for 8 cycles.
+# (Rounds 2-4 used 2 and 4, read off the per-wave s_memtime column; the
+# wall-clock figures are what a launch pays.)
+VALU_CYC, TRANS_CYC, MFMA_HOLD_CYC = 4.4, 8.4, 8.0
 
 
 def build_model(workload, device):
@@ -363,7 +365,8 @@ def valu_floor_ms(insts, per_launch_scale=1.0):
     the cycles each MFMA holds it, spread over the 1024 SIMDs at the max clock."""
     if not insts:
         return None
-    cyc = (VALU_CYC * (insts["valu"] - insts["valu_trans"]) + TRANS_CYC * insts["valu_trans"]
+    # (SQ_INSTS_VALU counts the MFMAs too: they are priced by their issue hold only)
+    cyc = (VALU_CYC * (insts["valu"] - insts["valu_trans"] - insts["mfma"]) + TRANS_CYC * insts["valu_trans"]
            + MFMA_HOLD_CYC * insts["mfma"]) * per_launch_scale
     return cyc / N_SIMD / (CLOCK_GHZ * 1e9) * 1e3
 
@@ -430,6 +433,8 @@ def _mfma_roofline(name, n_mfma, B, per, mean_ms, t_mfma, ref_flops, floors):
     f16 MFMA peak, so frac = the MFMA floor / the launch time."""
     mflops = n_mfma * MFMA_FLOP * (B / 16.0) * per
     achieved = mflops / (mean_ms * 1e-3) / 1e12
+    if "valu_issue_ms" in floors:  # the binding pipe of the VALU-heavy formulations (diagnostic)
+        floors["valu_issue_frac"] = round(floors["valu_issue_ms"] / mean_ms, 4)
     return {"kernel": name, "bound": "mfma", "achieved": round(achieved, 2),
             "peak": round(PEAK_MFMA_F16_TFLOPS, 1), "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_MFMA_F16_TFLOPS, 4),

@@ -361,14 +361,18 @@ struct ArArgs {
 
 // GEMM over the sub-records J, J + 1, ... of an NT-tile record; end() after
 // each ends the sub-record (barrier, next copy) and moves to the next slot.
+// busy (wave-uniform) false: a wave whose 16 rows all lie past the batch
+// (small batches: 40 rows leave the fourth wave of a workgroup empty) only
+// keeps the barriers and copies, not the MFMAs and their LDS reads
 template <int NS, int KB, bool T1, int NT, int J, class SlotF, class EndF>
 __device__ __forceinline__ void ar_parts(const h8 (&bh)[KB], const h8 (&bl)[KB], h4 bt, int lane,
-                                         f32x4 (&acc)[NT], SlotF slot, EndF end, float bsc = 1.0f) {
+                                         f32x4 (&acc)[NT], SlotF slot, EndF end, float bsc = 1.0f,
+                                         bool busy = true) {
     constexpr int T0 = J * NS;
     constexpr int N = (NT - T0) < NS ? (NT - T0) : NS;
-    gemm_h<KB, T1, N, NS, T0, NT, true, T0 + NS >= NT>(bh, bl, bt, slot(), lane, acc, bsc);
+    if (busy) gemm_h<KB, T1, N, NS, T0, NT, true, T0 + NS >= NT>(bh, bl, bt, slot(), lane, acc, bsc);
     end();
-    if constexpr (T0 + NS < NT) ar_parts<NS, KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end, bsc);
+    if constexpr (T0 + NS < NT) ar_parts<NS, KB, T1, NT, J + 1>(bh, bl, bt, lane, acc, slot, end, bsc, busy);
 }
 
 // The same over a hidden width with a 16-feature tail (tail kind 2): the full
@@ -376,22 +380,24 @@ __device__ __forceinline__ void ar_parts(const h8 (&bh)[KB], const h8 (&bl)[KB],
 // tile the tail's two MFMAs on B1 = {hi, lo}, B2 = {hi, 0} of the half tile
 template <int NS, int KB, int NT, int J, class SlotF, class EndF>
 __device__ __forceinline__ void ar_parts16(const h8 (&bh)[KB], const h8 (&bl)[KB], h8 b1, h8 b2, int lane,
-                                           f32x4 (&acc)[NT], SlotF slot, EndF end) {
+                                           f32x4 (&acc)[NT], SlotF slot, EndF end, bool busy = true) {
     constexpr int T0 = J * NS;
     constexpr int N = (NT - T0) < NS ? (NT - T0) : NS;
-    const float4* sl = slot();
-    gemm_h<KB, false, N, NS, T0, NT, true>(bh, bl, h4{0, 0, 0, 0}, sl, lane, acc);
-    const float4* t16 = sl + (KB * NS * 2 + 1) * 64;
+    if (busy) {
+        const float4* sl = slot();
+        gemm_h<KB, false, N, NS, T0, NT, true>(bh, bl, h4{0, 0, 0, 0}, sl, lane, acc);
+        const float4* t16 = sl + (KB * NS * 2 + 1) * 64;
 #pragma unroll
-    for (int t = 0; t < N; ++t) {
-        const h8 a1 = __builtin_bit_cast(h8, t16[(2 * t) * 64 + lane]);
-        const h8 a2 = __builtin_bit_cast(h8, t16[(2 * t + 1) * 64 + lane]);
-        acc[T0 + t] = mfma16(a1, b1, acc[T0 + t]);
-        acc[T0 + t] = mfma16(a2, b2, acc[T0 + t]);
+        for (int t = 0; t < N; ++t) {
+            const h8 a1 = __builtin_bit_cast(h8, t16[(2 * t) * 64 + lane]);
+            const h8 a2 = __builtin_bit_cast(h8, t16[(2 * t + 1) * 64 + lane]);
+            acc[T0 + t] = mfma16(a1, b1, acc[T0 + t]);
+            acc[T0 + t] = mfma16(a2, b2, acc[T0 + t]);
+        }
+        if constexpr (T0 + NS >= NT) mfma_result_wait();
     }
-    if constexpr (T0 + NS >= NT) mfma_result_wait();
     end();
-    if constexpr (T0 + NS < NT) ar_parts16<NS, KB, NT, J + 1>(bh, bl, b1, b2, lane, acc, slot, end);
+    if constexpr (T0 + NS < NT) ar_parts16<NS, KB, NT, J + 1>(bh, bl, b1, b2, lane, acc, slot, end, busy);
 }
 
 // activations of a hidden layer with a 16-feature tail: the full tiles by
@@ -474,6 +480,10 @@ __device__ __forceinline__ void ar_layer(ArArgs a) {
     const int64_t b0 = (rbk * kArWaves + wid) * 16;
     const bool row_ok = b0 + sl < a.batch;
     const int64_t brow = row_ok ? b0 + sl : a.batch - 1;  // rows past the batch re-read the last one
+    // every wave runs the GEMMs, rows or not: skipping them in a row-less wave
+    // (a branch around each gemm_h) cost the register instances 28-1,600 VGPR
+    // spills (k_fused_ar_s and k_fused_cl skip them)
+    constexpr bool busy = true;
 
     // the next sub-record st_s (conditioner st_i, part st_u) into slot st_s & 1;
     // layer-1 sub-records hold ceil(2i / 32) k-blocks.  Called once per
@@ -578,7 +588,7 @@ __device__ __forceinline__ void ar_layer(ArArgs a) {
                         ml[KB - 1][j] = j < lim ? ml[KB - 1][j] : (_Float16)0.0f;
                     }
                 }
-                ar_parts<NS, KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end);
+                ar_parts<NS, KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end, 1.0f, busy);
             };
             switch (kb1) {
                 case 1: layer1(std::integral_constant<int, 1>{}); break;
@@ -600,10 +610,10 @@ __device__ __forceinline__ void ar_layer(ArArgs a) {
                 act_operands16<KBH, HT>(h, c21, bh, bl, b1, b2);
                 {
                     f32x4 h2[HT];
-                    ar_parts16<NS, KBH, HT, 0>(bh, bl, b1, b2, lane, h2, slot, end);
+                    ar_parts16<NS, KBH, HT, 0>(bh, bl, b1, b2, lane, h2, slot, end, busy);
                     act_operands16<KBH, HT>(h2, c22, bh, bl, b1, b2);
                 }
-                ar_parts16<NS, KBH, NO, 0>(bh, bl, b1, b2, lane, o, slot, end);
+                ar_parts16<NS, KBH, NO, 0>(bh, bl, b1, b2, lane, o, slot, end, busy);
             } else {
                 act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
 #ifdef NFK_AR_DIAG_DUMP
@@ -611,13 +621,13 @@ __device__ __forceinline__ void ar_layer(ArArgs a) {
 #endif
                 {
                     f32x4 h2[HT];
-                    ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+                    ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end, 1.0f, busy);
                     act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
 #ifdef NFK_AR_DIAG_DUMP
                     if (i == 1 && blockIdx.x == 0) ar_dump_act<HT>(1, h2, KBH, wid * 16 + sl, q);
 #endif
                 }
-                ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+                ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end, 1.0f, busy);
             }
             // logits (unscaled: the exact power of two) into the slab, [sample][param]
 #ifdef NFK_AR_DIAG_DUMP
@@ -1031,6 +1041,7 @@ __device__ __forceinline__ void cl_layer(ClArgs a) {
     const int j_lo = (int)(((int64_t)sp * a.n_up) / a.csplit), j_hi = (int)(((int64_t)(sp + 1) * a.n_up) / a.csplit);
     const int64_t b0 = (rbk * NW + wid) * 16;
     const bool row_ok = b0 + sl < a.batch;
+    const bool busy = b0 < a.batch;  // (wave-uniform) any row of this wave in the batch
     const int64_t brow = row_ok ? b0 + sl : a.batch - 1;
 
     // the stream: layers 1 and 2 (2 NH sub-records), then the output records
@@ -1107,7 +1118,7 @@ __device__ __forceinline__ void cl_layer(ClArgs a) {
             h8 mh[KB], ml[KB];
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) mh[kb] = xh[kb], ml[kb] = xl[kb];
-            ar_parts<NS, KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end, bsc1);
+            ar_parts<NS, KB, false, HT, 0>(mh, ml, btail, lane, h, slot, end, bsc1, busy);
         };
         switch (a.kb1) {
             case 1: layer1(std::integral_constant<int, 1>{}); break;
@@ -1119,7 +1130,7 @@ __device__ __forceinline__ void cl_layer(ClArgs a) {
     }
     {
         f32x4 h2[HT];
-        ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+        ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end, 1.0f, busy);
         act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
     }
 
@@ -1136,7 +1147,7 @@ __device__ __forceinline__ void cl_layer(ClArgs a) {
         float* const slab = scr + c * 16 * PS;
         {
             f32x4 o[NO];
-            ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+            ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end, 1.0f, busy);
 #pragma unroll
             for (int t = 0; t < NO; ++t) {
                 const int p = 16 * t + 4 * q;
@@ -1472,6 +1483,7 @@ __global__ __launch_bounds__(64 * kArsNW, 1) void k_fused_ar_s(ArsArgs a) {
     const int p_lo = 1 + (int)(((int64_t)sp * a.npair) / a.csplit), p_hi = 1 + (int)(((int64_t)(sp + 1) * a.npair) / a.csplit);
     const int64_t b0 = (rbk * NW + wid) * 16;
     const bool row_ok = b0 + sl < a.batch;
+    const bool busy = b0 < a.batch;  // (wave-uniform) any row of this wave in the batch
     const int64_t brow = row_ok ? b0 + sl : a.batch - 1;
     // the conditioners of pair p: p, then dim - p (one when they coincide)
     auto cond_of = [&](int p, int m) { return m == 0 ? p : D - p; };
@@ -1610,7 +1622,7 @@ __global__ __launch_bounds__(64 * kArsNW, 1) void k_fused_ar_s(ArsArgs a) {
                     for (int t = 0; t < HT; ++t) h[t] = as_f32x4(sl4[t * 4 + q]);
                 }
                 const int nk = kb1 - kb0 < kArsKBS ? kb1 - kb0 : kArsKBS;
-                for (int kl = 0; kl < nk; ++kl) {
+                for (int kl = 0; kl < (busy ? nk : 0); ++kl) {
                     h8 th = __builtin_bit_cast(h8, sl4[(TB0 + (kl * NW + wid) * 2) * 64 + lane]);
                     h8 tl = __builtin_bit_cast(h8, sl4[(TB0 + (kl * NW + wid) * 2 + 1) * 64 + lane]);
                     if (kb0 + kl == kb1 - 1) {  // the k-block past feature 2i: masked (x[:, :i])
@@ -1636,11 +1648,11 @@ __global__ __launch_bounds__(64 * kArsNW, 1) void k_fused_ar_s(ArsArgs a) {
             act_operands<KBH, T1, HT>(h, c21, bh, bl, btail);
             {
                 f32x4 h2[HT];
-                ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end);
+                ar_parts<NS, KBH, T1, HT, 0>(bh, bl, btail, lane, h2, slot, end, 1.0f, busy);
                 act_operands<KBH, T1, HT>(h2, c22, bh, bl, btail);
             }
             f32x4 o[NO];
-            ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end);
+            ar_parts<NS, KBH, T1, NO, 0>(bh, bl, btail, lane, o, slot, end, 1.0f, busy);
             float* const slab = scr + nc * 16 * PS;
 #pragma unroll
             for (int t = 0; t < NO; ++t) {
