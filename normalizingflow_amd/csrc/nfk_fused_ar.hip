@@ -62,10 +62,13 @@ namespace {
 constexpr int kArNS = NFK_AR_NS;  // output tiles per sub-record (hidden widths up to 4 k-blocks)
 // wider conditioners (the applications' H = 354: 11 k-blocks) take 2-tile
 // sub-records, so two 46-KiB slots and the spline slabs fit one CU's LDS
+#ifndef NFK_AR_NS_WIDE
+#define NFK_AR_NS_WIDE 2  // (diagnostic A/B: 1-tile sub-records for the wide conditioners)
+#endif
 #ifdef NFK_AR_DIAG_NS2  // diagnostic: 2-tile sub-records for every width
 __host__ __device__ constexpr int ar_ns_for(int) { return 2; }
 #else
-__host__ __device__ constexpr int ar_ns_for(int kbh) { return kbh <= 4 ? kArNS : 2; }
+__host__ __device__ constexpr int ar_ns_for(int kbh) { return kbh <= 4 ? kArNS : NFK_AR_NS_WIDE; }
 #endif
 // waves per SIMD the register allocation targets: two for the NSF_CL-sized
 // conditioners, one (512 registers: MFMA accumulators in AGPRs) for the wide

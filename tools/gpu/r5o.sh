@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round 5 (o): AR/CL tests on the committed build, the c3 bench line with its CPU leg, a
+# Round 5 (o): the full GPU suite and smoke on the committed build, the c3 bench line with its CPU leg, a
 # rocprofv3 kernel-trace summary of the same command, the c3 chain's PMC passes (instruction
 # counts, HBM traffic) on this round's build, NSF_AR bench lines
 set -u
 O=gpurun_out/r5o; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_nsfar_fused.py tests/test_gpu_cl_wide.py -q -rf --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 $O/smoke.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python bench.py > $O/c3.json 2> $O/c3.err || { tail -5 $O/c3.err; exit 1; }
 echo "c3: $(python3 tools/bench_line.py $O/c3.json)"
