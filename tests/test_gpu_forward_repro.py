@@ -104,3 +104,24 @@ def test_wide_nsf_c5_layer_reproducible(hip_device, no_chain):
     assert layer._fused_pack(x.device) is not None
     _assert_same(_runs(lambda: layer(x)))
     flush_status_checks()
+
+
+def test_streamed_ar_reproducible(hip_device):
+    """The streamed NSF_AR form (k_fused_ar_s, Polymer's kernel; forced on a
+    config.py-shaped layer) at 2^16 + 77 rows -- 1,025 row blocks, every CU
+    busy several times over -- three runs bitwise equal, the log|det| column
+    sum (k_ar_ld_sum) included."""
+    from normalizingflow_amd import kernels as K_
+    lib = K_._lib.load()
+    torch.manual_seed(7)
+    layer = nff.NSF_AR(dim=96, K=32, B=1.5, hidden_dim=100).to(hip_device)
+    x = torch.randn((1 << 16) + 77, 96, device=hip_device)
+    prev = lib.nfk_debug_ar_stream(1)
+    try:
+        layer.invalidate_caches()
+        assert layer._fused_pack(x.device) is not None
+        _assert_same(_runs(lambda: layer(x)))
+    finally:
+        lib.nfk_debug_ar_stream(prev)
+        layer.invalidate_caches()
+    flush_status_checks()
