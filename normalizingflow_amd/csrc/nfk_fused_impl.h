@@ -12,6 +12,7 @@ int nfk_set_error(const char* msg);  // nfk_kernels.hip
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 
 #ifndef NFK_WAVES
@@ -466,23 +467,74 @@ __device__ __forceinline__ void gather_x(const float* __restrict__ x, int64_t ld
 // sign(x) (1 - t) / (1 + t), t = 2^(-2|x| log2e) in (0, 1]; c2 = -2 log2e
 // unscale.  Branch free, no overflow; absolute error ~1e-7 of the activation
 // (which only feeds the next linear layer, where absolute error propagates).
+// NFK_TANH6: 1 (default) 2^14 tanh = 2^15 / (1 + t) - 2^14 on t = e^(-2|x|), 6 VALU;
+// 0 the rounds 1-4 form (1 - t) / ((1 + t) / 2^14), 7 VALU; 2 a 5-VALU signed form.
+// A/B on one box (profiles/r5/r5s_tanh_ab.txt, kernel means of 3 runs): c2 chain
+// 4.849 / 4.702 / 4.768 ms, c3 chain 5.407 / 5.370 / 5.405 ms, Gaussian NSF_AR
+// 6.16 / - / 6.01 ms for 0 / 1 / 2; parity vs the oracle unchanged (7.6e-7 max rel.)
+#ifndef NFK_TANH6
+#define NFK_TANH6 1
+#endif
+#ifndef NFK_SPLIT_MIX
+#define NFK_SPLIT_MIX 1
+#endif
 __device__ __forceinline__ float tanh_scaled(float acc, float c2) {
+#if NFK_TANH6 == 2
+    // (A/B) 2^14 tanh(x) = 2^14 - 2^15 / (1 + e^(2x)) on the signed x: e^(2x)
+    // overflows to +inf for large x (the quotient to 0, tanh to 1) and
+    // underflows to 0 for large -x (tanh -1), so neither |x| nor copysign is
+    // needed: 5 VALU (mul, exp, add, rcp, fma)
+    const float t = __builtin_amdgcn_exp2f(acc * -c2);
+    return __builtin_fmaf(-2.0f * kActScale, __builtin_amdgcn_rcpf(1.0f + t), kActScale);
+#else
     const float t = __builtin_amdgcn_exp2f(__builtin_fabsf(acc) * c2);
+#if NFK_TANH6  // (A/B) 2^14 tanh = 2^15 / (1 + t) - 2^14: one VALU fewer
+    const float r = __builtin_fmaf(2.0f * kActScale, __builtin_amdgcn_rcpf(1.0f + t), -kActScale);
+#else
     const float inv = 1.0f / kActScale;
     const float r = (1.0f - t) * __builtin_amdgcn_rcpf(__builtin_fmaf(t, inv, inv));
+#endif
     return __builtin_copysignf(r, acc);
+#endif
+}
+
+// the fp16 residuals of (v0, v1) over their fp16 roundings (the halves of
+// hp): v - h is exact in fp32, so fma(h, -1, v) rounded once to fp16 is
+// bitwise (_Float16)(v - (float)h).  As an fma of an fp16 and an fp32 operand
+// with an fp16 result, written into either half of the packed pair, that is
+// ONE v_fma_mix{lo,hi}_f16 per element instead of an fp16 -> fp32 convert, a
+// subtract and an fp32 -> fp16 convert (hipcc turns fma(h, -1, v) back into the
+// subtract, hence the asm).  NFK_SPLIT_MIX=0: the plain expression.
+__device__ __forceinline__ uint32_t f16_residual_pair(float v0, float v1, uint32_t hp) {
+#if NFK_SPLIT_MIX
+    uint32_t r;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(v0));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(r) : "v"(hp), "v"(v1));
+    return r;
+#else
+    const _Float16 h0 = __builtin_bit_cast(_Float16, (uint16_t)(hp & 0xFFFFu));
+    const _Float16 h1 = __builtin_bit_cast(_Float16, (uint16_t)(hp >> 16));
+    const _Float16 l0 = (_Float16)(v0 - (float)h0), l1 = (_Float16)(v1 - (float)h1);
+    return (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+#endif
 }
 
 // B fragments (hi, lo) of k-block kb from the activations of tiles 2kb, 2kb+1
 template <int HT>
 __device__ __forceinline__ void split_act(const f32x4 (&a)[HT], int kb, h8& hi, h8& lo) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float v = a[2 * kb + (j >> 2)][j & 3];
-        const _Float16 h = (_Float16)v;
-        hi[j] = h;
-        lo[j] = (_Float16)(v - (float)h);
-    }
+    for (int j = 0; j < 8; ++j) hi[j] = (_Float16)a[2 * kb + (j >> 2)][j & 3];
+#if NFK_SPLIT_MIX
+    const u32x4 hp = __builtin_bit_cast(u32x4, hi);
+    u32x4 lp;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+        lp[p] = f16_residual_pair(a[2 * kb + (p >> 1)][2 * (p & 1)], a[2 * kb + (p >> 1)][2 * (p & 1) + 1], hp[p]);
+    lo = __builtin_bit_cast(h8, lp);
+#else
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lo[j] = (_Float16)(a[2 * kb + (j >> 2)][j & 3] - (float)hi[j]);
+#endif
 }
 
 // Wait after a GEMM's last MFMA before its accumulators are read (32 wait
