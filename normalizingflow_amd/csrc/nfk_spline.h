@@ -11,6 +11,10 @@
 // Host-side constants (NfkSplineConst) are evaluated in double exactly as the
 // Python scalars of the reference are, then rounded to fp32 once.
 #pragma once
+
+#ifndef NFK_MAX3_ASM
+#define NFK_MAX3_ASM 1
+#endif
 #include <hip/hip_runtime.h>
 
 #ifndef NFK_TREESUM
@@ -170,12 +174,51 @@ __device__ __forceinline__ float nfk_sum(const float (&v)[K]) {
 // knot edges at fma(s2, 0, lo) + ..., which is lo exactly unless the logits
 // were NaN -- then the edges, and everything the reference computes from its
 // NaN cumsum (utils.py:73-91), are NaN too.
+// max of K logits as a tree of three-input v_max3_f32 (inline asm): written with
+// fmaxf, hipcc first quiets every input (v_max_f32 x, x: IEEE mode's signalling
+// NaNs), about one instruction more per two inputs.  The logits are MFMA results,
+// never signalling NaNs, and a quiet NaN input leaves the max at the other
+// values in both forms (the exps of the NaN logit make the knots NaN).
+__device__ __forceinline__ float nfk_max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float nfk_max2(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 template <int K>
-__device__ __forceinline__ float nfk_prefix_nsf_lean(const float (&raw)[K], float l2e, float m2b,
-                                                     float fb30, float mb30, int (&pre)[K]) {
+__device__ __forceinline__ float nfk_max_lean(const float (&raw)[K]) {
+#if NFK_MAX3_ASM
+    float t[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) t[i] = raw[i];
+    int n = K;
+#pragma unroll
+    for (int pass = 0; pass < 8 && n > 1; ++pass) {  // (constant-folded: K is a template argument)
+        int w = 0;
+#pragma unroll
+        for (int i = 0; i < K; i += 3) {
+            if (i >= n) break;
+            t[w++] = (i + 2 < n) ? nfk_max3(t[i], t[i + 1], t[i + 2]) : (i + 1 < n ? nfk_max2(t[i], t[i + 1]) : t[i]);
+        }
+        n = w;
+    }
+    return t[0];
+#else
     float m = raw[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) m = fmaxf(m, raw[i]);
+    return m;
+#endif
+}
+
+template <int K>
+__device__ __forceinline__ float nfk_prefix_nsf_lean(const float (&raw)[K], float l2e, float m2b,
+                                                     float fb30, float mb30, int (&pre)[K]) {
+    const float m = nfk_max_lean<K>(raw);
     const float mL = m * l2e;
     float e[K];
 #pragma unroll
