@@ -382,8 +382,8 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
                         for (int j = 0; j < K - 1; ++j) fs[j * 64 + lane] = accd[s][j][r];
                         raw_k = fs[(k > 0 ? k - 1 : 0) * 64 + lane];
                         raw_k1 = fs[(k < K - 1 ? k : K - 2) * 64 + lane];
-                        const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
-                        const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
+                        const float dv_k = nfk_deriv_lean_s(raw_k, l2e3, c.min_d);
+                        const float dv_k1 = nfk_deriv_lean_s(raw_k1, l2e3, c.min_d);
                         const float d_k = (k == 0) ? c.d_edge : dv_k;
                         const float d_k1 = (k == K - 1) ? c.d_edge : dv_k1;
                         const float x = xv[s][r];

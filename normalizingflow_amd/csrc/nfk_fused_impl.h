@@ -1349,8 +1349,8 @@ __global__ __launch_bounds__(64 * kNsfWaves, SPLIT ? NFK_NSF_WPE_SPLIT : NFK_NSF
                 // at the two knots the bin uses; the padded ends are the constant d_edge
                 // both evaluated, then selected: as a conditional the compiler
                 // branches around the exp/log under an exec mask
-                const float dv_k = nfk_deriv_lean(raw_k * un3, c.min_d);
-                const float dv_k1 = nfk_deriv_lean(raw_k1 * un3, c.min_d);
+                const float dv_k = nfk_deriv_lean_s(raw_k, l2e3, c.min_d);
+                const float dv_k1 = nfk_deriv_lean_s(raw_k1, l2e3, c.min_d);
                 const float d_k = (k == 0) ? c.d_edge : dv_k;
                 const float d_k1 = (k == K - 1) ? c.d_edge : dv_k1;
                 const float x = xv[r];

@@ -487,8 +487,8 @@ __global__ __launch_bounds__(64 * kWideWaves, kWideWGs) void k_fused_nsf_wide(Wi
                     raw_k = (k >= j + 1) ? v : raw_k;
                     raw_k1 = (k >= j) ? v : raw_k1;
                 }
-                const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k * un3, c.min_d);
-                const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1 * un3, c.min_d);
+                const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean_s(raw_k, l2e3, c.min_d);
+                const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean_s(raw_k1, l2e3, c.min_d);
                 const float x = xv[h];
                 const float rw = nfk_rcp_fast(w_k[h]);
                 const float delta = h_k[h] * rw;

@@ -303,10 +303,16 @@ __device__ __forceinline__ nfk_f2 nfk_prefix_nsf_lean2(const float (&raw0)[K], c
 // min_d + softplus(softplus(v)) of NSF_CL + RQS (flows.py:235, utils.py:82) in
 // one step: e^softplus(v) = 1 + e^v, so softplus(softplus(v)) = log(2 + e^v);
 // torch's threshold 20 passes v through both softplus calls unchanged.
-__device__ __forceinline__ float nfk_deriv_lean(float v, float min_d) {
-    const float s = __builtin_amdgcn_logf(2.0f + __builtin_amdgcn_exp2f(v * kL2E)) * kLN2;
-    return min_d + (v > 20.0f ? v : s);
+// raw * sl2e = v log2(e) with v the derivative logit (sl2e = log2(e) times any
+// power-of-two scale raw still carries): min_d + softplus(softplus(v)) as
+// min_d + ln2 * (v log2e > 20 log2e ? v log2e : log2(2 + 2^(v log2e))), the
+// final multiply and add one fma (7 VALU; the round-4 form took 9)
+__device__ __forceinline__ float nfk_deriv_lean_s(float raw, float sl2e, float min_d) {
+    const float a = raw * sl2e;
+    const float t = __builtin_amdgcn_logf(2.0f + __builtin_amdgcn_exp2f(a));
+    return __builtin_fmaf(a > 20.0f * kL2E ? a : t, kLN2, min_d);
 }
+__device__ __forceinline__ float nfk_deriv_lean(float v, float min_d) { return nfk_deriv_lean_s(v, kL2E, min_d); }
 
 template <bool FAST>
 __device__ __forceinline__ float nfk_exp(float x) { return FAST ? nfk_exp_fast(x) : expf(x); }
