@@ -2,8 +2,9 @@
 
 The rule: a kernel that issues MFMAs must not contain
 packed-FP32 VALU instructions (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32)
-unless its register allocation (VGPRs + AGPRs > 256 of the 512 per lane) lets
-only one wave occupy a SIMD.  With dependent MFMA accumulate chains in flight
+unless its register allocation (the unified count the code object reports as
+.vgpr_count -- architectural VGPRs plus AGPRs -- above 256 of the 512 per lane)
+lets only one wave occupy a SIMD.  With dependent MFMA accumulate chains in flight
 on a SIMD, packed-FP32 results in lanes 48-63 of co-resident waves were
 intermittently wrong (tools/ubench_elem_twice.hip reproduces it; the same
 source without packed FP32 never does), so the rule removes the exposure
@@ -42,22 +43,25 @@ def _device_object(obj, tmp):
 
 
 def _registers(dev):
-    """kernel name -> (vgpr_count, agpr_count) from the code object's metadata notes."""
+    """kernel name -> (vgpr_count, agpr_count) from the code object's metadata notes.
+
+    Each kernel is one list item of amdhsa.kernels ("  - " at indent 2); its
+    keys are sorted, so .agpr_count comes before .name: a record is split out
+    whole before any key is read.  On gfx950 .vgpr_count is the unified total
+    (architectural VGPRs, aligned, plus .agpr_count)."""
     out = subprocess.run([_tool("llvm-readelf"), "--notes", dev], check=True, capture_output=True,
                          text=True).stdout
-    regs, cur = {}, {}
-    for line in out.splitlines():
-        line = line.strip().lstrip("- ").strip()
-        m = re.match(r"\.(name|vgpr_count|agpr_count):\s+(\S+)", line)
-        if not m:
-            continue
-        key, val = m.groups()
-        if key == "name":
-            cur = {}
-            regs[val] = cur
-        else:
-            cur[key] = int(val)
-    return {k: (v.get("vgpr_count", 0), v.get("agpr_count", 0)) for k, v in regs.items()}
+    return parse_notes(out)
+
+
+def parse_notes(out):
+    """_registers on the text of `llvm-readelf --notes`."""
+    regs = {}
+    for rec in re.split(r"(?m)^  - ", out)[1:]:
+        kv = dict(re.findall(r"(?m)^(?:|    )\.(\w+):\s+(\S+)", rec))  # the record's own keys, not its args'
+        if "name" in kv:
+            regs[kv["name"]] = (int(kv.get("vgpr_count", 0)), int(kv.get("agpr_count", 0)))
+    return regs
 
 
 def scan(obj):
@@ -87,7 +91,7 @@ def scan(obj):
 
 
 def one_wave_per_simd(r):
-    return r["vgpr"] + r["agpr"] > 256
+    return r["vgpr"] > 256  # .vgpr_count: the unified total (AGPRs included)
 
 
 def violations(objs):
