@@ -219,7 +219,13 @@ __global__ __launch_bounds__(64 * kNsfWaves, 2) void k_nsf_chain2(FusedArgs a) {
             const int t0 = r & ~15;
             const float* src = A->x + (b0 + (r < nall ? r : (t0 < nall ? t0 : 0))) * A->ldx;
             for (int c0 = 0; c0 < D; c0 += 64)
-                if (c0 + lane < D) dma4(src + c0 + lane, base + (r * XS + c0) * 4);
+                if (c0 + lane < D) {
+#if NFK_X_NT
+                    dma4_nt(src + c0 + lane, base + (r * XS + c0) * 4);
+#else
+                    dma4(src + c0 + lane, base + (r * XS + c0) * 4);
+#endif
+                }
         }
     }
     stage_split<KBH, T1, K, HT>(a, pk, 0, offA, offB, offC, slot, wid, lane);

@@ -378,6 +378,23 @@ __device__ __forceinline__ void dma4(const float* gsrc, uint32_t lds) {
                  : "memory");
 }
 
+// dma4 with the non-temporal cache policy: for bytes one workgroup reads once
+// (x rows), so they do not displace the weight records every workgroup re-reads.
+// NFK_X_NT: the chains' x rows (c3, c2) by this policy -- HBM traffic per launch
+// 1.27x -> 1.09x of the algorithmic bytes at c3, 1.14x -> 1.09x at c2, time
+// within 0.3 % (profiles/r5/r5zc_c3_x_nt_ab.txt, r5zd_c2_x_nt_ab.txt)
+#ifndef NFK_X_NT
+#define NFK_X_NT 1
+#endif
+__device__ __forceinline__ void dma4_nt(const float* gsrc, uint32_t lds) {
+    uint32_t saved;  // m0 is reserved by the compiler: restore it
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %2, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(gsrc)
+                 : "memory");
+}
+
 // every DMA and LDS access of this wave retired, then the workgroup barrier
 // Kernels that issue MFMAs and can share a SIMD with other waves are
 // code-generated without packed-FP32 VALU instructions (v_pk_{add,mul,fma}_f32):

@@ -579,7 +579,16 @@ __global__ __launch_bounds__(64 * kNsfWaves, 3) void k_rnvp_chain(RChainArgs a) 
             const int r = i / R4, c = 4 * (i - r * R4);
             const int hf = c >= XI ? 1 : 0, cc = c - hf * XI;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (r < nrows && cc < n) v = *reinterpret_cast<const float4*>(x + (b0 + r) * ldx + hf * n + cc);
+            if (r < nrows && cc < n) {
+                const float4* src = reinterpret_cast<const float4*>(x + (b0 + r) * ldx + hf * n + cc);
+#if NFK_X_NT
+                // read once: the nt policy (see dma4_nt)
+                const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src));
+                v = make_float4(t[0], t[1], t[2], t[3]);
+#else
+                v = *src;
+#endif
+            }
             *reinterpret_cast<float4*>(tile + r * RS + c) = v;
         }
     }
