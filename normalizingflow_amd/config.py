@@ -40,6 +40,11 @@ AR_BATCHED_VJP_BYTES  training: NSF_AR's forward-direction backward recomputes a
                the dim - 1 conditioners, one spline-VJP launch for every column)
                when its activations take at most this many bytes; above it,
                one column at a time.  0: always per column.
+AR_WORKSPACE_BYTES  the streamed NSF_AR forward (shapes like Polymer.yaml's 2,048
+               coordinates) needs a workspace of ~24 KB per row (per-column
+               log|det| terms and the trig operands); a batch whose workspace
+               would exceed this many bytes runs as several launches over
+               row blocks (results bitwise the same: rows are independent).
 """
 STRICT_CHECKS = True
 USE_FUSED = True
@@ -50,3 +55,4 @@ FUSED_VJP_MAX_ROWS = None
 USE_FCNN_DH = True
 USE_FCNN_FWD = True
 AR_BATCHED_VJP_BYTES = 4 << 30
+AR_WORKSPACE_BYTES = 1 << 30

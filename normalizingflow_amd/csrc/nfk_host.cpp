@@ -177,14 +177,16 @@ class ArWatch {
     std::vector<uint32_t> vers_;
 };
 
-// the watch of an NSF_AR layer: its own _parameters dict and init_param, and
-// ar_state's tree (the same stock-shape checks); None when the tree is not
+// the watch of an NSF_AR layer: its own _parameters and _modules dicts (the
+// latter holds `layers`: assigning a new ModuleList changes only it), init_param,
+// and ar_state's tree (the same stock-shape checks); None when the tree is not
 // that shape or the interpreter has no dict version tags
-py::object ar_watch(py::handle layer_params, py::handle layers_modules, py::handle init_param, py::handle fcnn_t,
-                    py::handle linear_t, py::handle tanh_t) {
+py::object ar_watch(py::handle layer_params, py::handle layer_modules, py::handle layers_modules,
+                    py::handle init_param, py::handle fcnn_t, py::handle linear_t, py::handle tanh_t) {
     if (!NFK_DICT_TAGS) return py::none();
     auto w = std::make_unique<ArWatch>();
-    if (!w->add_dict(layer_params.ptr()) || !w->add_tensor(init_param.ptr())) return py::none();
+    if (!w->add_dict(layer_params.ptr()) || !w->add_dict(layer_modules.ptr()) || !w->add_tensor(init_param.ptr()))
+        return py::none();
     PyObject* d = layers_modules.ptr();
     if (!w->add_dict(d)) return py::none();
     PyObject *key, *cond;

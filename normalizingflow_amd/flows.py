@@ -255,6 +255,19 @@ class _HipFlow(nn.Module):
             if name in self.__dict__:
                 self.__dict__[name] = None
 
+    def __getstate__(self):
+        """Copies and pickles (copy.deepcopy, torch.save of the module) carry no
+        derived state: the packs are device buffers keyed on this object's
+        parameters, the fingerprints hold object ids, and NSF_AR's pack watch is
+        a C++ object (csrc/nfk_host.cpp) that neither copies nor pickles."""
+        state = super().__getstate__()
+        for name in _DERIVED_STATE:
+            if name in state:
+                state[name] = None
+        if "_cols" in state:
+            state["_cols"] = {}
+        return state
+
     def _named_param_list(self):
         """[(name, parameter)] for the autograd node (named_parameters order)."""
         return list(self.named_parameters())
@@ -301,6 +314,9 @@ class FCNN(nn.Module):
 
 
 _HOST = []
+
+
+_DERIVED_STATE = ("_pack_cache", "_winv_key", "_vjp_cache", "_ar_tree", "_named_cache", "_ar_names")
 
 
 def _host_helper():
@@ -821,8 +837,8 @@ class NSF_AR(_HipFlow):
         pack, keep = K_.fused_ar_pack(ws, self.init_param, self.dim, hidden, self.K)
         hkey = None
         if hs is not None:
-            hw = hs.ar_watch(self.__dict__["_parameters"], self.layers._modules, self.init_param, FCNN, nn.Linear,
-                             nn.Tanh)
+            hw = hs.ar_watch(self.__dict__["_parameters"], self.__dict__["_modules"], self.layers._modules,
+                             self.init_param, FCNN, nn.Linear, nn.Tanh)
             if hw is None:
                 hw = hs.ar_state(self.layers._modules, self.init_param, FCNN, nn.Linear, nn.Tanh)
                 hw = hw if hw >= 0 else None

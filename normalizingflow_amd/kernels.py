@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, config
 
 F32 = torch.float32
 
@@ -506,17 +506,34 @@ def fused_ar_pack(weights, init_param, dim, hidden, K):
 
 def fused_ar(x, pack, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, inverse=False, status=None,
              split=True):
-    """One fused NSF_AR layer (include/nfk.h nfk_fused_ar_ws; split=False: no
-    column split, the nfk_fused_ar launch)."""
+    """One fused NSF_AR layer (include/nfk.h nfk_fused_ar_ws).  split=False:
+    no column split (the nfk_fused_ar launch) where the shape has the
+    register form; the streamed-only shapes (fused_ar_inverse_supported
+    False) always take their workspace, and a batch whose workspace exceeds
+    config.AR_WORKSPACE_BYTES runs over row blocks."""
     dev = _require_hip(x, pack, out, logdet, status)
     B = x.shape[0]
+    if x.dim() != 2 or x.shape[1] != dim or out.shape != x.shape:
+        raise ValueError("fused_ar: x and out must be [B, %d]" % dim)
+    lib = _lib.load()
+    streamed = not bool(lib.nfk_fused_ar_inverse_supported(dim, hidden, K))
+    if streamed and inverse:
+        raise ValueError("fused_ar: the inverse of this shape is not fused (fused_ar_inverse_supported)")
+    # a batch too small to fill the GPU splits the forward's conditioners over
+    # workgroups; the per-column log|det| terms go through a workspace (and the
+    # streamed form's trig operands)
+    nws = int(lib.nfk_fused_ar_workspace(dim, hidden, K, B, 1 if inverse else 0)) if (split or streamed) else 0
+    if streamed and 4 * nws > config.AR_WORKSPACE_BYTES and B > 64:
+        rows = max(64, int(config.AR_WORKSPACE_BYTES // (4 * nws / B)) // 64 * 64)
+        if rows < B:
+            for r0 in range(0, B, rows):
+                r1 = min(B, r0 + rows)
+                fused_ar(x[r0:r1], pack, dim, hidden, K, tail_bound, out[r0:r1],
+                         logdet=None if logdet is None else logdet[r0:r1], logdet_mode=logdet_mode,
+                         status=status, split=split)
+            return
     xp, ldx = _mat(x, "x")
     op, ldo = _mat(out, "out")
-    if x.shape[1] != dim or out.shape != x.shape:
-        raise ValueError("fused_ar: x and out must be [B, %d]" % dim)
-    # a batch too small to fill the GPU splits the forward's conditioners over
-    # workgroups; the per-column log|det| terms go through a workspace
-    nws = int(_lib.load().nfk_fused_ar_workspace(dim, hidden, K, B, 1 if inverse else 0)) if split else 0
     ws = torch.empty(nws, dtype=F32, device=dev) if nws > 0 else None
     _timed("nfk_fused_ar", dev, "nfk_fused_ar_ws", xp, ldx, pack.data_ptr(), dim, hidden, K, float(tail_bound),
            op, ldo, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0,

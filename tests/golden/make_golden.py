@@ -476,13 +476,42 @@ def negdisc_cl_cases():
     print("model: reference asserts on %d of %d knife-edge rows" % (len(m_rows), n))
 
 
+def _f64_run(layer, inputs):
+    """The fp64 companion of a layer's forward / inverse outputs:
+    {"<out>_f64", "<ld>_f64"} for each (out name -> input) of ``inputs``
+    ("z": forward of the input, anything else: inverse).  Run with fp64 as
+    torch's default dtype, so the reference's own log_det accumulator
+    (``torch.zeros(z.shape[0])``, flows.py:177, 195) is fp64 too: the
+    companion is then the fp64 truth of the sum over every column, not an
+    fp32 sum of fp64 terms.  (trig_transform's ``torch.tensor(np.pi)``,
+    flows.py:173, is then fp64 as well; the fp32 pi moves log|det| by < 1e-8
+    at these shapes.)"""
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        l64 = _f64(layer)
+        out = {}
+        with torch.no_grad():
+            for name, v in inputs.items():
+                fn = l64.forward if name == "z" else l64.inverse
+                o, ld = fn(v.double().clone())
+                assert o.dtype == torch.float64 and ld.dtype == torch.float64
+                ldname = {"z": "ld", "rt_x": "rt_ld", "inv_x": "inv_ld"}[name]
+                out.update({name + "_f64": o, ldname + "_f64": ld})
+        return out
+    finally:
+        torch.set_default_dtype(prev)
+
+
 def case_layer_seeded(name, ctor, kwargs, x, seed=1234):
     """case_layer for a layer too large to commit its weights (the
     applications' NSF_AR: 18 M parameters): the fixture holds the seed and, per
     state_dict entry, the fp64 sum, the fp64 sum of squares and the first 8
     values; tests/golden_io.py rebuilds the weights from the seed through the
     package's own constructor (same init order as the reference) and checks
-    them against these before use."""
+    them against these before use.  With fp64 companions of the forward and
+    both inverses (_f64_run), so a test can tell the reference's own fp32
+    error from ours."""
     torch.manual_seed(seed)
     layer = ctor(**kwargs)
     arrays = dict(x=x)
@@ -493,6 +522,7 @@ def case_layer_seeded(name, ctor, kwargs, x, seed=1234):
         arrays.update(rt_x=xi, rt_ld=ldi)
         xa, lda = layer.inverse(x.clone())
         arrays.update(inv_x=xa, inv_ld=lda)
+    arrays.update(_f64_run(layer, dict(z=x, rt_x=z, inv_x=x)))
     sd = layer.state_dict()
     sums = [torch.stack([v.detach().double().flatten().sum(), v.detach().double().flatten().square().sum()])
             for v in sd.values()]
@@ -526,10 +556,11 @@ def ar_cases():
 
 
 def ar_app_cases():
-    """NSF_AR at the applications' own shape: Einstein.yaml / LJ.yaml / Fe_*.yaml
-    (flow NSF_AR, nsplines 32, hidden_dim 354; nparticles 32 x dim 3 = 96
+    """NSF_AR at the applications' own shape: Einstein.yaml / LJ.yaml (flow
+    NSF_AR, nsplines 32, hidden_dim 354; nparticles 32 x dim 3 = 96
     coordinates, setup.py:48, 57-58), B = (nparticles / (8 rho))^(1/3) at
-    Einstein's rho 1.28 (setup.py:42-43); positions inside the box mostly."""
+    Einstein's rho 1.28 (setup.py:42-43); positions inside the box mostly.
+    (Fe_*.yaml's 54 particles, dim 162, are ar_fe_cases.)"""
     B = (32 / (8 * 1.28)) ** (1.0 / 3.0)
     g = torch.Generator().manual_seed(37)
     x = torch.randn(64, 96, generator=g) * (0.6 * B)

@@ -12,7 +12,11 @@ fixture's seed), nsfar_d2048_k32_h100 (Polymer.yaml: 2048 x 1, nsplines 32,
 hidden 100), plus random ones.  Tolerances: z rtol 1e-5 / atol
 2e-5, log|det| rtol 1e-5 / atol 5e-5 (a sum over dim columns), as in
 test_gpu_parity.py; the inverse conditions on its own outputs, so it is
-compared at 1e-4 absolute where the forward uses 2e-5."""
+compared at 1e-4 absolute where the forward uses 2e-5.  Where a log|det|
+(a sum over up to 2,048 columns) misses 5e-5, the fp64 truth decides
+(test_gpu_parity.close_or_on_par: our max and p99 error against it within
+2x the fp32 reference's own) -- the fixtures' fp64 companions, or the
+oracle run in fp64 on the same inputs."""
 import pytest
 import torch
 
@@ -22,6 +26,7 @@ import nf.models as nfm
 from normalizingflow_amd import config, flush_status_checks
 from normalizingflow_amd import kernels as K_
 from oracle import nf_oracle as orc
+from test_gpu_parity import close_or_on_par
 
 pytestmark = pytest.mark.gpu
 
@@ -35,6 +40,18 @@ def close(a, b, rtol, atol):
 
 def _sd(layer):
     return {k: v.detach().cpu() for k, v in layer.state_dict().items()}
+
+
+def _f64(sd):
+    return {k: v.double() for k, v in sd.items()}
+
+
+def _oracle_ar(x, sd, dim, K, B, inverse=False):
+    """(out, log|det|) of the oracle in fp32 and its fp64 truth: (o32, l32, o64, l64)."""
+    with torch.no_grad():
+        o, l = orc.nsf_ar(x, sd, "", dim, K, B, inverse=inverse)
+        o64, l64 = orc.nsf_ar(x.double(), _f64(sd), "", dim, K, B, inverse=inverse)
+    return o, l, o64, l64
 
 
 def _launches(fn):
@@ -61,14 +78,13 @@ def test_fused_ar_vs_reference_golden(name, hip_device):
         (z, ld), n = _launches(lambda: layer(x))
         assert n == {"nfk_fused_ar": 1}, n  # the whole layer is one launch
         close(z, data["z"], Z_RTOL, Z_ATOL)
-        # log|det| sums dim columns: its slack grows with dim (5e-5 up to 40 columns)
-        close(ld, data["ld"], LD_RTOL, LD_ATOL * max(1.0, kw["dim"] / 40.0))
+        close_or_on_par(ld, data["ld"], data.get("ld_f64"), LD_RTOL, LD_ATOL)
         xi, ldi = layer.inverse(z)
         close(xi, data["rt_x"], 1e-5, 1e-4)
-        close(ldi, data["rt_ld"], 1e-5, 1e-4)
+        close_or_on_par(ldi, data["rt_ld"], data.get("rt_ld_f64"), LD_RTOL, LD_ATOL)
         xa, lda = layer.inverse(x)
         close(xa, data["inv_x"], 1e-5, 1e-4)
-        close(lda, data["inv_ld"], 1e-5, 1e-4)
+        close_or_on_par(lda, data["inv_ld"], data.get("inv_ld_f64"), LD_RTOL, LD_ATOL)
     flush_status_checks()
 
 
@@ -85,9 +101,8 @@ def test_fused_ar_vs_oracle_and_unfused(dim, K, H, B, rows, hip_device):
     sd = _sd(layer)
     layer = layer.to(hip_device)
     x = torch.randn(rows, dim, generator=torch.Generator().manual_seed(dim)) * 1.3
-    with torch.no_grad():
-        z_ref, ld_ref = orc.nsf_ar(x, sd, "", dim, K, B)
-        xi_ref, ldi_ref = orc.nsf_ar(x, sd, "", dim, K, B, inverse=True)
+    z_ref, ld_ref, _, ld64 = _oracle_ar(x, sd, dim, K, B)
+    xi_ref, ldi_ref, _, ldi64 = _oracle_ar(x, sd, dim, K, B, inverse=True)
     xd = x.to(hip_device)
     with torch.no_grad():
         assert layer._fused_pack(xd.device) is not None
@@ -100,14 +115,12 @@ def test_fused_ar_vs_oracle_and_unfused(dim, K, H, B, rows, hip_device):
             zu, ldu = layer(xd)
         finally:
             config.USE_FUSED = prev
-    # log|det| sums dim columns: its slack grows with dim (5e-5 up to 40 columns)
-    ld_atol = LD_ATOL * max(1.0, dim / 40.0)
     close(z, z_ref, Z_RTOL, Z_ATOL)
-    close(ld, ld_ref, LD_RTOL, ld_atol)
+    close_or_on_par(ld, ld_ref, ld64, LD_RTOL, LD_ATOL)
     close(zu, z_ref, Z_RTOL, Z_ATOL)
-    close(ldu, ld_ref, LD_RTOL, ld_atol)
+    close_or_on_par(ldu, ld_ref, ld64, LD_RTOL, LD_ATOL)
     close(xi, xi_ref, 1e-5, 1e-4)
-    close(ldi, ldi_ref, 1e-5, 1e-4)
+    close_or_on_par(ldi, ldi_ref, ldi64, LD_RTOL, LD_ATOL)
     flush_status_checks()
 
 
@@ -200,10 +213,9 @@ def test_fused_ar_column_split_bitwise(dim, K, H, B, rows, hip_device):
     if rows > 333 or rows < 40:
         return  # (one row: some column has no element inside [-B, B], where the reference raises)
     # and the oracle on the split result
-    with torch.no_grad():
-        z_ref, ld_ref = orc.nsf_ar(x.cpu(), _sd(layer), "", dim, K, B)
+    z_ref, ld_ref, _, ld64 = _oracle_ar(x.cpu(), _sd(layer), dim, K, B)
     close(res[True][0], z_ref, Z_RTOL, Z_ATOL)
-    close(res[True][1], ld_ref, LD_RTOL, LD_ATOL * max(1.0, dim / 40.0))
+    close_or_on_par(res[True][1], ld_ref, ld64, LD_RTOL, LD_ATOL)
 
 
 @pytest.mark.parametrize("dim,K,H,B,rows", [(96, 32, 354, 1.462, 40), (40, 10, 80, 4.0, 1000), (5, 4, 16, 3.0, 77)])
@@ -261,8 +273,11 @@ def test_fe162_forward_one_launch_and_speed(hip_device):
     import time
     B = 3 * 2.8841 / 2
     torch.manual_seed(54)
-    layer = nff.NSF_AR(dim=162, K=32, B=B, hidden_dim=354).to(hip_device)
-    x = torch.randn(50, 162, device=hip_device) * (0.6 * B)
+    layer = nff.NSF_AR(dim=162, K=32, B=B, hidden_dim=354)
+    sd = _sd(layer)
+    layer = layer.to(hip_device)
+    xc = torch.randn(50, 162, generator=torch.Generator().manual_seed(54)) * (0.6 * B)
+    x = xc.to(hip_device)
     with torch.no_grad():
         (z, ld), n = _launches(lambda: layer(x))
         assert n == {"nfk_fused_ar": 1}, n
@@ -286,8 +301,10 @@ def test_fe162_forward_one_launch_and_speed(hip_device):
         finally:
             config.USE_FUSED = prev
             layer.invalidate_caches()
-    close(z, zu, Z_RTOL, Z_ATOL)
-    close(ld, ldu, LD_RTOL, LD_ATOL * 162 / 40.0)
+    z_ref, ld_ref, _, ld64 = _oracle_ar(xc, sd, 162, 32, B)
+    for zz, ll in ((z, ld), (zu, ldu)):
+        close(zz, z_ref, Z_RTOL, Z_ATOL)
+        close_or_on_par(ll, ld_ref, ld64, LD_RTOL, LD_ATOL)
     print("fe162 forward at 50 rows: fused %.3f ms, per-column %.3f ms (%.1fx)"
           % (t_fused * 1e3, t_col * 1e3, t_col / t_fused))
     assert t_col >= 10 * t_fused, (t_fused, t_col)
@@ -304,13 +321,13 @@ def test_polymer2048_vs_reference_golden(hip_device):
     with torch.no_grad():
         z, ld = layer(x)
         close(z, data["z"], Z_RTOL, Z_ATOL)
-        close(ld, data["ld"], LD_RTOL, 2e-3)  # a sum over 2048 columns
+        close_or_on_par(ld, data["ld"], data["ld_f64"], LD_RTOL, LD_ATOL)  # a sum over 2048 columns
         xi, ldi = layer.inverse(z)
         close(xi, data["rt_x"], 1e-5, 1e-4)
-        close(ldi, data["rt_ld"], 1e-5, 2e-3)
+        close_or_on_par(ldi, data["rt_ld"], data["rt_ld_f64"], LD_RTOL, LD_ATOL)
         xa, lda = layer.inverse(x)
         close(xa, data["inv_x"], 1e-5, 1e-4)
-        close(lda, data["inv_ld"], 1e-5, 2e-3)
+        close_or_on_par(lda, data["inv_ld"], data["inv_ld_f64"], LD_RTOL, LD_ATOL)
     flush_status_checks()
 
 
@@ -367,9 +384,9 @@ def test_polymer2048_forward_one_launch_and_speed(hip_device):
     with torch.no_grad():
         (z, ld), n = _launches(lambda: layer(xd))
         assert n == {"nfk_fused_ar": 1}, n
-        z_ref, ld_ref = orc.nsf_ar(x, sd, "", 2048, 32, 0.5)
+        z_ref, ld_ref, _, ld64 = _oracle_ar(x, sd, 2048, 32, 0.5)
         close(z, z_ref, Z_RTOL, Z_ATOL)
-        close(ld, ld_ref, LD_RTOL, 2e-3)
+        close_or_on_par(ld, ld_ref, ld64, LD_RTOL, LD_ATOL)
 
         def timed(fn, reps):
             fn()
@@ -392,4 +409,85 @@ def test_polymer2048_forward_one_launch_and_speed(hip_device):
     print("poly2048 forward at 40 rows: fused %.3f ms, per-column %.3f ms (%.1fx)"
           % (t_fused * 1e3, t_col * 1e3, t_col / t_fused))
     assert t_col >= 10 * t_fused, (t_fused, t_col)
+    flush_status_checks()
+
+
+def test_fused_ar_deepcopy_after_forward(hip_device):
+    """copy.deepcopy of a layer after a fused forward (its pack cache holds the
+    C++ watch): the copy gives bitwise the original's output, and an update to
+    the copy's weights changes the copy only."""
+    import copy
+    torch.manual_seed(9)
+    layer = nff.NSF_AR(dim=24, K=8, B=3.0, hidden_dim=64).to(hip_device)
+    x = torch.randn(300, 24, device=hip_device)
+    with torch.no_grad():
+        z, ld = layer(x)
+        c = copy.deepcopy(layer)
+        zc, ldc = c(x)
+        assert torch.equal(z, zc) and torch.equal(ld, ldc)
+        c.layers[10].network[4].bias.add_(0.5)
+        zc2, _ = c(x)
+        z2, ld2 = layer(x)
+    assert not torch.equal(zc2, z)
+    assert torch.equal(z2, z) and torch.equal(ld2, ld)
+    flush_status_checks()
+
+
+def test_polymer2048_row_blocks_bitwise(hip_device):
+    """The streamed form's workspace (~24 KB per row at 2,048 coordinates) is
+    capped by config.AR_WORKSPACE_BYTES: a batch over the cap runs as launches
+    over row blocks, bitwise the one-launch result; split=False takes the
+    workspace too (the streamed shapes have no workspace-free launch)."""
+    torch.manual_seed(4)
+    layer = nff.NSF_AR(dim=2048, K=32, B=0.5, hidden_dim=100).to(hip_device)
+    x = torch.randn(300, 2048, device=hip_device) * 0.3
+    pack = layer._fused_pack(x.device)
+    per_row = 4 * K_._lib.load().nfk_fused_ar_workspace(2048, 100, 32, 300, 0) / 300
+    res = []
+    for cap, split, nl in ((1 << 40, True, 1), (int(per_row * 100), True, 5), (1 << 40, False, 1)):
+        prev = config.AR_WORKSPACE_BYTES
+        config.AR_WORKSPACE_BYTES = cap
+        try:
+            z = torch.empty_like(x)
+            ld = torch.full((300,), 1.5, device=hip_device)
+            st = torch.zeros(2048, dtype=torch.int32, device=hip_device)
+            (_, n) = _launches(lambda: K_.fused_ar(x, pack, 2048, 100, 32, 0.5, z, logdet=ld, logdet_mode=2,
+                                                  status=st, split=split))
+        finally:
+            config.AR_WORKSPACE_BYTES = prev
+        assert n == {"nfk_fused_ar": nl}, (cap, n)
+        res.append((z, ld, st))
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dim,H,B,rows", [(96, 354, (32 / (8 * 1.28)) ** (1.0 / 3.0), 40),
+                                          (162, 354, 3 * 2.8841 / 2, 50), (2048, 100, 0.5, 40)])
+def test_fused_ar_app_model_log_prob(dim, H, B, rows, hip_device):
+    """A 2-layer NSF_AR model at the applications' shapes (Einstein/LJ dim 96,
+    Fe dim 162, Polymer dim 2048) and their training batches: log_prob
+    (models.py:37-40) against the oracle at the north star's rtol 1e-5, and
+    our error against the oracle's fp64 run within 2x the oracle's own fp32
+    error where the 1e-5 agreement is not bitwise."""
+    torch.manual_seed(dim + 1)
+    flows = [nff.NSF_AR(dim=dim, K=32, B=B, hidden_dim=H) for _ in range(2)]
+    model = nfm.NormalizingFlowModel(torch.distributions.MultivariateNormal(torch.zeros(dim), torch.eye(dim)),
+                                     flows)
+    sd = _sd(model)
+    specs = [dict(type="NSF_AR", prefix="flows.%d." % i, dim=dim, K=32, B=B) for i in range(2)]
+    x = torch.randn(rows, dim, generator=torch.Generator().manual_seed(dim)) * (0.6 * B)
+    with torch.no_grad():
+        ref = orc.model_log_prob(specs, sd, x)
+        ref64 = orc.model_log_prob(specs, _f64(sd), x.double())
+    model = model.to(hip_device)
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(dim, device=hip_device),
+                                                        torch.eye(dim, device=hip_device))
+    (lp, n) = _launches(lambda: model.log_prob(x.to(hip_device)))
+    assert n.get("nfk_fused_ar") == 2, n
+    close(lp, ref, 1e-5, 1e-5)
+    e_ours = float((lp.cpu().double() - ref64).abs().max())
+    e_ref = float((ref.double() - ref64).abs().max())
+    print("dim %d log_prob: max |ours - fp64| %.3g, max |oracle fp32 - fp64| %.3g" % (dim, e_ours, e_ref))
+    assert e_ours <= 2 * e_ref + 1e-5 * float(ref64.abs().max()), (e_ours, e_ref)
     flush_status_checks()

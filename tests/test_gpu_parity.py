@@ -55,6 +55,27 @@ def on_par(ours, ref, truth, rtol=1e-5, atol=2e-5, within=0.99, factor=4.0):
     assert qo <= factor * qr + 1e-6, (qo, qr)
 
 
+def close_or_on_par(ours, ref, truth, rtol, atol, factor=2.0):
+    """NSF_AR outputs that sum or chain through hundreds to thousands of
+    columns (log|det|: a sum over dim columns; the inverse: conditioned on
+    its own outputs): within rtol/atol of the reference, or -- only where the
+    fixture holds the fp64 truth -- our max and p99 error against that truth
+    within ``factor``x the reference's own fp32 error (the
+    reference's fp32 log|det| at Polymer's 2,048 columns is itself 1.4e-4 off
+    its fp64 value, a bias that grows with dim)."""
+    if truth is not None:
+        o, r, t = ours.detach().cpu().double(), ref.detach().cpu().double(), truth.double()
+        print("close_or_on_par: max |ours - ref| %.3g; vs fp64 max ours %.3g ref %.3g, p99 ours %.3g ref %.3g"
+              % ((o - r).abs().max(), (o - t).abs().max(), (r - t).abs().max(),
+                 torch.quantile((o - t).abs().flatten(), 0.99), torch.quantile((r - t).abs().flatten(), 0.99)))
+    try:
+        close(ours, ref, rtol, atol)
+    except AssertionError:
+        if truth is None:
+            raise
+        on_par(ours, ref, truth, rtol, atol, within=0.0, factor=factor)
+
+
 def build_layer(meta):
     kw = dict(meta["kwargs"])
     if meta["type"] == "Planar":
@@ -100,23 +121,22 @@ def test_layer_vs_reference_golden(name, hip_device):
     layer = build_layer(meta)
     gio.load_into(layer, sd)
     layer = layer.to(hip_device)
-    # NSF_AR sums dim log|det| terms (the slack grows with dim: 5e-5 up to 40
-    # columns) and its inverse conditions on its own outputs through dim - 1
-    # conditioners (test_gpu_nsfar_fused.py's 1e-4)
-    ar = meta["type"] == "NSF_AR"
-    ld_atol = LD_ATOL * max(1.0, meta["kwargs"].get("dim", 0) / 40.0) if ar else LD_ATOL
-    inv_atol = 1e-4 if ar else 5e-5
+    # the fp64 truth of every output (make_golden.py _f64_run: fp64 log_det
+    # accumulator too) in the seeded applications-shape NSF_AR fixtures; the
+    # others must agree with the reference outright
+    seeded = meta.get("sd_from_seed", False)
+    t = {k: d.get(k + "_f64") if seeded else None for k in ("ld", "rt_x", "rt_ld", "inv_x", "inv_ld")}
     with torch.no_grad():
         z, ld = layer(d["x"].to(hip_device))
         close(z, d["z"], Z_RTOL, Z_ATOL)
-        close(ld, d["ld"], LD_RTOL, ld_atol)
+        close_or_on_par(ld, d["ld"], t["ld"], LD_RTOL, LD_ATOL)
         if "rt_x" in d:
             xi, ldi = layer.inverse(d["z"].to(hip_device))
-            close(xi, d["rt_x"], Z_RTOL, inv_atol)
-            close(ldi, d["rt_ld"], LD_RTOL, ld_atol)
+            close_or_on_par(xi, d["rt_x"], t["rt_x"], Z_RTOL, 5e-5)
+            close_or_on_par(ldi, d["rt_ld"], t["rt_ld"], LD_RTOL, LD_ATOL)
             xa, lda = layer.inverse(d["x"].to(hip_device))
-            close(xa, d["inv_x"], Z_RTOL, inv_atol)
-            close(lda, d["inv_ld"], LD_RTOL, ld_atol)
+            close_or_on_par(xa, d["inv_x"], t["inv_x"], Z_RTOL, 5e-5)
+            close_or_on_par(lda, d["inv_ld"], t["inv_ld"], LD_RTOL, LD_ATOL)
 
 
 def _golden_model(meta, sd, device):

@@ -69,12 +69,13 @@ def test_ar_state_fast_at_polymer_size(hs):
 
 
 def _watch(hs, layer):
-    return hs.ar_watch(layer.__dict__["_parameters"], layer.layers._modules, layer.init_param, nff.FCNN, nn.Linear,
-                       nn.Tanh)
+    return hs.ar_watch(layer.__dict__["_parameters"], layer.__dict__["_modules"], layer.layers._modules,
+                       layer.init_param, nff.FCNN, nn.Linear, nn.Tanh)
 
 
 @pytest.mark.parametrize("change", ["inplace", "init_inplace", "init_replaced", "linear_replaced", "tanh_replaced",
-                                    "param_replaced", "data_assigned", "cond_replaced", "cond_appended"])
+                                    "param_replaced", "data_assigned", "cond_replaced", "cond_appended",
+                                    "layers_replaced"])
 def test_ar_watch_invalidated_by_every_change(hs, change):
     """The watch (dict version tags + parameter storage/version) turns invalid
     on each change that alters the pack key, and stays valid otherwise."""
@@ -102,6 +103,10 @@ def test_ar_watch_invalidated_by_every_change(hs, change):
         layer.layers[6] = nff.FCNN(14, 11, 16)
     elif change == "cond_appended":
         layer.layers.append(nff.FCNN(24, 11, 16))
+    elif change == "layers_replaced":
+        # a new ModuleList lives in the layer's own _modules dict, outside the
+        # conditioner tree the watch walked
+        layer.layers = nn.ModuleList([nff.FCNN(2 * i, 11, 16) for i in range(1, 12)])
     assert not w.valid()
 
 
@@ -124,3 +129,25 @@ def test_ar_watch_fast_at_polymer_size(hs):
         assert w.valid()
     dt = (time.perf_counter() - t0) / 10
     assert dt < 5e-3, dt
+
+
+def test_copies_and_pickles_drop_the_watch(hs):
+    """A layer holding the watch a fused GPU forward leaves behind (the C++
+    ArWatch in _pack_cache) deep-copies and pickles: the copy carries no derived
+    state and rebuilds its own pack; the original keeps its cache."""
+    import copy
+    import pickle
+    torch.manual_seed(0)
+    layer = nff.NSF_AR(dim=6, K=4, B=3.0, hidden_dim=16)
+    w = _watch(hs, layer)
+    layer._pack_cache = (("cpu", ()), torch.zeros(4), 16, None, ("cpu", w))
+    layer._stock_linears()
+    layer._named_param_list()
+    for c in (copy.deepcopy(layer), pickle.loads(pickle.dumps(layer))):
+        assert c._pack_cache is None and c._ar_tree is None and c.__dict__.get("_named_cache") is None
+        assert c._cols == {}
+        sd, sc = layer.state_dict(), c.state_dict()
+        assert sd.keys() == sc.keys() and all(torch.equal(sd[k], sc[k]) for k in sd)
+        assert len(c._stock_linears()) == 3 * 5
+        assert [n for n, _ in c._named_param_list()] == [n for n, _ in layer.named_parameters()]
+    assert layer._pack_cache[4][1] is w and w.valid()

@@ -55,11 +55,28 @@ def test_layer_fixture(name):
         xa, lda = orc.apply_layer(spec, d["x"], sd, inverse=True)
         _close(xa, d["inv_x"], atol=at); _close(lda, d["inv_ld"], atol=at)
     if "z_f64" in d:
-        sd64 = {k: v.double() for k, v in sd.items()}
-        z64, ld64 = orc.apply_layer(spec, d["x"].double(), sd64)
-        _close(z64, d["z_f64"], rtol=1e-12, atol=1e-12)
-        # the reference accumulates NSF_CL's log_det in an fp32 zeros() buffer (flows.py:228)
-        _close(ld64.to(d["ld_f64"].dtype).expand_as(d["ld_f64"]), d["ld_f64"], rtol=1e-6, atol=1e-5)
+        # the seeded applications-shape NSF_AR fixtures' fp64 companions ran with
+        # fp64 as torch's default dtype (make_golden.py _f64_run: fp64 log_det
+        # accumulator, and torch.tensor(np.pi) in fp64): the oracle likewise
+        seeded = meta.get("sd_from_seed", False)
+        prev = torch.get_default_dtype()
+        if seeded:
+            torch.set_default_dtype(torch.float64)
+        try:
+            sd64 = {k: v.double() for k, v in sd.items()}
+            z64, ld64 = orc.apply_layer(spec, d["x"].double(), sd64)
+            _close(z64, d["z_f64"], rtol=1e-12, atol=1e-12)
+            if seeded:
+                _close(ld64, d["ld_f64"], rtol=1e-10, atol=1e-10)
+                for src, o, l in ((d["z"], "rt_x", "rt_ld"), (d["x"], "inv_x", "inv_ld")):
+                    xi64, ldi64 = orc.apply_layer(spec, src.double(), sd64, inverse=True)
+                    _close(xi64, d[o + "_f64"], rtol=1e-10, atol=1e-10)
+                    _close(ldi64, d[l + "_f64"], rtol=1e-10, atol=1e-10)
+            else:
+                # the reference accumulates NSF_CL's log_det in an fp32 zeros() buffer (flows.py:228)
+                _close(ld64.to(d["ld_f64"].dtype).expand_as(d["ld_f64"]), d["ld_f64"], rtol=1e-6, atol=1e-5)
+        finally:
+            torch.set_default_dtype(prev)
 
 
 def _model_specs(meta):
