@@ -590,8 +590,22 @@ def ar_polymer_cases():
     case_layer_seeded("nsfar_d2048_k32_h100", rflows.NSF_AR, dict(dim=2048, K=32, B=0.5, hidden_dim=100), x)
 
 
+def rnvp_polymer_cases():
+    """RealNVP at Polymer_rnvp.yaml's shape (applications/input/Polymer_rnvp.yaml:
+    8-9, 16-18: nparticles 2048 x dim 1, RealNVP with hidden_dim 4000; the
+    driver applications/examples/polymer.py:29 loads this config) at the
+    config's 40-row batch (:30).  Four FCNN(1024, 1024, 4000) conditioners,
+    96.8 M parameters: rebuilt from the seed.  Inputs at the prior's scale
+    (vars 0.1, :24)."""
+    g = torch.Generator().manual_seed(47)
+    x = torch.randn(40, 2048, generator=g) * 0.1 ** 0.5
+    case_layer_seeded("realnvp_d2048_h4000", rflows.RealNVP, dict(dim=2048, hidden_dim=4000), x)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["ar_fe"]:
+    if sys.argv[1:] == ["rnvp_polymer"]:
+        rnvp_polymer_cases()
+    elif sys.argv[1:] == ["ar_fe"]:
         ar_fe_cases()
     elif sys.argv[1:] == ["ar_polymer"]:
         ar_polymer_cases()
