@@ -125,3 +125,19 @@ def test_streamed_ar_reproducible(hip_device):
         lib.nfk_debug_ar_stream(prev)
         layer.invalidate_caches()
     flush_status_checks()
+
+
+@pytest.mark.parametrize("dim,B", [(96, (32 / (8 * 1.28)) ** (1.0 / 3.0)), (162, 3 * 2.8841 / 2)])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_fused_ar_h354_reproducible(dim, B, inverse, hip_device):
+    """The one-wave-per-SIMD NSF_AR instances that keep packed FP32 (the
+    build rule's exemption, DESIGN.md section 10.5: k_fused_ar<11, ...> at the
+    applications' hidden 354 -- Einstein/LJ dim 96, Fe dim 162), forward and
+    inverse, at 2^16 + 77 rows: every SIMD of the chip busy several rounds
+    over; three runs bitwise equal."""
+    torch.manual_seed(8 + dim)
+    layer = nff.NSF_AR(dim=dim, K=32, B=B, hidden_dim=354).to(hip_device)
+    x = torch.randn((1 << 16) + 77, dim, device=hip_device) * (0.6 * B)
+    assert layer._fused_pack(x.device) is not None
+    _assert_same(_runs(lambda: layer.inverse(x) if inverse else layer(x)))
+    flush_status_checks()
