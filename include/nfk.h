@@ -482,6 +482,36 @@ int nfk_fcnn_linear(const float* x, int64_t ldx, int32_t P, const float* pack, c
                     int32_t tanh_out, int32_t H, float* out, int64_t ldo, int64_t batch,
                     nfk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * RealNVP layers with wide conditioners at small batches (nfk_wide_rnvp.hip):
+ * applications/input/Polymer_rnvp.yaml's RealNVP(2048, hidden 4000) at the
+ * config's 40 rows and the driver's sample(100) (applications/examples/
+ * polymer.py:29,37-41).  Replaces RealNVP.forward / inverse (nf/flows.py:52-76)
+ * with its four FCNN conditioners (flows.py:20-35) when the layer is the
+ * weight stream: every weight read once per layer.
+ *
+ * nfk_wlin_pack: an nn.Linear weight W [N, K] (out x in, row-major) re-packed
+ * once into nfk_wlin_pack_floats(N, K) floats (fp16 hi/lo MFMA fragments of
+ * 2^s W, one power of two per matrix).
+ *
+ * nfk_wide_rnvp: one RealNVP layer.  packs / biases: 12 device pointers each,
+ * [6 c + 2 l + g] for half-coupling c (0: s1/t1, 1: s2/t2), Linear l (0, 1, 2
+ * = network.0, .2, .4) and conditioner g (0 = s, 1 = t); biases are the
+ * Linears' fp32 bias vectors.  x [batch, 2 half] (row stride ldx) -> z (ldz;
+ * may equal x), logdet mode 0 none / 1 write / 2 accumulate (forward +sum s,
+ * inverse -sum s, flows.py:61-62, 74-75).  workspace: at least
+ * nfk_wide_rnvp_workspace(half, hidden, batch) floats, 16-byte aligned.  Rows
+ * are processed 128 per pass (every pass streams the weights once).
+ * half and hidden multiples of 4 (nfk_wide_rnvp_supported).
+ * ------------------------------------------------------------------------- */
+int64_t nfk_wlin_pack_floats(int32_t N, int32_t K);
+int nfk_wlin_pack(const float* W, int32_t N, int32_t K, float* pack, nfk_stream_t stream);
+int nfk_wide_rnvp_supported(int32_t half, int32_t hidden);
+int64_t nfk_wide_rnvp_workspace(int32_t half, int32_t hidden, int64_t batch);
+int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const float* const* biases, int32_t half,
+                  int32_t hidden, float* z, int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
+                  int32_t inverse, float* workspace, int64_t workspace_floats, nfk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,11 @@ AR_WORKSPACE_BYTES  the streamed NSF_AR forward (shapes like Polymer.yaml's 2,04
                log|det| terms and the trig operands); a batch whose workspace
                would exceed this many bytes runs as several launches over
                row blocks (results bitwise the same: rows are independent).
+USE_WIDE_RNVP  RealNVP layers whose conditioners are too wide for the fused kernel
+               (Polymer_rnvp.yaml: hidden 4000) run as a weight stream
+               (nfk_wide_rnvp: every Linear packed once, each weight read once
+               per layer) at batches of at most WIDE_RNVP_MAX_ROWS rows (128 per
+               pass); larger batches, or off: library GEMMs + the affine kernel.
 """
 STRICT_CHECKS = True
 USE_FUSED = True
@@ -56,3 +61,5 @@ USE_FCNN_DH = True
 USE_FCNN_FWD = True
 AR_BATCHED_VJP_BYTES = 4 << 30
 AR_WORKSPACE_BYTES = 1 << 30
+USE_WIDE_RNVP = True
+WIDE_RNVP_MAX_ROWS = 1024

@@ -1,0 +1,635 @@
+// nfk_wide_rnvp.hip -- RealNVP layers with wide conditioners at small batches:
+// applications/input/Polymer_rnvp.yaml's flow (RealNVP(2048, hidden 4000) x 10,
+// batch 40; the driver, applications/examples/polymer.py:29,37-41, samples 100
+// rows and evaluates them), nf/flows.py:44-76 over FCNN conditioners (20-35).
+//
+// At 40-128 rows a layer is its weights: 4 FCNN(1024, 1024, 4000) = 96.8 M
+// parameters (387 MB) against 40 x 2048 x 4 B of x.  Every weight is read once
+// per layer launch sequence, so the floor is the HBM stream (48 us per layer
+// at 8 TB/s).  Per half-coupling (s and t conditioners of one input run side
+// by side as the two "groups" of every stage):
+//
+//   k_wl_rows   x half -> fp16 hi/lo B fragments of the input, per-row 2^e scale
+//   k_wl_gemm   L1: [M, half] x W1^T for s and t     -> split-K partial sums
+//   k_wl_act    sum the partials, unscale, + b1, tanh -> hi/lo fragments (2^14)
+//   k_wl_gemm   L2: [M, H] x W2^T (s, t)              -> partials
+//   k_wl_act    + b2, tanh                             -> fragments
+//   k_wl_gemm   L3: [M, H] x W3^T (s, t)              -> partials
+//   k_wl_rows   s, t = partials + b3; the affine coupling (flows.py:56, 59 /
+//               69, 72), log|det| += (-)sum s per row (fixed order), and the
+//               fragments of the output half: the next half-coupling's input
+//
+// GEMM (k_wl_gemm): weights packed once (nfk_wlin_pack) as the A operand of
+// v_mfma_f32_16x16x32_f16 in the two-way fp16 split of the fused kernels
+// (hi = f16(2^s w), lo = f16(2^s w - hi); products lo.hi + hi.lo + hi.hi in
+// fp32 accumulators; 2^s puts max|W| just under 2^15), 16 output features x 32
+// k per 2-KiB (hi, lo) block, the blocks of one 16-feature tile contiguous over
+// k.  A workgroup = 4 waves (one per SIMD) owns 4 NTW output tiles of one group
+// and a chunk of KC k-blocks: the chunk's input fragments (MT sample tiles)
+// are copied into LDS once (LDS-DMA) and shared by the 4 waves; each wave
+// streams its NTW tiles' weights from HBM straight into registers, kWlPF
+// k-blocks ahead, and writes fp32 partial sums [group][split][row][feature].
+// The split count is chosen so the grid covers every CU (>= 256 workgroups)
+// with as few partial sums as that allows; they are summed in split order by
+// the next stage (deterministic, bitwise reproducible).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/nfk.h"
+
+int nfk_set_error(const char* msg);  // nfk_kernels.hip
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWlWaves = 4;                    // waves per GEMM workgroup (one per SIMD)
+constexpr int kWlPF = 8;                       // k-blocks of weights in flight per wave
+constexpr int kWlMaxMT = 8;                    // sample tiles per pass: 128 rows
+constexpr int kWlHdr = 64;                     // pack header floats ([0] = 2^-s)
+constexpr size_t kWlLdsMax = 128 * 1024;       // the input chunk of one GEMM workgroup
+constexpr float kWlAct = 16384.0f;             // tanh outputs split at 2^14
+constexpr int kWlTarget = 256;                 // GEMM workgroups: at least one per CU
+// the weight stream's loads non-temporal (every weight is read once per layer)
+#ifndef NFK_WL_NT
+#define NFK_WL_NT 1
+#endif
+
+int wl_status(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        nfk_set_error(what);
+        return (int)e;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// one 16-byte LDS-DMA per lane (global_load_lds_dwordx4; m0 = the LDS base of
+// the wave's 1-KiB block, restored after: the compiler reserves m0)
+__device__ __forceinline__ void dma16(const float4* gsrc, uint32_t lds) {
+    uint32_t saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(gsrc)
+                 : "memory");
+}
+
+// ---------------------------------------------------------------------------
+// pack: float[0] = 2^-s (exact), float[1] = max|W| (bits, atomicMax), body
+// from float kWlHdr: halfs [nt][kb][part][lane][8] = part of 2^s W[16 nt +
+// (lane & 15)][32 kb + 8 (lane >> 4) + j] (zero outside N x K), then one
+// all-zero 2-KiB block
+__global__ __launch_bounds__(256) void k_wl_max(const float* __restrict__ W, int64_t n, float* pack) {
+    float mx = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        mx = fmaxf(mx, fabsf(W[i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    if ((threadIdx.x & 63) == 0 && mx > 0.0f)
+        atomicMax(reinterpret_cast<int*>(pack) + 1, __float_as_int(fminf(mx, 3.0e38f)));
+}
+
+__global__ __launch_bounds__(256) void k_wl_pack(const float* __restrict__ W, int N, int K, int KB, int64_t units,
+                                                 float* pack) {
+    const float mx = __int_as_float(reinterpret_cast<const int*>(pack)[1]);
+    int ex = 0;
+    if (mx > 0.0f) frexpf(mx, &ex);  // mx < 2^ex
+    const float s = ldexpf(1.0f, 15 - ex);
+    if (blockIdx.x == 0 && threadIdx.x == 0) pack[0] = ldexpf(1.0f, ex - 15);
+    h8* body = reinterpret_cast<h8*>(pack + kWlHdr);
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(u & 63), part = (int)((u >> 6) & 1);
+        const int64_t blk = u >> 7;  // nt KB + kb
+        const int kb = (int)(blk % KB), nt = (int)(blk / KB);
+        const int n = 16 * nt + (lane & 15), k0 = 32 * kb + 8 * (lane >> 4);
+        h8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float w = (n < N && k0 + j < K) ? W[(int64_t)n * K + k0 + j] * s : 0.0f;
+            const _Float16 hi = (_Float16)w;
+            v[j] = part == 0 ? hi : (_Float16)(w - (float)hi);
+        }
+        body[u] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+struct WlGemm {
+    const float* pack[2];  // the two groups' packs (s, t)
+    const float* xf[2];    // their input fragments: halfs [mt][kb][part][lane][8]
+    float* part;           // fp32 partial sums [group][split][row][feature]
+    int N, NT, KB;         // features per group, their 16-tiles, k-blocks
+    int KS, KC, M, nblk;   // splits, k-blocks per split, rows, feature blocks per group
+};
+
+template <int MT, int NTW>
+__global__ __launch_bounds__(64 * kWlWaves, 1) void k_wl_gemm(WlGemm a) {
+    extern __shared__ __attribute__((aligned(16))) float4 xs[];  // [MT][KC][part][64]
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int b = blockIdx.x;
+    const int ks = b % a.KS;
+    b /= a.KS;
+    const int nb = b % a.nblk, g = b / a.nblk;
+    const int kb0 = ks * a.KC;
+    const int nkc = a.KB - kb0 < a.KC ? a.KB - kb0 : a.KC;
+    const float4* xg = reinterpret_cast<const float4*>(a.xf[g]);
+    const f32x4* wg = reinterpret_cast<const f32x4*>(a.pack[g] + kWlHdr);
+
+    // the chunk's input fragments: MT x nkc x {hi, lo} 1-KiB blocks by LDS-DMA,
+    // issued before the weight prologue (vmcnt counts in issue order)
+    const uint32_t xb = lds_addr(xs);
+    for (int i = wid; i < MT * nkc * 2; i += kWlWaves) {
+        const int s = i / (2 * nkc), r = i - s * 2 * nkc;  // r = 2 kk + part
+        dma16(xg + ((int64_t)(s * a.KB + kb0) * 2 + r) * 64 + lane, xb + (uint32_t)((s * a.KC * 2 + r) * 1024));
+    }
+    // weight ring: k-block kk of the chunk in w[kk % kWlPF].  The loop runs a
+    // multiple of kWlPF steps without branches (one refill per step keeps the
+    // ring's loads in a fixed order the compiler's vmcnt waits follow); steps
+    // past the chunk read the pack's zero block (L2-resident) and add zeros
+    const int nt0 = (nb * kWlWaves + wid) * NTW;
+    int ntc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) ntc[t] = nt0 + t < a.NT ? nt0 + t : a.NT - 1;
+    const int64_t zoff = (int64_t)a.NT * a.KB * 2 * 64;  // the zero block (f32x4 units)
+    f32x4 w[kWlPF][NTW][2];
+    auto wload = [&](int kk, f32x4 (&dst)[NTW][2]) {
+        // (a wave-uniform offset select, not a branch: the loads stay in one
+        // basic block, so the waits before each step count the ring exactly)
+        const int64_t live = kk < nkc ? 1 : 0;
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+            const int64_t off = ((int64_t)ntc[t] * a.KB + kb0 + kk) * 2 * 64;
+            const f32x4* p = wg + (zoff + live * (off - zoff)) + lane;
+#if NFK_WL_NT
+            dst[t][0] = __builtin_nontemporal_load(p);
+            dst[t][1] = __builtin_nontemporal_load(p + 64);
+#else
+            dst[t][0] = p[0];
+            dst[t][1] = p[64];
+#endif
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < kWlPF; ++j) wload(j, w[j]);
+    // the DMAs were issued first: with the prologue's loads still outstanding
+    // they have landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWlPF * NTW * 2) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    f32x4 acc[NTW][MT];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+        for (int s = 0; s < MT; ++s) acc[t][s] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int nkr = (nkc + kWlPF - 1) / kWlPF * kWlPF;
+    for (int k0 = 0; k0 < nkr; k0 += kWlPF) {
+#pragma unroll
+        for (int j = 0; j < kWlPF; ++j) {
+            const int kk = k0 + j;
+            const int kx = kk < nkc ? kk : nkc - 1;  // (finite fragments against the zero block)
+            h8 xh[MT], xl[MT];
+#pragma unroll
+            for (int s = 0; s < MT; ++s) {
+                const float4* f = xs + ((s * a.KC + kx) * 2) * 64 + lane;
+                xh[s] = __builtin_bit_cast(h8, f[0]);
+                xl[s] = __builtin_bit_cast(h8, f[64]);
+            }
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) {
+                const h8 ah = __builtin_bit_cast(h8, w[j][t][0]), al = __builtin_bit_cast(h8, w[j][t][1]);
+#pragma unroll
+                for (int s = 0; s < MT; ++s) {
+                    acc[t][s] = mfma16(al, xh[s], acc[t][s]);
+                    acc[t][s] = mfma16(ah, xl[s], acc[t][s]);
+                    acc[t][s] = mfma16(ah, xh[s], acc[t][s]);
+                }
+            }
+            wload(kk + kWlPF, w[j]);
+            // (keep the refill here: the scheduler otherwise sinks the ring's
+            // loads to the end of the unrolled body and the prefetch depth collapses)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // partial sums: lane (q, n) of tile (t, s) holds row 16 s + n, features
+    // 16 nt + 4 q .. + 3
+    const int q = lane >> 4, n = lane & 15;
+    float* P = a.part + (int64_t)(g * a.KS + ks) * a.M * a.N;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+        if (nt0 + t >= a.NT) continue;
+        const int f0 = 16 * (nt0 + t) + 4 * q;
+        if (f0 >= a.N) continue;
+#pragma unroll
+        for (int s = 0; s < MT; ++s) {
+            const int m = 16 * s + n;
+            if (m < a.M)
+                *reinterpret_cast<float4*>(P + (int64_t)m * a.N + f0) =
+                    make_float4(acc[t][s][0], acc[t][s][1], acc[t][s][2], acc[t][s][3]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// hidden activations: h = tanh(sum_split P * 2^-s * u_row + b), split at 2^14
+// into the next GEMM's fragments.  One thread per (group, row, 8 features)
+struct WlAct {
+    const float* part;    // [2][KS][M][N]
+    const float* pack[2];
+    const float* bias[2];
+    const float* xun;     // per-row input unscale of the GEMM (nullptr: 2^-14, a hidden layer)
+    float* out[2];        // fragments [MT][KBo][part][64][8] halfs
+    int N, KS, M, MT, KBo;
+};
+
+__global__ __launch_bounds__(256) void k_wl_act(WlAct a) {
+    const int64_t per_g = (int64_t)a.MT * a.KBo * 64;  // (mt, kb, lane) = one 16-B hi + lo pair each
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= 2 * per_g) return;
+    const int g = (int)(i / per_g);
+    i -= g * per_g;
+    const int lane = (int)(i & 63);
+    const int64_t blk = i >> 6;  // mt KBo + kb
+    const int kb = (int)(blk % a.KBo), mt = (int)(blk / a.KBo);
+    const int m = 16 * mt + (lane & 15), f0 = 32 * kb + 8 * (lane >> 4);
+    h8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hi[j] = lo[j] = (_Float16)0.0f;
+    if (m < a.M) {
+        const float u = a.pack[g][0] * (a.xun != nullptr ? a.xun[m] : 1.0f / kWlAct);
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+        const float* P = a.part + ((int64_t)g * a.KS * a.M + m) * a.N + f0;
+        const bool full = f0 + 8 <= a.N;
+        for (int ks = 0; ks < a.KS; ++ks) {
+            const float* p = P + (int64_t)ks * a.M * a.N;
+            if (full) {
+                const float4 x0 = *reinterpret_cast<const float4*>(p), x1 = *reinterpret_cast<const float4*>(p + 4);
+                v[0] += x0.x, v[1] += x0.y, v[2] += x0.z, v[3] += x0.w;
+                v[4] += x1.x, v[5] += x1.y, v[6] += x1.z, v[7] += x1.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (f0 + j < a.N) v[j] += p[j];
+            }
+        }
+        const float* bz = a.bias[g];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (f0 + j < a.N) {
+                const float h = tanhf(v[j] * u + bz[f0 + j]) * kWlAct;
+                const _Float16 hh = (_Float16)h;
+                hi[j] = hh;
+                lo[j] = (_Float16)(h - (float)hh);
+            }
+        }
+    }
+    h8* o = reinterpret_cast<h8*>(a.out[g]) + (blk * 2) * 64 + lane;
+    o[0] = hi;
+    o[64] = lo;
+}
+
+// ---------------------------------------------------------------------------
+// one workgroup per row: (a) part == nullptr: the row of x as fragments (the
+// first half-coupling's input); (b) the affine half-coupling of the row from
+// the L3 partial sums (s = group 0, t = group 1), its log|det|, and optionally
+// the fragments of the output half (the next half-coupling's input)
+struct WlRows {
+    const float* part;    // [2][KS][M][h] or nullptr
+    const float* pack[2];
+    const float* bias[2];
+    const float* xin;     // the half being transformed (or split)
+    int64_t ldin;
+    float* out;           // the transformed half (coupling only)
+    int64_t ldo;
+    float* logdet;
+    int mode, inverse;
+    float* frag;          // fragments of the row's values [MT][KBf][part][64][8], or nullptr
+    float* frag_un;       // their per-row unscale 2^(e - 14)
+    int h, KS, M, MT, KBf;
+};
+
+constexpr int kRowThreads = 256;
+
+__global__ __launch_bounds__(kRowThreads) void k_wl_rows(WlRows a) {
+    extern __shared__ float rowv[];  // the row's values (h floats) when fragments are written
+    __shared__ float red[kRowThreads / 64];
+    const int m = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool live = m < a.M;
+    float amax = 0.0f, lsum = 0.0f;
+    if (live) {
+        const float* xr = a.xin + (int64_t)m * a.ldin;
+        if (a.part == nullptr) {
+            for (int c = tid; c < a.h; c += kRowThreads) {
+                const float v = xr[c];
+                rowv[c] = v;
+                amax = fmaxf(amax, fabsf(v));
+            }
+        } else {
+            const float us = a.pack[0][0] * (1.0f / kWlAct), ut = a.pack[1][0] * (1.0f / kWlAct);
+            const float* Ps = a.part + (int64_t)m * a.h;
+            const float* Pt = a.part + ((int64_t)a.KS * a.M + m) * a.h;
+            const int64_t st = (int64_t)a.M * a.h;
+            float* orow = a.out + (int64_t)m * a.ldo;
+            for (int c = tid; c < a.h; c += kRowThreads) {
+                float s = 0.0f, t = 0.0f;
+                for (int ks = 0; ks < a.KS; ++ks) {
+                    s += Ps[ks * st + c];
+                    t += Pt[ks * st + c];
+                }
+                s = s * us + a.bias[0][c];
+                t = t * ut + a.bias[1][c];
+                const float x = xr[c];
+                // flows.py:56, 59 (t + x exp(s)) and 69, 72 ((x - t) exp(-s)),
+                // each operation rounded (no contraction: -ffp-contract=off)
+                const float o = a.inverse ? (x - t) * expf(-s) : t + x * expf(s);
+                orow[c] = o;
+                lsum += s;
+                if (a.frag != nullptr) rowv[c] = o;
+                amax = fmaxf(amax, fabsf(o));
+            }
+        }
+    }
+    if (a.part != nullptr && a.mode != 0) {
+        // sum s over the row: each thread its columns in order, then a fixed tree
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off, 64);
+        if (lane == 0) red[wid] = lsum;
+        __syncthreads();
+        if (tid == 0 && live) {
+            float tot = 0.0f;
+            for (int w = 0; w < kRowThreads / 64; ++w) tot += red[w];
+            const float ld = a.inverse ? -tot : tot;
+            a.logdet[m] = a.mode == 2 ? a.logdet[m] + ld : ld;
+        }
+        __syncthreads();
+    }
+    if (a.frag == nullptr) return;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+    if (lane == 0) red[wid] = amax;
+    __syncthreads();
+    float mx = 0.0f;
+    for (int w = 0; w < kRowThreads / 64; ++w) mx = fmaxf(mx, red[w]);
+    int ex = 0;
+    if (mx > 0.0f && mx < 3.0e38f) frexpf(mx, &ex);  // mx < 2^ex
+    ex = ex < -64 ? -64 : ex;
+    const float sc = ldexpf(1.0f, 14 - ex);
+    if (tid == 0) a.frag_un[m] = live ? ldexpf(1.0f, ex - 14) : 0.0f;
+    const int mt = m >> 4;
+    h8* base = reinterpret_cast<h8*>(a.frag);
+    for (int u = tid; u < a.KBf * 4; u += kRowThreads) {
+        const int kb = u >> 2, q = u & 3, f0 = 32 * kb + 8 * q;
+        h8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float v = (live && f0 + j < a.h) ? rowv[f0 + j] * sc : 0.0f;
+            const _Float16 hh = (_Float16)v;
+            hi[j] = hh;
+            lo[j] = (_Float16)(v - (float)hh);
+        }
+        const int ln = 16 * q + (m & 15);
+        h8* o = base + ((int64_t)(mt * a.KBf + kb) * 2) * 64 + ln;
+        o[0] = hi;
+        o[64] = lo;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host: the GEMM stage plan
+struct WlPlan {
+    int NTW, KS, KC, nblk;
+    size_t lds;
+};
+
+WlPlan wl_plan(int N, int KB, int MT) {
+    WlPlan p{};
+    const int NT = (N + 15) / 16;
+    const int kcmax = (int)(kWlLdsMax / ((size_t)MT * 2048));
+    int ksmin = (KB + kcmax - 1) / kcmax;
+    // two tiles per wave where the feature blocks alone nearly cover the GPU
+    p.NTW = (2 * ((NT + 7) / 8) * ksmin >= kWlTarget) ? 2 : 1;
+    p.nblk = (NT + kWlWaves * p.NTW - 1) / (kWlWaves * p.NTW);
+    int ks = (kWlTarget + 2 * p.nblk - 1) / (2 * p.nblk);
+    ks = ks > ksmin ? ks : ksmin;
+    ks = ks < KB ? ks : KB;
+    p.KC = (KB + ks - 1) / ks;
+    p.KS = (KB + p.KC - 1) / p.KC;
+    p.lds = (size_t)MT * p.KC * 2048;
+    return p;
+}
+
+template <int MT, int NTW>
+int wl_gemm_launch(const WlGemm& a, const WlPlan& p, hipStream_t st) {
+    static bool attr = false;  // (every instance sets its dynamic-LDS cap once)
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wl_gemm<MT, NTW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWlLdsMax);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_wl_gemm<MT, NTW>), dim3((unsigned)(2 * p.nblk * p.KS)), dim3(64 * kWlWaves), p.lds, st,
+                       a);
+    return wl_status("nfk_wide_rnvp: GEMM launch");
+}
+
+int wl_gemm(const float* const pk[2], const float* const xf[2], float* part, int N, int K, int M, int MT,
+            hipStream_t st) {
+    const int KB = (K + 31) / 32;
+    const WlPlan p = wl_plan(N, KB, MT);
+    WlGemm a;
+    a.pack[0] = pk[0], a.pack[1] = pk[1];
+    a.xf[0] = xf[0], a.xf[1] = xf[1];
+    a.part = part;
+    a.N = N, a.NT = (N + 15) / 16, a.KB = KB, a.KS = p.KS, a.KC = p.KC, a.M = M, a.nblk = p.nblk;
+#define NFK_WL_CASE(mt)                                                                   \
+    case mt:                                                                              \
+        return p.NTW == 2 ? wl_gemm_launch<mt, 2>(a, p, st) : wl_gemm_launch<mt, 1>(a, p, st);
+    switch (MT) {
+        NFK_WL_CASE(1) NFK_WL_CASE(2) NFK_WL_CASE(3) NFK_WL_CASE(4) NFK_WL_CASE(5) NFK_WL_CASE(6)
+        NFK_WL_CASE(7) NFK_WL_CASE(8)
+        default: return nfk_set_error("nfk_wide_rnvp: bad row tile count");
+    }
+#undef NFK_WL_CASE
+}
+
+int64_t frag_floats(int MT, int K) { return (int64_t)MT * ((K + 31) / 32) * 512; }
+
+// workspace of one pass of MT sample tiles (floats, each region 16-byte aligned)
+struct WlWs {
+    float *fx[2], *fun[2], *fh[2][2], *part;
+    int64_t total;
+};
+
+WlWs wl_ws(float* base, int half, int hidden, int MT) {
+    WlWs w{};
+    const int M = 16 * MT;
+    int64_t off = 0;
+    auto take = [&](int64_t n) {
+        float* p = base == nullptr ? nullptr : base + off;
+        off += (n + 3) / 4 * 4;
+        return p;
+    };
+    for (int i = 0; i < 2; ++i) w.fx[i] = take(frag_floats(MT, half));
+    for (int i = 0; i < 2; ++i) w.fun[i] = take(M);
+    for (int l = 0; l < 2; ++l)
+        for (int g = 0; g < 2; ++g) w.fh[l][g] = take(frag_floats(MT, hidden));
+    int64_t pmax = 0;
+    const int shapes[3][2] = {{hidden, half}, {hidden, hidden}, {half, hidden}};  // (N, K) per stage
+    for (auto& s : shapes) {
+        const WlPlan p = wl_plan(s[0], (s[1] + 31) / 32, MT);
+        const int64_t n = 2LL * p.KS * M * s[0];
+        pmax = n > pmax ? n : pmax;
+    }
+    w.part = take(pmax);
+    w.total = off;
+    return w;
+}
+
+}  // namespace
+
+extern "C" int64_t nfk_wlin_pack_floats(int32_t N, int32_t K) {
+    if (N <= 0 || K <= 0) return 0;
+    // header, the fragment blocks, one zero block (the GEMM's steps past a chunk)
+    return kWlHdr + (int64_t)((N + 15) / 16) * ((K + 31) / 32) * 512 + 512;
+}
+
+extern "C" int nfk_wlin_pack(const float* W, int32_t N, int32_t K, float* pack, nfk_stream_t stream) {
+    if (nfk_wlin_pack_floats(N, K) == 0) return nfk_set_error("nfk_wlin_pack: bad shape");
+    if (!W || !pack) return nfk_set_error("nfk_wlin_pack: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t body = (int64_t)((N + 15) / 16) * ((K + 31) / 32) * 512;
+    if (hipMemsetAsync(pack, 0, kWlHdr * sizeof(float), st) != hipSuccess ||
+        hipMemsetAsync(pack + kWlHdr + body, 0, 512 * sizeof(float), st) != hipSuccess)
+        return nfk_set_error("nfk_wlin_pack: memset failed");
+    const int64_t n = (int64_t)N * K;
+    const int64_t gm = (n + 4095) / 4096;
+    hipLaunchKernelGGL(k_wl_max, dim3((unsigned)(gm < 1024 ? gm : 1024)), dim3(256), 0, st, W, n, pack);
+    const int KB = (K + 31) / 32;
+    const int64_t units = (int64_t)((N + 15) / 16) * KB * 128;
+    const int64_t gp = (units + 255) / 256;
+    hipLaunchKernelGGL(k_wl_pack, dim3((unsigned)(gp < 8192 ? gp : 8192)), dim3(256), 0, st, W, N, K, KB, units, pack);
+    return wl_status("nfk_wlin_pack");
+}
+
+extern "C" int nfk_wide_rnvp_supported(int32_t half, int32_t hidden) {
+    return (half >= 4 && half % 4 == 0 && half <= 16384 && hidden >= 16 && hidden % 4 == 0 && hidden <= 16384) ? 1 : 0;
+}
+
+extern "C" int64_t nfk_wide_rnvp_workspace(int32_t half, int32_t hidden, int64_t batch) {
+    if (!nfk_wide_rnvp_supported(half, hidden) || batch <= 0) return 0;
+    const int64_t mt = (batch + 15) / 16;
+    return wl_ws(nullptr, half, hidden, (int)(mt < kWlMaxMT ? mt : kWlMaxMT)).total;
+}
+
+extern "C" int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const float* const* biases,
+                             int32_t half, int32_t hidden, float* z, int64_t ldz, float* logdet, int32_t logdet_mode,
+                             int64_t batch, int32_t inverse, float* workspace, int64_t workspace_floats,
+                             nfk_stream_t stream) {
+    if (!nfk_wide_rnvp_supported(half, hidden)) return nfk_set_error("nfk_wide_rnvp: shape not supported");
+    if (batch < 0) return nfk_set_error("nfk_wide_rnvp: bad batch");
+    if (batch == 0) return 0;
+    if (!x || !packs || !biases || !z || !workspace) return nfk_set_error("nfk_wide_rnvp: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_wide_rnvp: null logdet");
+    if (ldx < 2 * half || ldz < 2 * half) return nfk_set_error("nfk_wide_rnvp: bad leading dimension");
+    if (workspace_floats < nfk_wide_rnvp_workspace(half, hidden, batch))
+        return nfk_set_error("nfk_wide_rnvp: workspace too small (nfk_wide_rnvp_workspace)");
+    for (int i = 0; i < 12; ++i)
+        if (!packs[i] || !biases[i]) return nfk_set_error("nfk_wide_rnvp: null pack or bias");
+    hipStream_t st = (hipStream_t)stream;
+    const int h = half, H = hidden;
+    // half-couplings in execution order: forward 1 then 2, inverse 2 then 1.
+    // Coupling c (0 = s1/t1: reads the lower half, changes the upper; 1 =
+    // s2/t2: reads the upper, changes the lower), packs [6 c + 2 layer + group]
+    for (int64_t r0 = 0; r0 < batch; r0 += 16 * kWlMaxMT) {
+        const int M = (int)(batch - r0 < 16 * kWlMaxMT ? batch - r0 : 16 * kWlMaxMT);
+        const int MT = (M + 15) / 16;
+        const WlWs w = wl_ws(workspace, h, H, MT);
+        const float* xr = x + r0 * ldx;
+        float* zr = z + r0 * ldz;
+        float* ldr = logdet_mode != 0 ? logdet + r0 : nullptr;
+        const int first = inverse ? 1 : 0;
+        // the first conditioner's input: x's lower half (forward) or upper (inverse)
+        {
+            WlRows a{};
+            a.xin = xr + (first == 0 ? 0 : h);
+            a.ldin = ldx;
+            a.frag = w.fx[0];
+            a.frag_un = w.fun[0];
+            a.h = h, a.M = M, a.MT = MT, a.KBf = (h + 31) / 32;
+            hipLaunchKernelGGL(k_wl_rows, dim3(16 * MT), dim3(kRowThreads), (size_t)h * sizeof(float), st, a);
+            if (int e = wl_status("nfk_wide_rnvp: rows launch")) return e;
+        }
+        for (int step = 0; step < 2; ++step) {
+            const int c = inverse ? 1 - step : step;
+            const float* const* pk = packs + 6 * c;
+            const float* const* bs = biases + 6 * c;
+            const int fi = step;  // this coupling's input fragments
+            // L1: [M, h] -> [M, H] (s and t), + b1, tanh
+            {
+                const float* p2[2] = {pk[0], pk[1]};
+                const float* x2[2] = {w.fx[fi], w.fx[fi]};
+                if (int e = wl_gemm(p2, x2, w.part, H, h, M, MT, st)) return e;
+                const WlPlan p = wl_plan(H, (h + 31) / 32, MT);
+                WlAct a{};
+                a.part = w.part, a.pack[0] = pk[0], a.pack[1] = pk[1], a.bias[0] = bs[0], a.bias[1] = bs[1];
+                a.xun = w.fun[fi], a.out[0] = w.fh[0][0], a.out[1] = w.fh[0][1];
+                a.N = H, a.KS = p.KS, a.M = M, a.MT = MT, a.KBo = (H + 31) / 32;
+                const int64_t n = 2LL * MT * a.KBo * 64;
+                hipLaunchKernelGGL(k_wl_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+                if (int e = wl_status("nfk_wide_rnvp: act launch")) return e;
+            }
+            // L2: [M, H] -> [M, H], + b2, tanh
+            {
+                const float* p2[2] = {pk[2], pk[3]};
+                const float* x2[2] = {w.fh[0][0], w.fh[0][1]};
+                if (int e = wl_gemm(p2, x2, w.part, H, H, M, MT, st)) return e;
+                const WlPlan p = wl_plan(H, (H + 31) / 32, MT);
+                WlAct a{};
+                a.part = w.part, a.pack[0] = pk[2], a.pack[1] = pk[3], a.bias[0] = bs[2], a.bias[1] = bs[3];
+                a.xun = nullptr, a.out[0] = w.fh[1][0], a.out[1] = w.fh[1][1];
+                a.N = H, a.KS = p.KS, a.M = M, a.MT = MT, a.KBo = (H + 31) / 32;
+                const int64_t n = 2LL * MT * a.KBo * 64;
+                hipLaunchKernelGGL(k_wl_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+                if (int e = wl_status("nfk_wide_rnvp: act launch")) return e;
+            }
+            // L3: [M, H] -> [M, h] (s, t), + b3; the coupling of the other half
+            {
+                const float* p2[2] = {pk[4], pk[5]};
+                const float* x2[2] = {w.fh[1][0], w.fh[1][1]};
+                if (int e = wl_gemm(p2, x2, w.part, h, H, M, MT, st)) return e;
+                const WlPlan p = wl_plan(h, (H + 31) / 32, MT);
+                const int col = c == 0 ? h : 0;  // the half this coupling changes
+                WlRows a{};
+                a.part = w.part, a.pack[0] = pk[4], a.pack[1] = pk[5], a.bias[0] = bs[4], a.bias[1] = bs[5];
+                a.xin = xr + col, a.ldin = ldx, a.out = zr + col, a.ldo = ldz;
+                a.logdet = ldr;
+                a.mode = ldr == nullptr ? 0 : (step == 0 ? logdet_mode : 2);
+                a.inverse = inverse ? 1 : 0;
+                // the first coupling's output is the second one's input
+                a.frag = step == 0 ? w.fx[1] : nullptr;
+                a.frag_un = step == 0 ? w.fun[1] : nullptr;
+                a.h = h, a.KS = p.KS, a.M = M, a.MT = MT, a.KBf = (h + 31) / 32;
+                hipLaunchKernelGGL(k_wl_rows, dim3(16 * MT), dim3(kRowThreads),
+                                   step == 0 ? (size_t)h * sizeof(float) : 0, st, a);
+                if (int e = wl_status("nfk_wide_rnvp: coupling launch")) return e;
+            }
+        }
+    }
+    return 0;
+}

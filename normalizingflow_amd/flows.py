@@ -251,7 +251,7 @@ class _HipFlow(nn.Module):
         (optimizer steps, ``with torch.no_grad(): p.add_(...)``,
         ``load_state_dict``) bumps.  Writes through ``p.data`` do not bump it:
         call this (or NormalizingFlowModel.invalidate_caches) after them."""
-        for name in ("_pack_cache", "_winv_key", "_vjp_cache"):
+        for name in ("_pack_cache", "_winv_key", "_vjp_cache", "_wide_cache"):
             if name in self.__dict__:
                 self.__dict__[name] = None
 
@@ -316,7 +316,7 @@ class FCNN(nn.Module):
 _HOST = []
 
 
-_DERIVED_STATE = ("_pack_cache", "_winv_key", "_vjp_cache", "_ar_tree", "_named_cache", "_ar_names")
+_DERIVED_STATE = ("_pack_cache", "_winv_key", "_vjp_cache", "_ar_tree", "_named_cache", "_ar_names", "_wide_cache")
 
 
 def _host_helper():
@@ -433,6 +433,37 @@ class RealNVP(_HipFlow):
         self._pack_cache = (key, pack, hidden, hp)
         return pack
 
+    def _wide_pack(self, device, batch):
+        """(packs, biases) of nfk_wide_rnvp -- the layer as a weight stream
+        (Polymer_rnvp.yaml's RealNVP(2048, hidden 4000) at its 40-row batches):
+        every Linear of the four conditioners packed once (nfk_wlin_pack),
+        rebuilt when any parameter changes; None when it does not apply (non-stock
+        conditioners, unequal hidden widths, an unsupported shape, or a batch
+        above config.WIDE_RNVP_MAX_ROWS, where library GEMMs are compute-bound
+        and faster)."""
+        nets = (self.s1, self.t1, self.s2, self.t2)
+        if not config.USE_WIDE_RNVP or batch > config.WIDE_RNVP_MAX_ROWS or self.dim % 2:
+            return None
+        if torch.device(device).type != "cuda" or not all(_is_stock_fcnn(n) for n in nets):
+            return None
+        hidden = self.s1.network[0].out_features
+        if any(n.network[0].out_features != hidden for n in nets) or not K_.wide_rnvp_supported(self.dim // 2,
+                                                                                                 hidden):
+            return None
+        # pack index 6 c + 2 l + g: c = 0 (s1, t1) / 1 (s2, t2), l = Linear 0/2/4, g = s/t
+        order = [(n, i) for c in ((self.s1, self.t1), (self.s2, self.t2)) for i in (0, 2, 4) for n in c]
+        params = [t for n, i in order for t in (n.network[i].weight, n.network[i].bias)]
+        if any(p.device != device or p.dtype != torch.float32 for p in params):
+            return None
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        c = self.__dict__.get("_wide_cache")
+        if c is not None and c[0] == key:
+            return c[1]
+        packs = [K_.wlin_pack(n.network[i].weight) for n, i in order]
+        biases = [n.network[i].bias.detach().contiguous() for n, i in order]
+        self.__dict__["_wide_cache"] = (key, (packs, biases, hidden))
+        return packs, biases, hidden
+
     def _chain_shape(self, device):
         """("rnvp", kernel half_dim, hidden, half_dim) when this layer runs as the
         fused kernel and the chain form applies (so it may join an
@@ -455,6 +486,12 @@ class RealNVP(_HipFlow):
             zk = torch.empty_like(xk, memory_format=torch.contiguous_format)
             K_.fused_realnvp(xk, pack, hp, hidden, zk, logdet=logdet, logdet_mode=mode, inverse=inverse)
             return rnvp_unpad(zk, h, hp)
+        wide = self._wide_pack(x.device, x.shape[0])
+        if wide is not None:
+            z = torch.empty_like(x, memory_format=torch.contiguous_format)
+            xc = x if x.stride(1) == 1 else x.contiguous()
+            K_.wide_rnvp(xc, wide[0], wide[1], h, wide[2], z, logdet=logdet, logdet_mode=mode, inverse=inverse)
+            return z
         z = torch.empty_like(x, memory_format=torch.contiguous_format)
         lo, up = x[:, :h], x[:, h:]
         zlo, zup = z[:, :h], z[:, h:]

@@ -744,3 +744,52 @@ def fused_realnvp(x, wpack, half_dim, hidden, z, *, logdet, logdet_mode, inverse
     zp, ldz = _mat(z, "z")
     _timed("nfk_fused_realnvp", dev, "nfk_fused_realnvp", xp, ldx, wpack.data_ptr(), half_dim, hidden, zp, ldz,
            _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, _stream(dev))
+
+
+# ---- RealNVP with wide conditioners at small batches (nfk_wide_rnvp.hip)
+def wlin_pack(W):
+    """An nn.Linear weight [N, K] as the weight-streaming pack (nfk_wlin_pack:
+    fp16 hi/lo MFMA fragments, one power-of-two scale, a zero block)."""
+    dev = _require_hip(W)
+    W = W.detach()
+    if W.dtype != F32 or not W.is_contiguous():
+        W = W.contiguous().to(F32)
+    if W.dim() != 2:
+        raise ValueError("wlin_pack: W must be 2-D")
+    N, K = W.shape
+    n = int(_lib.load().nfk_wlin_pack_floats(N, K))
+    if n <= 0:
+        raise ValueError("wlin_pack: bad shape %s" % (tuple(W.shape),))
+    pack = torch.empty(n, dtype=F32, device=dev)
+    _lib.call("nfk_wlin_pack", W.data_ptr(), N, K, pack.data_ptr(), _stream(dev))
+    return pack
+
+
+def wide_rnvp_supported(half, hidden):
+    return bool(_lib.load().nfk_wide_rnvp_supported(half, hidden))
+
+
+def wide_rnvp(x, packs, biases, half, hidden, z, *, logdet, logdet_mode, inverse=False):
+    """One RealNVP layer through the weight stream (include/nfk.h
+    nfk_wide_rnvp).  packs / biases: 12 device tensors each, index
+    6 c + 2 l + g (half-coupling c: 0 = s1/t1, 1 = s2/t2; Linear l = network.0,
+    .2, .4; conditioner g: 0 = s, 1 = t)."""
+    dev = _require_hip(x, z, logdet, *packs, *biases)
+    B = x.shape[0]
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    if x.shape[1] != 2 * half or z.shape != x.shape:
+        raise ValueError("wide_rnvp: x and z must be [B, %d]" % (2 * half))
+    if len(packs) != 12 or len(biases) != 12:
+        raise ValueError("wide_rnvp: 12 packs and 12 biases")
+    for b in biases:
+        if b.dtype != F32 or not b.is_contiguous():
+            raise ValueError("wide_rnvp: biases must be contiguous float32")
+    lib = _lib.load()
+    nws = int(lib.nfk_wide_rnvp_workspace(half, hidden, B))
+    ws = torch.empty(max(nws, 4), dtype=F32, device=dev)
+    pk = (ctypes.c_void_p * 12)(*[t.data_ptr() for t in packs])
+    bs = (ctypes.c_void_p * 12)(*[t.data_ptr() for t in biases])
+    _timed("nfk_wide_rnvp", dev, "nfk_wide_rnvp", xp, ldx, ctypes.addressof(pk), ctypes.addressof(bs), half, hidden,
+           zp, ldz, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, ws.data_ptr(), nws,
+           _stream(dev))

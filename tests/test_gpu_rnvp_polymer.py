@@ -77,3 +77,85 @@ def test_rnvp2048_sample(model2, hip_device):
     close(xs, ref_x, Z_RTOL, 5e-5)
     close(lpx, ref_lpx, 1e-5, 1e-3)
     flush_status_checks()
+
+
+def _lib_path(fn):
+    """fn() with the weight-stream path off (library GEMMs + nfk_affine_coupling)."""
+    from normalizingflow_amd import config
+    prev = config.USE_WIDE_RNVP
+    config.USE_WIDE_RNVP = False
+    try:
+        return fn()
+    finally:
+        config.USE_WIDE_RNVP = prev
+
+
+@pytest.mark.parametrize("dim,H,rows", [(2048, 4000, 40), (2048, 4000, 100), (40, 300, 1), (40, 300, 129),
+                                        (200, 1000, 256)])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_wide_rnvp_vs_library_path_and_oracle(dim, H, rows, inverse, hip_device):
+    """The weight-stream layer (nfk_wide_rnvp: one call per layer, 128 rows per
+    pass) against the library-GEMM path and the oracle, forward and inverse,
+    log|det| written (mode 1) and accumulated (mode 2); ragged row counts and
+    two-pass batches (129, 256 rows)."""
+    from normalizingflow_amd import kernels as K_
+    torch.manual_seed(dim + H)
+    layer = nff.RealNVP(dim, hidden_dim=H)
+    sd = {k: v.detach().clone() for k, v in layer.state_dict().items()}
+    layer = layer.to(hip_device)
+    x = torch.randn(rows, dim, generator=torch.Generator().manual_seed(rows)) * 0.5
+    xd = x.to(hip_device)
+    with torch.no_grad():
+        assert layer._wide_pack(xd.device, rows) is not None
+        K_.TIMER = K_.KernelTimer()
+        try:
+            z, ld = (layer.inverse if inverse else layer)(xd)
+            torch.cuda.synchronize()
+            n = {k: v[0] for k, v in K_.TIMER.summary().items()}
+        finally:
+            K_.TIMER = None
+        assert n == {"nfk_wide_rnvp": 1}, n
+        zl, ldl = _lib_path(lambda: (layer.inverse if inverse else layer)(xd))
+        ref = orc.apply_layer(dict(type="RealNVP", prefix="", dim=dim), x, sd, inverse=inverse)
+        # accumulate mode on a preset log|det|
+        ld0 = torch.linspace(-2.0, 2.0, rows, device=hip_device)
+        z2 = torch.empty_like(xd)
+        p, b, hid = layer._wide_pack(xd.device, rows)
+        K_.wide_rnvp(xd, p, b, dim // 2, hid, z2, logdet=ld0, logdet_mode=2, inverse=inverse)
+    close(z, ref[0], Z_RTOL, Z_ATOL)
+    close(ld, ref[1], LD_RTOL, LD_ATOL)
+    close(zl, ref[0], Z_RTOL, Z_ATOL)
+    assert torch.equal(z2, z)
+    close(ld0 - torch.linspace(-2.0, 2.0, rows, device=hip_device), ld, 1e-6, 1e-5)
+
+
+def test_wide_rnvp_reproducible_and_in_place(hip_device):
+    """Three runs bitwise equal (split-K partial sums added in a fixed order),
+    and z may alias x (each element is read before it is written)."""
+    from normalizingflow_amd import kernels as K_
+    torch.manual_seed(5)
+    layer = nff.RealNVP(2048, hidden_dim=4000).to(hip_device)
+    x = torch.randn(100, 2048, device=hip_device) * 0.3
+    with torch.no_grad():
+        outs = [layer(x) for _ in range(3)]
+        for z, ld in outs[1:]:
+            assert torch.equal(z, outs[0][0]) and torch.equal(ld, outs[0][1])
+        p, b, hid = layer._wide_pack(x.device, 100)
+        xi = x.clone()
+        ld = torch.empty(100, device=hip_device)
+        K_.wide_rnvp(xi, p, b, 1024, hid, xi, logdet=ld, logdet_mode=1)
+    assert torch.equal(xi, outs[0][0]) and torch.equal(ld, outs[0][1])
+
+
+def test_wide_rnvp_cache_follows_weight_updates(hip_device):
+    """An in-place weight update (optimizer step) rebuilds the packs."""
+    torch.manual_seed(6)
+    layer = nff.RealNVP(64, hidden_dim=512).to(hip_device)
+    x = torch.randn(30, 64, device=hip_device)
+    with torch.no_grad():
+        z0, _ = layer(x)
+        layer.t2.network[4].bias.add_(0.25)
+        z1, _ = layer(x)
+        zl, _ = _lib_path(lambda: layer(x))
+    assert not torch.equal(z0, z1)
+    close(z1, zl, Z_RTOL, Z_ATOL)

@@ -35,13 +35,27 @@ def main():
     wbytes = 4 * sum(p.numel() for p in model.parameters())
     floor_ms = wbytes / 8e12 * 1e3
     out = {"weights_bytes": wbytes, "hbm_floor_ms_per_step": floor_ms}
+    from normalizingflow_amd import config
+    from normalizingflow_amd import kernels as K_
     with torch.no_grad():
-        for rows in (40, 100, 500):
-            x = torch.randn(rows, D, device=dev) * 0.1 ** 0.5
-            t = timed(lambda: model.log_prob(x))
-            out["log_prob_%d_ms" % rows] = t
-            out["log_prob_%d_frac_of_hbm_floor" % rows] = floor_ms / t
-        out["sample_100_ms"] = timed(lambda: model.sample(100), 10)
+        for wide in (True, False):
+            config.USE_WIDE_RNVP = wide
+            tag = "wide" if wide else "library"
+            for rows in (40, 100, 500):
+                x = torch.randn(rows, D, device=dev) * 0.1 ** 0.5
+                t = timed(lambda: model.log_prob(x))
+                out["%s_log_prob_%d_ms" % (tag, rows)] = t
+                out["%s_log_prob_%d_frac_of_hbm_floor" % (tag, rows)] = floor_ms / t
+            out["%s_sample_100_ms" % tag] = timed(lambda: model.sample(100), 10)
+        config.USE_WIDE_RNVP = True
+        # per-layer call time of the weight stream (HIP events around each call)
+        x = torch.randn(40, D, device=dev) * 0.1 ** 0.5
+        K_.TIMER = K_.KernelTimer()
+        for _ in range(5):
+            model.log_prob(x)
+        torch.cuda.synchronize()
+        out["wide_layer_call_40"] = {k: {"calls": v[0], "mean_ms": v[1]} for k, v in K_.TIMER.summary().items()}
+        K_.TIMER = None
         # one conditioner's three GEMMs at 40 rows (torch Linear: library GEMM)
         net = flows[0].s1
         x = torch.randn(40, D // 2, device=dev)
