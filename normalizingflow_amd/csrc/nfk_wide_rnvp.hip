@@ -48,9 +48,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWlWaves = 4;                    // waves per GEMM workgroup (one per SIMD)
 constexpr int kWlPF = 8;                       // k-blocks of weights in flight per wave
+constexpr int kWlRing = kWlPF + 1;             // LDS slots of input fragments
 constexpr int kWlMaxMT = 8;                    // sample tiles per pass: 128 rows
 constexpr int kWlHdr = 64;                     // pack header floats ([0] = 2^-s)
-constexpr size_t kWlLdsMax = 128 * 1024;       // the input chunk of one GEMM workgroup
 constexpr float kWlAct = 16384.0f;             // tanh outputs split at 2^14
 constexpr int kWlTarget = 256;                 // GEMM workgroups: at least one per CU
 // the weight stream's loads non-temporal (every weight is read once per layer)
@@ -136,7 +136,13 @@ struct WlGemm {
 
 template <int MT, int NTW>
 __global__ __launch_bounds__(64 * kWlWaves, 1) void k_wl_gemm(WlGemm a) {
-    extern __shared__ __attribute__((aligned(16))) float4 xs[];  // [MT][KC][part][64]
+    // the input fragments of k-block kk of the chunk: 2 MT 1-KiB blocks in
+    // ring slot kk % kWlRing, copied by LDS-DMA kWlPF k-blocks ahead together
+    // with the weights (every wave copies D blocks per step; a wave with fewer
+    // distinct blocks re-copies the last one, so every wave's vmcnt is the same)
+    constexpr int XB = 2 * MT, D = (XB + kWlWaves - 1) / kWlWaves;
+    constexpr int PER = D + 2 * NTW;  // vector-memory operations per wave and step
+    extern __shared__ __attribute__((aligned(16))) float4 xs[];  // [kWlRing][XB][64]
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int b = blockIdx.x;
@@ -147,27 +153,26 @@ __global__ __launch_bounds__(64 * kWlWaves, 1) void k_wl_gemm(WlGemm a) {
     const int nkc = a.KB - kb0 < a.KC ? a.KB - kb0 : a.KC;
     const float4* xg = reinterpret_cast<const float4*>(a.xf[g]);
     const f32x4* wg = reinterpret_cast<const f32x4*>(a.pack[g] + kWlHdr);
-
-    // the chunk's input fragments: MT x nkc x {hi, lo} 1-KiB blocks by LDS-DMA,
-    // issued before the weight prologue (vmcnt counts in issue order)
     const uint32_t xb = lds_addr(xs);
-    for (int i = wid; i < MT * nkc * 2; i += kWlWaves) {
-        const int s = i / (2 * nkc), r = i - s * 2 * nkc;  // r = 2 kk + part
-        dma16(xg + ((int64_t)(s * a.KB + kb0) * 2 + r) * 64 + lane, xb + (uint32_t)((s * a.KC * 2 + r) * 1024));
-    }
-    // weight ring: k-block kk of the chunk in w[kk % kWlPF].  The loop runs a
-    // multiple of kWlPF steps without branches (one refill per step keeps the
-    // ring's loads in a fixed order the compiler's vmcnt waits follow); steps
-    // past the chunk read the pack's zero block (L2-resident) and add zeros
     const int nt0 = (nb * kWlWaves + wid) * NTW;
     int ntc[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; ++t) ntc[t] = nt0 + t < a.NT ? nt0 + t : a.NT - 1;
+    // steps past the chunk read the pack's zero block (L2-resident) and re-copy
+    // the chunk's last input block: they add zeros, and keep the loop free of
+    // branches, so the ring's loads stay in a fixed order the waits count
     const int64_t zoff = (int64_t)a.NT * a.KB * 2 * 64;  // the zero block (f32x4 units)
     f32x4 w[kWlPF][NTW][2];
-    auto wload = [&](int kk, f32x4 (&dst)[NTW][2]) {
-        // (a wave-uniform offset select, not a branch: the loads stay in one
-        // basic block, so the waits before each step count the ring exactly)
+    auto issue = [&](int kk, f32x4 (&dst)[NTW][2]) {
+        const int kx = kk < nkc ? kk : nkc - 1;
+        const uint32_t slot = xb + (uint32_t)((kk % kWlRing) * XB * 1024);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int blk = wid + kWlWaves * d < XB ? wid + kWlWaves * d : XB - 1;  // (wave-uniform)
+            const int s = blk >> 1, part = blk & 1;
+            dma16(xg + ((int64_t)(s * a.KB + kb0 + kx) * 2 + part) * 64 + lane, slot + (uint32_t)(blk * 1024));
+        }
+        // (a wave-uniform offset select, not a branch)
         const int64_t live = kk < nkc ? 1 : 0;
 #pragma unroll
         for (int t = 0; t < NTW; ++t) {
@@ -183,12 +188,7 @@ __global__ __launch_bounds__(64 * kWlWaves, 1) void k_wl_gemm(WlGemm a) {
         }
     };
 #pragma unroll
-    for (int j = 0; j < kWlPF; ++j) wload(j, w[j]);
-    // the DMAs were issued first: with the prologue's loads still outstanding
-    // they have landed
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWlPF * NTW * 2) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    for (int j = 0; j < kWlPF; ++j) issue(j, w[j]);
 
     f32x4 acc[NTW][MT];
 #pragma unroll
@@ -200,13 +200,17 @@ __global__ __launch_bounds__(64 * kWlWaves, 1) void k_wl_gemm(WlGemm a) {
 #pragma unroll
         for (int j = 0; j < kWlPF; ++j) {
             const int kk = k0 + j;
-            const int kx = kk < nkc ? kk : nkc - 1;  // (finite fragments against the zero block)
+            // this step's copies and weights landed (the kWlPF - 1 later steps'
+            // operations may still be in flight), then every wave's copies
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kWlPF - 1) * PER) : "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const float4* f = xs + (kk % kWlRing) * XB * 64 + lane;
             h8 xh[MT], xl[MT];
 #pragma unroll
             for (int s = 0; s < MT; ++s) {
-                const float4* f = xs + ((s * a.KC + kx) * 2) * 64 + lane;
-                xh[s] = __builtin_bit_cast(h8, f[0]);
-                xl[s] = __builtin_bit_cast(h8, f[64]);
+                xh[s] = __builtin_bit_cast(h8, f[(2 * s) * 64]);
+                xl[s] = __builtin_bit_cast(h8, f[(2 * s + 1) * 64]);
             }
 #pragma unroll
             for (int t = 0; t < NTW; ++t) {
@@ -218,7 +222,9 @@ __global__ __launch_bounds__(64 * kWlWaves, 1) void k_wl_gemm(WlGemm a) {
                     acc[t][s] = mfma16(ah, xh[s], acc[t][s]);
                 }
             }
-            wload(kk + kWlPF, w[j]);
+            // the slot refilled below was read one step ago: every wave has
+            // passed this step's barrier, so its reads of it have returned
+            issue(kk + kWlPF, w[j]);
             // (keep the refill here: the scheduler otherwise sinks the ring's
             // loads to the end of the unrolled body and the prefetch depth collapses)
             __builtin_amdgcn_sched_barrier(0);
@@ -257,15 +263,15 @@ struct WlAct {
 };
 
 __global__ __launch_bounds__(256) void k_wl_act(WlAct a) {
-    const int64_t per_g = (int64_t)a.MT * a.KBo * 64;  // (mt, kb, lane) = one 16-B hi + lo pair each
+    // thread i: group g, row m (padded to 16 MT), features 8 n8 .. + 7, n8
+    // fastest: a wave reads 64 consecutive 32-B runs of one partial-sum row
+    const int N8 = 4 * a.KBo, RM = 16 * a.MT;
     int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= 2 * per_g) return;
-    const int g = (int)(i / per_g);
-    i -= g * per_g;
-    const int lane = (int)(i & 63);
-    const int64_t blk = i >> 6;  // mt KBo + kb
-    const int kb = (int)(blk % a.KBo), mt = (int)(blk / a.KBo);
-    const int m = 16 * mt + (lane & 15), f0 = 32 * kb + 8 * (lane >> 4);
+    if (i >= 2LL * RM * N8) return;
+    const int n8 = (int)(i % N8);
+    i /= N8;
+    const int m = (int)(i % RM), g = (int)(i / RM);
+    const int kb = n8 >> 2, q = n8 & 3, f0 = 8 * n8;
     h8 hi, lo;
 #pragma unroll
     for (int j = 0; j < 8; ++j) hi[j] = lo[j] = (_Float16)0.0f;
@@ -275,18 +281,30 @@ __global__ __launch_bounds__(256) void k_wl_act(WlAct a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = 0.0f;
         const float* P = a.part + ((int64_t)g * a.KS * a.M + m) * a.N + f0;
-        const bool full = f0 + 8 <= a.N;
-        for (int ks = 0; ks < a.KS; ++ks) {
-            const float* p = P + (int64_t)ks * a.M * a.N;
-            if (full) {
-                const float4 x0 = *reinterpret_cast<const float4*>(p), x1 = *reinterpret_cast<const float4*>(p + 4);
+        const int64_t st = (int64_t)a.M * a.N;
+        if (f0 + 8 <= a.N) {
+            int ks = 0;
+            for (; ks + 2 <= a.KS; ks += 2) {  // two splits' loads in flight, added in split order
+                const float4 x0 = *reinterpret_cast<const float4*>(P + ks * st);
+                const float4 x1 = *reinterpret_cast<const float4*>(P + ks * st + 4);
+                const float4 y0 = *reinterpret_cast<const float4*>(P + (ks + 1) * st);
+                const float4 y1 = *reinterpret_cast<const float4*>(P + (ks + 1) * st + 4);
                 v[0] += x0.x, v[1] += x0.y, v[2] += x0.z, v[3] += x0.w;
                 v[4] += x1.x, v[5] += x1.y, v[6] += x1.z, v[7] += x1.w;
-            } else {
+                v[0] += y0.x, v[1] += y0.y, v[2] += y0.z, v[3] += y0.w;
+                v[4] += y1.x, v[5] += y1.y, v[6] += y1.z, v[7] += y1.w;
+            }
+            if (ks < a.KS) {
+                const float4 x0 = *reinterpret_cast<const float4*>(P + ks * st);
+                const float4 x1 = *reinterpret_cast<const float4*>(P + ks * st + 4);
+                v[0] += x0.x, v[1] += x0.y, v[2] += x0.z, v[3] += x0.w;
+                v[4] += x1.x, v[5] += x1.y, v[6] += x1.z, v[7] += x1.w;
+            }
+        } else {
+            for (int ks = 0; ks < a.KS; ++ks)
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    if (f0 + j < a.N) v[j] += p[j];
-            }
+                    if (f0 + j < a.N) v[j] += P[ks * st + j];
         }
         const float* bz = a.bias[g];
 #pragma unroll
@@ -299,7 +317,7 @@ __global__ __launch_bounds__(256) void k_wl_act(WlAct a) {
             }
         }
     }
-    h8* o = reinterpret_cast<h8*>(a.out[g]) + (blk * 2) * 64 + lane;
+    h8* o = reinterpret_cast<h8*>(a.out[g]) + ((int64_t)((m >> 4) * a.KBo + kb) * 2) * 64 + 16 * q + (m & 15);
     o[0] = hi;
     o[64] = lo;
 }
@@ -324,7 +342,7 @@ struct WlRows {
     int h, KS, M, MT, KBf;
 };
 
-constexpr int kRowThreads = 256;
+constexpr int kRowThreads = 1024;  // one thread per column at Polymer_rnvp's half of 1024
 
 __global__ __launch_bounds__(kRowThreads) void k_wl_rows(WlRows a) {
     extern __shared__ float rowv[];  // the row's values (h floats) when fragments are written
@@ -419,28 +437,32 @@ struct WlPlan {
 };
 
 WlPlan wl_plan(int N, int KB, int MT) {
+    // one round of workgroups over the CUs (one 4-wave workgroup each), as few
+    // k splits (partial sums) as that allows: two output tiles per wave where
+    // that still gives >= 3/4 of a round, else one
     WlPlan p{};
     const int NT = (N + 15) / 16;
-    const int kcmax = (int)(kWlLdsMax / ((size_t)MT * 2048));
-    int ksmin = (KB + kcmax - 1) / kcmax;
-    // two tiles per wave where the feature blocks alone nearly cover the GPU
-    p.NTW = (2 * ((NT + 7) / 8) * ksmin >= kWlTarget) ? 2 : 1;
-    p.nblk = (NT + kWlWaves * p.NTW - 1) / (kWlWaves * p.NTW);
-    int ks = (kWlTarget + 2 * p.nblk - 1) / (2 * p.nblk);
-    ks = ks > ksmin ? ks : ksmin;
-    ks = ks < KB ? ks : KB;
-    p.KC = (KB + ks - 1) / ks;
-    p.KS = (KB + p.KC - 1) / p.KC;
-    p.lds = (size_t)MT * p.KC * 2048;
+    for (int ntw = 2; ntw >= 1; --ntw) {
+        const int nblk = (NT + kWlWaves * ntw - 1) / (kWlWaves * ntw);
+        int ks = kWlTarget / (2 * nblk);
+        ks = ks < 1 ? 1 : (ks > KB ? KB : ks);
+        const int kc = (KB + ks - 1) / ks;
+        ks = (KB + kc - 1) / kc;
+        p = WlPlan{ntw, ks, kc, nblk, 0};
+        if (4 * 2 * nblk * ks >= 3 * kWlTarget) break;
+    }
+    // (at least 84 KiB: one workgroup per CU, so the round spreads over every CU)
+    p.lds = (size_t)kWlRing * 2 * MT * 1024;
+    p.lds = p.lds > (size_t)84 * 1024 ? p.lds : (size_t)84 * 1024;
     return p;
 }
 
 template <int MT, int NTW>
 int wl_gemm_launch(const WlGemm& a, const WlPlan& p, hipStream_t st) {
-    static bool attr = false;  // (every instance sets its dynamic-LDS cap once)
+    static bool attr = false;  // (every instance sets its dynamic-LDS size once)
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wl_gemm<MT, NTW>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWlLdsMax);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     hipLaunchKernelGGL((k_wl_gemm<MT, NTW>), dim3((unsigned)(2 * p.nblk * p.KS)), dim3(64 * kWlWaves), p.lds, st,
