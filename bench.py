@@ -91,11 +91,16 @@ WORKLOADS = {
     # config.py:40 (100), nlayers 2, B = ncellx * cell_len / 2 = 0.5
     "poly2048": ("2048-dim synthetic Gaussian, NSF_AR autoregressive RQS (Polymer.yaml: K=32, H=100, "
                  "B=0.5, 2 layers), log_prob", "NSF_AR", dict(dim=2048, K=32, B=0.5, hidden_dim=100), 2048, 2),
+    # Polymer_rnvp.yaml's flow, the config the reference's Polymer driver loads
+    # (applications/examples/polymer.py:29): RealNVP(2048, hidden 4000) x 10,
+    # batch 40 (:30); each layer is its 387 MB of weights at these batches
+    "rnvp2048": ("2048-dim synthetic Gaussian, 10-layer RealNVP affine coupling (Polymer_rnvp.yaml: H=4000), "
+                 "log_prob", "RealNVP", dict(dim=2048, hidden_dim=4000), 2048, 10),
 }
 # default per-GPU rows: c1 is BASELINE's 4,096-row case; ar354 runs at its
 # configs' own training batch (Einstein.yaml / LJ.yaml batch_size 40), where
 # the fused layer splits its conditioners over the GPU (nfk_fused_ar_ws)
-DEFAULT_BATCH = {"c1": 4096, "ar354": 40, "fe162": 50, "poly2048": 40}
+DEFAULT_BATCH = {"c1": 4096, "ar354": 40, "fe162": 50, "poly2048": 40, "rnvp2048": 40}
 # BASELINE.md's figures for the same metric and config: the reference's own
 # CPU path measured in the survey container (8-core Xeon, 8 threads, fp32;
 # no GPU figures exist): c1 at B = 4096, c2 and c3 at B = 2^20 (c5 is quoted
@@ -135,6 +140,7 @@ METRICS = {
     "ar354": "samples/sec log_prob (96-dim rows, 2 NSF_AR autoregressive RQS layers, K=32, H=354; rows per step = config.global_batch, default the applications' 40)",
     "fe162": "samples/sec log_prob (162-dim rows, 2 NSF_AR autoregressive RQS layers, K=32, H=354; rows per step = config.global_batch, default the Fe configs' 50)",
     "poly2048": "samples/sec log_prob (2048-dim rows, 2 NSF_AR autoregressive RQS layers, K=32, H=100; rows per step = config.global_batch, default Polymer.yaml's 40)",
+    "rnvp2048": "samples/sec log_prob (2048-dim rows, 10 RealNVP affine coupling layers, H=4000; rows per step = config.global_batch, default Polymer_rnvp.yaml's 40)",
 }
 
 
@@ -152,6 +158,7 @@ ARITH = {
     "fe162": _SPLIT + "; the 2 tail features of H=354 as one 16x16x16 f16 MFMA per tile"
              " (nfk_fused_ar.hip, one wave per SIMD; layer 1 on the fp16-split trig features)",
     "poly2048": _SPLIT + _TAIL + " (nfk_fused_ar.hip; layer 1 on the fp16-split trig features)",
+    "rnvp2048": _SPLIT + " (nfk_wide_rnvp.hip: split-K weight-stream GEMMs, fp32 partial sums added in split order)",
 }
 # the line's dtype: what the path computes in (fp32 values and outputs; the
 # conditioner's products on the fp16 matrix cores as a two-way split)
@@ -487,6 +494,19 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
         return out
     if name == "nfk_fused_ar":
         return roofline_ar(kw, B, L * n_steps / n_launch, n_launch, mean_ms, traffic, insts)
+    if name == "nfk_wide_rnvp":
+        # one layer per launch: its four FCNNs' weights read once (fp16 hi + lo:
+        # 4 B per weight, the fp32 bytes) + x in, z out, log|det| RMW
+        D2, H = kw["dim"] // 2, kw["hidden_dim"]
+        wts = 4 * 4 * (D2 * H + H + H * H + H + H * D2 + D2)
+        byts = wts + (2 * kw["dim"] * 4 + 8) * B
+        achieved = byts / (mean_ms * 1e-3) / 1e9
+        return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                **hbm_fields(traffic, byts, mean_ms), "launches": n_launch, "mean_ms": round(mean_ms, 4),
+                "floor_ms": round(byts / (PEAK_HBM_GBS * 1e9) * 1e3, 4),
+                "per_launch": "%d samples x 1 layer: %d B algorithmic (the layer's weights once + x, z, "
+                              "log|det|; the kernel streams them once per 128-row pass)" % (B, byts)}
     if name == "nfk_rqs_coupling" and kind == "NSF_AR":
         P = 3 * kw["K"] - 1
         byts = (4 + P * 4 + 4 + 8) * B                            # one column: x, params, z, log|det| RMW
@@ -701,10 +721,11 @@ def main():
         step -- the small-batch workloads (c1) and per-rank batches of at most
         2^17 rows (the 8-GPU strong-scaling shard), where the host-side launch
         and status-copy overhead is ~2 % of a step.  Not the NSF_AR workloads
-        (ar354, fe162, poly2048), whose roofline needs the kernel timer."""
+        (ar354, fe162, poly2048) or rnvp2048, whose roofline needs the kernel timer."""
         if args.graph != "auto":
             return args.graph == "on"
-        return args.workload == "c1" or (B <= (1 << 17) and WORKLOADS[args.workload][1] != "NSF_AR")
+        return args.workload == "c1" or (B <= (1 << 17) and WORKLOADS[args.workload][1] != "NSF_AR"
+                                         and args.workload != "rnvp2048")
 
     def run(mode):
         """One mode's timed loop: W warm-up steps, then K steps bracketed by a
