@@ -512,6 +512,27 @@ int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const 
                   int32_t hidden, float* z, int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
                   int32_t inverse, float* workspace, int64_t workspace_floats, nfk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * NSF_AR inverse for the layers the fused kernel's inverse does not take
+ * (nfk_fused_ar_inverse_supported == 0: Polymer.yaml's 2,048 coordinates),
+ * nfk_ar_seqinv.hip: NSF_AR.inverse (nf/flows.py:193-209) column by column,
+ * two launches per coordinate issued from the library (conditioner i's layer 1
+ * split over workgroups, then its layers 2-3, the spline's inverse and the
+ * trig features of x_i in one workgroup), fp32 arithmetic, the weights read in
+ * place.  weights: a DEVICE table of 6 (dim - 1) pointers (W1, b1, W2, b2, W3,
+ * b3 of conditioners 1 .. dim-1, fp32 contiguous nn.Linear tensors: the same
+ * table nfk_fused_ar_pack reads); init_param [3K-1].  z -> x [batch, dim],
+ * logdet mode 0/1/2 (the inverse's -log|det|), status [dim] (nullable).
+ * workspace: nfk_ar_seqinv_workspace(dim, hidden, K, batch) floats.  64 rows
+ * per pass.  hidden <= 128, K in {4, 8, 10, 16, 32}.
+ * ------------------------------------------------------------------------- */
+int nfk_ar_seqinv_supported(int32_t dim, int32_t hidden, int32_t K);
+int64_t nfk_ar_seqinv_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch);
+int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* weights, const float* init_param, int32_t dim,
+                  int32_t hidden, int32_t K, double tail_bound, float* x, int64_t ldx, float* logdet,
+                  int32_t logdet_mode, int64_t batch, int32_t* status, float* workspace, int64_t workspace_floats,
+                  nfk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,9 @@ USE_WIDE_RNVP  RealNVP layers whose conditioners are too wide for the fused kern
                (nfk_wide_rnvp: every Linear packed once, each weight read once
                per layer) at batches of at most WIDE_RNVP_MAX_ROWS rows (128 per
                pass); larger batches, or off: library GEMMs + the affine kernel.
+USE_AR_SEQINV  the NSF_AR inverse of layers the fused inverse does not take (Polymer's
+               2,048 coordinates) through nfk_ar_seqinv (two launches per column
+               issued by the library, fp32); off: the per-column host loop.
 """
 STRICT_CHECKS = True
 USE_FUSED = True
@@ -63,3 +66,4 @@ AR_BATCHED_VJP_BYTES = 4 << 30
 AR_WORKSPACE_BYTES = 1 << 30
 USE_WIDE_RNVP = True
 WIDE_RNVP_MAX_ROWS = 1024
+USE_AR_SEQINV = True

@@ -1,0 +1,255 @@
+// nfk_ar_seqinv.hip -- the NSF_AR inverse (nf/flows.py:193-209) for the layers
+// whose inverse the fused register form cannot hold: Polymer.yaml's 2,048
+// coordinates (applications/input/Polymer.yaml:8-9, 17-18; sampled by the
+// applications' sample() calls, nf/models.py:31-35).
+//
+// The inverse is sequential: conditioner i reads the trig features of the
+// coordinates already inverted (x[:, :i], flows.py:201), so coordinate i waits
+// for i - 1.  Per coordinate, two launches driven from C++ (no host round trip
+// and no Python between them):
+//
+//   k_sq_l1   layer 1 of conditioner i, [M, 2i] x W1_i^T, the 2i features split
+//             into 64-feature chunks over workgroups (W1_i is up to 100 x 4,094
+//             at Polymer: 1.6 MB); fp32 partial sums per chunk
+//   k_sq_fin  one workgroup: the chunks summed in order + b1, tanh, layer 2,
+//             tanh, the output layer (95 logits per row), the spline's inverse
+//             (nfk_rqs_element_lean: the reference's 2B softmax / softplus,
+//             then RQS, utils.py:27-152), x[:, i], the row's log|det| summed in
+//             column order (flows.py:208), the status word of column i, and
+//             cos / sin (pi x_i / B) for the later conditioners (flows.py:172-173)
+//
+// The conditioners' nn.Linear weights are read in place (fp32, a device table
+// of their pointers: the fused pack's table), and the arithmetic is fp32 FMA
+// throughout: the inverse is latency-bound (4,095 dependent launches per layer
+// at Polymer's shape), not bandwidth- or FLOP-bound, and every weight is read
+// once per layer (1.68 GB at Polymer, 0.2 ms of HBM time).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/nfk.h"
+#include "nfk_spline.h"
+
+int nfk_set_error(const char* msg);  // nfk_kernels.hip
+NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, double top, int tails, double min_w,
+                              double min_h, double min_d);
+
+namespace {
+
+constexpr int kSqFC = 64;        // layer-1 features per workgroup
+constexpr int kSqThreads = 256;  // k_sq_l1
+constexpr int kSqFin = 1024;     // k_sq_fin
+constexpr int kSqMaxRows = 64;   // rows per pass
+constexpr int kSqMaxH = 128;     // hidden width the LDS tiles hold
+
+struct SqArgs {
+    const float* const* w;  // [6 (dim - 1)]: conditioner i = 1 .. dim-1: W1 [H, 2i], b1, W2 [H, H], b2, W3 [P, H], b3
+    const float* init;      // init_param [P]
+    const float* z;         // this pass's rows of the layer input
+    int64_t ldz;
+    float* x;               // ... of the output
+    int64_t ldx;
+    float* feat;            // [2][M][dim]: cos, sin (pi x / B) of the inverted coordinates
+    float* part;            // [chunks][M][H] layer-1 partial sums
+    float* ldacc;           // [M] the rows' log|det| so far (column order)
+    float* logdet;          // [M] (this pass's rows) or null
+    int32_t* status;        // [dim] or null
+    int mode, dim, H, M;
+    float pi, bnd;
+    NfkSplineConst c;
+};
+
+__global__ __launch_bounds__(kSqThreads) void k_sq_l1(SqArgs a, int i) {
+    __shared__ float ws[kSqMaxH][kSqFC + 1];     // W1_i rows h, features f0 .. f0 + 63
+    __shared__ float fs[kSqMaxRows][kSqFC + 1];  // the rows' features
+    const int F = 2 * i, f0 = blockIdx.x * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
+    const float* W1 = a.w[6 * (i - 1)];
+    for (int e = threadIdx.x; e < a.H * kSqFC; e += kSqThreads) {
+        const int h = e / kSqFC, f = e - h * kSqFC;
+        ws[h][f] = f < nf ? W1[(int64_t)h * F + f0 + f] : 0.0f;
+    }
+    // feature f of conditioner i: cos(pi x_f / B) for f < i, sin(pi x_(f-i) / B)
+    // above (trig_transform's cat, flows.py:172-173)
+    for (int e = threadIdx.x; e < a.M * kSqFC; e += kSqThreads) {
+        const int m = e / kSqFC, f = e - m * kSqFC, g = f0 + f;
+        float v = 0.0f;
+        if (f < nf) v = g < i ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)a.M + m) * a.dim + (g - i)];
+        fs[m][f] = v;
+    }
+    __syncthreads();
+    float* P = a.part + (int64_t)blockIdx.x * a.M * a.H;
+    for (int e = threadIdx.x; e < a.M * a.H; e += kSqThreads) {
+        const int m = e / a.H, h = e - m * a.H;
+        float s = 0.0f;
+        for (int f = 0; f < nf; ++f) s = __builtin_fmaf(fs[m][f], ws[h][f], s);
+        P[e] = s;
+    }
+}
+
+// dynamic LDS of k_sq_fin: h1 [M][H+1], h2 [M][H+1], logits [M][P+1]
+inline size_t sq_fin_lds(int M, int H, int K) { return (size_t)M * (2 * (H + 1) + 3 * K) * sizeof(float); }
+
+template <int K>
+__global__ __launch_bounds__(kSqFin) void k_sq_fin(SqArgs a, int i, int nch) {
+    constexpr int P = 3 * K - 1;
+    extern __shared__ float sq_lds[];
+    __shared__ int bits;
+    const int H = a.H, M = a.M, HS = H + 1;
+    float* h1 = sq_lds;
+    float* h2 = h1 + M * HS;
+    float* lg = h2 + M * HS;  // row stride P + 1
+    if (i == 0) {
+        // coordinate 0: init_param, the same logits for every row (flows.py:196-199)
+        for (int e = threadIdx.x; e < M * P; e += kSqFin) {
+            const int m = e / P, p = e - m * P;
+            lg[m * (P + 1) + p] = a.init[p];
+        }
+    } else {
+        const float* const* w = a.w + 6 * (i - 1);
+        const float *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
+        for (int e = threadIdx.x; e < M * H; e += kSqFin) {
+            const int m = e / H, h = e - m * H;
+            float s = 0.0f;
+            for (int c = 0; c < nch; ++c) s += a.part[((int64_t)c * M + m) * H + h];
+            h1[m * HS + h] = tanhf(s + b1[h]);
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < M * H; e += kSqFin) {
+            const int m = e / H, h = e - m * H;
+            const float* wr = W2 + (int64_t)h * H;
+            float s = 0.0f;
+            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h1[m * HS + k], wr[k], s);
+            h2[m * HS + h] = tanhf(s + b2[h]);
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < M * P; e += kSqFin) {
+            const int m = e / P, p = e - m * P;
+            const float* wr = W3 + (int64_t)p * H;
+            float s = 0.0f;
+            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h2[m * HS + k], wr[k], s);
+            lg[m * (P + 1) + p] = s + b3[p];
+        }
+    }
+    __syncthreads();
+    // the spline of column i, one row per thread
+    const int m = threadIdx.x;
+    bool in = false, nd = false;
+    if (m < M) {
+        float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
+        const float* lr = lg + m * (P + 1);
+#pragma unroll
+        for (int p = 0; p < K; ++p) wr[p] = lr[p];
+#pragma unroll
+        for (int p = 0; p < K; ++p) hr[p] = lr[K + p];
+#pragma unroll
+        for (int p = 0; p < K - 1; ++p) dr[p] = lr[2 * K + p];
+        const float zv = a.z[(int64_t)m * a.ldz + i];
+        float out, lad;
+        nfk_rqs_element_lean<K, true>(zv, wr, hr, dr, a.c, out, lad, in, nd);
+        a.x[(int64_t)m * a.ldx + i] = out;
+        const float acc = (i == 0 ? 0.0f : a.ldacc[m]) + lad;
+        if (i + 1 < a.dim) {
+            a.ldacc[m] = acc;
+            const float arg = (a.pi * out) / a.bnd;  // (pi x) / B, flows.py:173's operation order
+            a.feat[(int64_t)m * a.dim + i] = cosf(arg);
+            a.feat[((int64_t)M + m) * a.dim + i] = sinf(arg);
+        } else if (a.logdet != nullptr && a.mode != 0) {
+            a.logdet[m] = a.mode == 2 ? a.logdet[m] + acc : acc;
+        }
+    }
+    if (a.status != nullptr) {
+        const bool ins = __any(in), neg = __any(in && nd);
+        if (threadIdx.x == 0) bits = 0;
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0 && (ins || neg))
+            atomicOr(&bits, (ins ? NFK_ST_INSIDE_SEEN : 0) | (neg ? NFK_ST_NEG_DISC : 0));
+        __syncthreads();
+        if (threadIdx.x == 0 && bits != 0 && (a.status[i] & bits) != bits) atomicOr(a.status + i, bits);
+    }
+}
+
+int sq_status() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        nfk_set_error("nfk_ar_seqinv: launch failed");
+        return (int)e;
+    }
+    return 0;
+}
+
+int64_t sq_chunks(int dim) { return (2LL * (dim - 1) + kSqFC - 1) / kSqFC; }
+
+}  // namespace
+
+extern "C" int nfk_ar_seqinv_supported(int32_t dim, int32_t hidden, int32_t K) {
+    const bool k_ok = K == 4 || K == 8 || K == 10 || K == 16 || K == 32;
+    return (dim >= 2 && dim <= 65536 && hidden >= 1 && hidden <= kSqMaxH && k_ok) ? 1 : 0;
+}
+
+extern "C" int64_t nfk_ar_seqinv_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch) {
+    if (!nfk_ar_seqinv_supported(dim, hidden, K) || batch <= 0) return 0;
+    const int64_t M = batch < kSqMaxRows ? batch : kSqMaxRows;
+    return 2 * M * dim + sq_chunks(dim) * M * hidden + M;
+}
+
+extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* weights, const float* init_param,
+                             int32_t dim, int32_t hidden, int32_t K, double tail_bound, float* x, int64_t ldx,
+                             float* logdet, int32_t logdet_mode, int64_t batch, int32_t* status, float* workspace,
+                             int64_t workspace_floats, nfk_stream_t stream) {
+    if (!nfk_ar_seqinv_supported(dim, hidden, K)) return nfk_set_error("nfk_ar_seqinv: shape not supported");
+    if (batch < 0) return nfk_set_error("nfk_ar_seqinv: bad batch");
+    if (batch == 0) return 0;
+    if (!z || !weights || !init_param || !x || !workspace) return nfk_set_error("nfk_ar_seqinv: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_ar_seqinv: null logdet");
+    if (ldz < dim || ldx < dim) return nfk_set_error("nfk_ar_seqinv: bad leading dimension");
+    if (workspace_floats < nfk_ar_seqinv_workspace(dim, hidden, K, batch))
+        return nfk_set_error("nfk_ar_seqinv: workspace too small (nfk_ar_seqinv_workspace)");
+    hipStream_t st = (hipStream_t)stream;
+    for (int64_t r0 = 0; r0 < batch; r0 += kSqMaxRows) {
+        const int M = (int)(batch - r0 < kSqMaxRows ? batch - r0 : kSqMaxRows);
+        SqArgs a;
+        a.w = weights;
+        a.init = init_param;
+        a.z = z + r0 * ldz;
+        a.ldz = ldz;
+        a.x = x + r0 * ldx;
+        a.ldx = ldx;
+        a.feat = workspace;
+        a.part = workspace + 2LL * M * dim;
+        a.ldacc = a.part + sq_chunks(dim) * M * hidden;
+        a.logdet = logdet_mode != 0 ? logdet + r0 : nullptr;
+        a.status = status;
+        a.mode = logdet_mode;
+        a.dim = dim;
+        a.H = hidden;
+        a.M = M;
+        a.pi = (float)M_PI;  // torch.tensor(np.pi) times an fp32 tensor: an fp32 product
+        a.bnd = (float)tail_bound;
+        // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:206-207)
+        a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+        const size_t lds = sq_fin_lds(M, hidden, K);
+        static bool attr = false;
+        if (!attr) {
+#define NFK_SQ_ATTR(k) \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sq_fin<k>), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              (int)sq_fin_lds(kSqMaxRows, kSqMaxH, k));
+            NFK_SQ_ATTR(4) NFK_SQ_ATTR(8) NFK_SQ_ATTR(10) NFK_SQ_ATTR(16) NFK_SQ_ATTR(32)
+#undef NFK_SQ_ATTR
+            attr = true;
+        }
+        for (int i = 0; i < dim; ++i) {
+            const int nch = (2 * i + kSqFC - 1) / kSqFC;
+            if (i > 0) {
+                hipLaunchKernelGGL(k_sq_l1, dim3((unsigned)nch), dim3(kSqThreads), 0, st, a, i);
+                if (int e = sq_status()) return e;
+            }
+#define NFK_SQ_FIN(k) \
+    if (K == k) hipLaunchKernelGGL(k_sq_fin<k>, dim3(1), dim3(kSqFin), lds, st, a, i, nch);
+            NFK_SQ_FIN(4) NFK_SQ_FIN(8) NFK_SQ_FIN(10) NFK_SQ_FIN(16) NFK_SQ_FIN(32)
+#undef NFK_SQ_FIN
+            if (int e = sq_status()) return e;
+        }
+    }
+    return 0;
+}

@@ -904,7 +904,15 @@ class NSF_AR(_HipFlow):
         n = x.shape[0]
         pack = self._fused_pack(x.device)
         if pack is not None and inverse and not K_.fused_ar_inverse_supported(self.dim, self._pack_cache[2], self.K):
-            pack = None  # (a streamed-forward shape: the inverse runs per column)
+            # a streamed-forward shape (Polymer's 2,048 coordinates): the inverse
+            # column by column, both launches per column issued by the library
+            hidden, keep = self._pack_cache[2], self._pack_cache[3]
+            if config.USE_AR_SEQINV and K_.ar_seqinv_supported(self.dim, hidden, self.K):
+                z = torch.empty_like(x, memory_format=torch.contiguous_format)
+                K_.ar_seqinv(x, keep[0], keep[1], self.dim, hidden, self.K, float(self.B), z, logdet=logdet,
+                             logdet_mode=mode, status=status)
+                return z
+            pack = None  # (the per-column path below)
         if pack is not None:
             z = torch.empty_like(x, memory_format=torch.contiguous_format)
             K_.fused_ar(x, pack, self.dim, self._pack_cache[2], self.K, float(self.B), z, logdet=logdet,

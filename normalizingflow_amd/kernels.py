@@ -793,3 +793,28 @@ def wide_rnvp(x, packs, biases, half, hidden, z, *, logdet, logdet_mode, inverse
     _timed("nfk_wide_rnvp", dev, "nfk_wide_rnvp", xp, ldx, ctypes.addressof(pk), ctypes.addressof(bs), half, hidden,
            zp, ldz, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, ws.data_ptr(), nws,
            _stream(dev))
+
+
+# ---- NSF_AR inverse, column by column from the library (nfk_ar_seqinv.hip)
+def ar_seqinv_supported(dim, hidden, K):
+    return bool(_lib.load().nfk_ar_seqinv_supported(dim, hidden, K))
+
+
+def ar_seqinv(z, table, init_param, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, status=None):
+    """NSF_AR.inverse of one layer (include/nfk.h nfk_ar_seqinv): ``table`` is
+    the device table of the conditioners' Linear tensors that fused_ar_pack
+    built (6 per conditioner)."""
+    dev = _require_hip(z, table, init_param, out, logdet, status)
+    B = z.shape[0]
+    zp, ldz = _mat(z, "z")
+    op, ldo = _mat(out, "out")
+    if z.shape[1] != dim or out.shape != z.shape:
+        raise ValueError("ar_seqinv: z and out must be [B, %d]" % dim)
+    if table.dtype != torch.int64 or table.numel() != 6 * (dim - 1):
+        raise ValueError("ar_seqinv: the pointer table must hold 6 (dim - 1) int64 entries")
+    lib = _lib.load()
+    nws = int(lib.nfk_ar_seqinv_workspace(dim, hidden, K, B))
+    ws = torch.empty(max(nws, 4), dtype=F32, device=dev)
+    _timed("nfk_ar_seqinv", dev, "nfk_ar_seqinv", zp, ldz, table.data_ptr(), _vec(init_param, 3 * K - 1, "init_param"),
+           dim, hidden, K, float(tail_bound), op, ldo, _vec(logdet, B, "logdet"), logdet_mode, B,
+           _vec(status, dim, "status", torch.int32), ws.data_ptr(), nws, _stream(dev))

@@ -491,3 +491,81 @@ def test_fused_ar_app_model_log_prob(dim, H, B, rows, hip_device):
     print("dim %d log_prob: max |ours - fp64| %.3g, max |oracle fp32 - fp64| %.3g" % (dim, e_ours, e_ref))
     assert e_ours <= 2 * e_ref + 1e-5 * float(ref64.abs().max()), (e_ours, e_ref)
     flush_status_checks()
+
+
+@pytest.mark.parametrize("dim,K,rows", [(96, 32, 77), (40, 32, 40), (130, 32, 5)])
+def test_ar_seqinv_vs_oracle(dim, K, rows, hip_device):
+    """The library-driven column-by-column inverse (nfk_ar_seqinv: the layers
+    whose inverse the fused register form does not take; forced here with the
+    streamed form on config.py-shaped layers) against the oracle's inverse,
+    ragged batches over two 64-row passes, log|det| modes 1 and 2, an element
+    outside [-B, B] (the identity tail), run-to-run bitwise."""
+    lib = K_._lib.load()
+    torch.manual_seed(dim + K)
+    layer = nff.NSF_AR(dim=dim, K=K, B=1.5, hidden_dim=100)
+    sd = _sd(layer)
+    layer = layer.to(hip_device)
+    z = torch.randn(rows, dim, generator=torch.Generator().manual_seed(rows)) * 0.7
+    z[0, dim // 3] = 9.0
+    xi_ref, ldi_ref, _, ldi64 = _oracle_ar(z, sd, dim, K, 1.5, inverse=True)
+    zd = z.to(hip_device)
+    prev = lib.nfk_debug_ar_stream(1)
+    try:
+        layer.invalidate_caches()
+        assert not K_.fused_ar_inverse_supported(dim, 100, K)
+        with torch.no_grad():
+            (res, n) = _launches(lambda: layer.inverse(zd))
+            assert n == {"nfk_ar_seqinv": 1}, n
+            xi, ldi = res
+            xi2, ldi2 = layer.inverse(zd)
+            ld0 = torch.linspace(-1.0, 1.0, rows, device=hip_device)
+            out = torch.empty_like(zd)
+            st = torch.zeros(dim, dtype=torch.int32, device=hip_device)
+            keep = layer._pack_cache[3]
+            K_.ar_seqinv(zd, keep[0], keep[1], dim, 100, K, 1.5, out, logdet=ld0, logdet_mode=2, status=st)
+    finally:
+        lib.nfk_debug_ar_stream(prev)
+        layer.invalidate_caches()
+    assert torch.equal(xi, xi2) and torch.equal(ldi, ldi2)
+    close(xi, xi_ref, 1e-5, 1e-4)
+    close_or_on_par(ldi, ldi_ref, ldi64, LD_RTOL, LD_ATOL)
+    assert torch.equal(out, xi)
+    close(ld0 - torch.linspace(-1.0, 1.0, rows, device=hip_device), ldi, 1e-6, 1e-5)
+    assert int(st[dim // 3]) & 1 and all(int(v) & 1 for v in st.cpu())  # NFK_ST_INSIDE_SEEN in every column
+
+
+def test_polymer2048_inverse_speed(hip_device):
+    """Polymer.yaml's layer inverted at the 40-row batch: the library-driven
+    column loop (nfk_ar_seqinv) bitwise-run-to-run, close to the per-column host
+    path, and timed against it."""
+    import time
+    from normalizingflow_amd import config as cfg
+    torch.manual_seed(2049)
+    layer = nff.NSF_AR(dim=2048, K=32, B=0.5, hidden_dim=100).to(hip_device)
+    z = torch.randn(40, 2048, device=hip_device) * 0.2
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    with torch.no_grad():
+        xs, lds = layer.inverse(z)
+        t_seq = timed(lambda: layer.inverse(z), 3)
+        prev = cfg.USE_AR_SEQINV
+        cfg.USE_AR_SEQINV = False
+        try:
+            xc, ldc = layer.inverse(z)
+            t_col = timed(lambda: layer.inverse(z), 1)
+        finally:
+            cfg.USE_AR_SEQINV = prev
+    close(xs, xc, 1e-5, 1e-4)
+    close(lds, ldc, LD_RTOL, 5e-4)
+    print("poly2048 inverse at 40 rows: seqinv %.2f ms, per-column %.2f ms (%.1fx)"
+          % (t_seq * 1e3, t_col * 1e3, t_col / t_seq))
+    assert t_seq < t_col
+    flush_status_checks()
