@@ -37,11 +37,10 @@ NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, d
 
 namespace {
 
-constexpr int kSqFC = 64;        // layer-1 features per workgroup
-constexpr int kSqThreads = 256;  // k_sq_l1
-constexpr int kSqFin = 1024;     // k_sq_fin
+constexpr int kSqFC = 128;       // layer-1 features per k_sq_l1 workgroup
+constexpr int kSqThreads = 256;  // both kernels
 constexpr int kSqMaxRows = 64;   // rows per pass
-constexpr int kSqMaxH = 128;     // hidden width the LDS tiles hold
+constexpr int kSqMaxH = 128;     // hidden width (k_sq_l1's 4 x 4 register tiles: 64 rows x 128)
 
 struct SqArgs {
     const float* const* w;  // [6 (dim - 1)]: conditioner i = 1 .. dim-1: W1 [H, 2i], b1, W2 [H, H], b2, W3 [P, H], b3
@@ -51,121 +50,145 @@ struct SqArgs {
     float* x;               // ... of the output
     int64_t ldx;
     float* feat;            // [2][M][dim]: cos, sin (pi x / B) of the inverted coordinates
-    float* part;            // [chunks][M][H] layer-1 partial sums
+    float* part;            // [M][chunks][H] layer-1 partial sums
     float* ldacc;           // [M] the rows' log|det| so far (column order)
     float* logdet;          // [M] (this pass's rows) or null
     int32_t* status;        // [dim] or null
-    int mode, dim, H, M;
+    int mode, dim, H, M, nchmax;
     float pi, bnd;
     NfkSplineConst c;
 };
 
+// layer 1 of conditioner i over features f0 .. f0 + 127 (workgroup = chunk):
+// the chunk's weights and the rows' features through LDS ([f][h], [f][m]),
+// each thread a 4-row x 4-unit register tile
 __global__ __launch_bounds__(kSqThreads) void k_sq_l1(SqArgs a, int i) {
-    __shared__ float ws[kSqMaxH][kSqFC + 1];     // W1_i rows h, features f0 .. f0 + 63
-    __shared__ float fs[kSqMaxRows][kSqFC + 1];  // the rows' features
+    __shared__ float ws[kSqFC][kSqMaxH];
+    __shared__ float fs[kSqFC][kSqMaxRows];
     const int F = 2 * i, f0 = blockIdx.x * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
+    const int H = a.H, M = a.M;
     const float* W1 = a.w[6 * (i - 1)];
-    for (int e = threadIdx.x; e < a.H * kSqFC; e += kSqThreads) {
-        const int h = e / kSqFC, f = e - h * kSqFC;
-        ws[h][f] = f < nf ? W1[(int64_t)h * F + f0 + f] : 0.0f;
+    for (int e = threadIdx.x; e < H * kSqFC; e += kSqThreads) {
+        const int h = e / kSqFC, f = e - h * kSqFC;  // (consecutive threads: one weight row)
+        ws[f][h] = f < nf ? W1[(int64_t)h * F + f0 + f] : 0.0f;
     }
     // feature f of conditioner i: cos(pi x_f / B) for f < i, sin(pi x_(f-i) / B)
     // above (trig_transform's cat, flows.py:172-173)
-    for (int e = threadIdx.x; e < a.M * kSqFC; e += kSqThreads) {
+    for (int e = threadIdx.x; e < M * kSqFC; e += kSqThreads) {
         const int m = e / kSqFC, f = e - m * kSqFC, g = f0 + f;
         float v = 0.0f;
-        if (f < nf) v = g < i ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)a.M + m) * a.dim + (g - i)];
-        fs[m][f] = v;
+        if (f < nf) v = g < i ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)M + m) * a.dim + (g - i)];
+        fs[f][m] = v;
     }
     __syncthreads();
-    float* P = a.part + (int64_t)blockIdx.x * a.M * a.H;
-    for (int e = threadIdx.x; e < a.M * a.H; e += kSqThreads) {
-        const int m = e / a.H, h = e - m * a.H;
-        float s = 0.0f;
-        for (int f = 0; f < nf; ++f) s = __builtin_fmaf(fs[m][f], ws[h][f], s);
-        P[e] = s;
+    const int HT = (H + 3) / 4, MT4 = (M + 3) / 4;
+    for (int t = threadIdx.x; t < HT * MT4; t += kSqThreads) {
+        const int h0 = 4 * (t % HT), m0 = 4 * (t / HT);
+        float acc[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[r][u] = 0.0f;
+        for (int f = 0; f < nf; ++f) {
+            float fv[4], wv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) fv[r] = fs[f][(m0 + r) & (kSqMaxRows - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) wv[u] = ws[f][(h0 + u) & (kSqMaxH - 1)];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[r][u] = __builtin_fmaf(fv[r], wv[u], acc[r][u]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (m0 + r < M && h0 + u < H)
+                    a.part[((int64_t)(m0 + r) * a.nchmax + blockIdx.x) * H + h0 + u] = acc[r][u];
     }
 }
 
-// dynamic LDS of k_sq_fin: h1 [M][H+1], h2 [M][H+1], logits [M][P+1]
-inline size_t sq_fin_lds(int M, int H, int K) { return (size_t)M * (2 * (H + 1) + 3 * K) * sizeof(float); }
+// dynamic LDS of k_sq_fin: the row's partials [nch][H], h1 [H], h2 [H],
+// logits [P], and one weight matrix at a time (W2 [H][H], then W3 [P][H])
+inline size_t sq_fin_lds(int nch, int H, int K) {
+    const int P = 3 * K - 1;
+    const int wmax = H * H > P * H ? H * H : P * H;
+    return (size_t)(nch * H + 2 * H + P + 1 + wmax) * sizeof(float);
+}
 
+// the rest of conditioner i for ONE row (workgroup = row): the layer-1 chunks
+// summed in order + b1, tanh, layer 2, tanh, the output layer, the spline's
+// inverse, x[m, i], the row's log|det|, the status word, cos / sin of x[m, i]
 template <int K>
-__global__ __launch_bounds__(kSqFin) void k_sq_fin(SqArgs a, int i, int nch) {
+__global__ __launch_bounds__(kSqThreads) void k_sq_fin(SqArgs a, int i, int nch) {
     constexpr int P = 3 * K - 1;
     extern __shared__ float sq_lds[];
-    __shared__ int bits;
-    const int H = a.H, M = a.M, HS = H + 1;
-    float* h1 = sq_lds;
-    float* h2 = h1 + M * HS;
-    float* lg = h2 + M * HS;  // row stride P + 1
+    const int H = a.H, m = blockIdx.x, tid = threadIdx.x;
+    float* pr = sq_lds;        // [nch][H]
+    float* h1 = pr + nch * H;  // [H]
+    float* h2 = h1 + H;        // [H]
+    float* lg = h2 + H;        // [P]
+    float* wl = lg + P + 1;    // W2 or W3 (row-major, as nn.Linear)
     if (i == 0) {
         // coordinate 0: init_param, the same logits for every row (flows.py:196-199)
-        for (int e = threadIdx.x; e < M * P; e += kSqFin) {
-            const int m = e / P, p = e - m * P;
-            lg[m * (P + 1) + p] = a.init[p];
-        }
+        for (int p = tid; p < P; p += kSqThreads) lg[p] = a.init[p];
     } else {
         const float* const* w = a.w + 6 * (i - 1);
         const float *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
-        for (int e = threadIdx.x; e < M * H; e += kSqFin) {
-            const int m = e / H, h = e - m * H;
+        // the row's partials (contiguous) and W2, loads in flight together
+        const float* src = a.part + (int64_t)m * a.nchmax * H;
+        for (int e = tid; e < nch * H; e += kSqThreads) pr[e] = src[e];
+        for (int e = tid; e < H * H; e += kSqThreads) wl[e] = W2[e];
+        __syncthreads();
+        for (int h = tid; h < H; h += kSqThreads) {
             float s = 0.0f;
-            for (int c = 0; c < nch; ++c) s += a.part[((int64_t)c * M + m) * H + h];
-            h1[m * HS + h] = tanhf(s + b1[h]);
+            for (int c = 0; c < nch; ++c) s += pr[c * H + h];
+            h1[h] = tanhf(s + b1[h]);
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < M * H; e += kSqFin) {
-            const int m = e / H, h = e - m * H;
-            const float* wr = W2 + (int64_t)h * H;
+        for (int h = tid; h < H; h += kSqThreads) {
+            const float* wr = wl + h * H;
             float s = 0.0f;
-            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h1[m * HS + k], wr[k], s);
-            h2[m * HS + h] = tanhf(s + b2[h]);
+            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h1[k], wr[k], s);
+            h2[h] = tanhf(s + b2[h]);
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < M * P; e += kSqFin) {
-            const int m = e / P, p = e - m * P;
-            const float* wr = W3 + (int64_t)p * H;
+        for (int e = tid; e < P * H; e += kSqThreads) wl[e] = W3[e];
+        __syncthreads();
+        for (int p = tid; p < P; p += kSqThreads) {
+            const float* wr = wl + p * H;
             float s = 0.0f;
-            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h2[m * HS + k], wr[k], s);
-            lg[m * (P + 1) + p] = s + b3[p];
+            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h2[k], wr[k], s);
+            lg[p] = s + b3[p];
         }
     }
     __syncthreads();
-    // the spline of column i, one row per thread
-    const int m = threadIdx.x;
-    bool in = false, nd = false;
-    if (m < M) {
-        float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
-        const float* lr = lg + m * (P + 1);
+    if (tid != 0) return;
+    float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
 #pragma unroll
-        for (int p = 0; p < K; ++p) wr[p] = lr[p];
+    for (int p = 0; p < K; ++p) wr[p] = lg[p];
 #pragma unroll
-        for (int p = 0; p < K; ++p) hr[p] = lr[K + p];
+    for (int p = 0; p < K; ++p) hr[p] = lg[K + p];
 #pragma unroll
-        for (int p = 0; p < K - 1; ++p) dr[p] = lr[2 * K + p];
-        const float zv = a.z[(int64_t)m * a.ldz + i];
-        float out, lad;
-        nfk_rqs_element_lean<K, true>(zv, wr, hr, dr, a.c, out, lad, in, nd);
-        a.x[(int64_t)m * a.ldx + i] = out;
-        const float acc = (i == 0 ? 0.0f : a.ldacc[m]) + lad;
-        if (i + 1 < a.dim) {
-            a.ldacc[m] = acc;
-            const float arg = (a.pi * out) / a.bnd;  // (pi x) / B, flows.py:173's operation order
-            a.feat[(int64_t)m * a.dim + i] = cosf(arg);
-            a.feat[((int64_t)M + m) * a.dim + i] = sinf(arg);
-        } else if (a.logdet != nullptr && a.mode != 0) {
-            a.logdet[m] = a.mode == 2 ? a.logdet[m] + acc : acc;
-        }
+    for (int p = 0; p < K - 1; ++p) dr[p] = lg[2 * K + p];
+    const float zv = a.z[(int64_t)m * a.ldz + i];
+    float out, lad;
+    bool in, nd;
+    nfk_rqs_element_lean<K, true>(zv, wr, hr, dr, a.c, out, lad, in, nd);
+    a.x[(int64_t)m * a.ldx + i] = out;
+    const float acc = (i == 0 ? 0.0f : a.ldacc[m]) + lad;
+    if (i + 1 < a.dim) {
+        a.ldacc[m] = acc;
+        const float arg = (a.pi * out) / a.bnd;  // (pi x) / B, flows.py:173's operation order
+        a.feat[(int64_t)m * a.dim + i] = cosf(arg);
+        a.feat[((int64_t)a.M + m) * a.dim + i] = sinf(arg);
+    } else if (a.logdet != nullptr && a.mode != 0) {
+        a.logdet[m] = a.mode == 2 ? a.logdet[m] + acc : acc;
     }
     if (a.status != nullptr) {
-        const bool ins = __any(in), neg = __any(in && nd);
-        if (threadIdx.x == 0) bits = 0;
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0 && (ins || neg))
-            atomicOr(&bits, (ins ? NFK_ST_INSIDE_SEEN : 0) | (neg ? NFK_ST_NEG_DISC : 0));
-        __syncthreads();
-        if (threadIdx.x == 0 && bits != 0 && (a.status[i] & bits) != bits) atomicOr(a.status + i, bits);
+        const int bits = (in ? NFK_ST_INSIDE_SEEN : 0) | (in && nd ? NFK_ST_NEG_DISC : 0);
+        if (bits != 0 && (a.status[i] & bits) != bits) atomicOr(a.status + i, bits);
     }
 }
 
@@ -178,19 +201,21 @@ int sq_status() {
     return 0;
 }
 
-int64_t sq_chunks(int dim) { return (2LL * (dim - 1) + kSqFC - 1) / kSqFC; }
+int sq_chunks(int dim) { return (int)((2LL * (dim - 1) + kSqFC - 1) / kSqFC); }
 
 }  // namespace
 
 extern "C" int nfk_ar_seqinv_supported(int32_t dim, int32_t hidden, int32_t K) {
     const bool k_ok = K == 4 || K == 8 || K == 10 || K == 16 || K == 32;
-    return (dim >= 2 && dim <= 65536 && hidden >= 1 && hidden <= kSqMaxH && k_ok) ? 1 : 0;
+    // (k_sq_fin's LDS: the row's layer-1 chunks, the activations, one weight matrix)
+    const bool lds_ok = dim >= 2 && sq_fin_lds(sq_chunks(dim), hidden, K) <= (size_t)160 * 1024;
+    return (dim >= 2 && dim <= 65536 && hidden >= 1 && hidden <= kSqMaxH && k_ok && lds_ok) ? 1 : 0;
 }
 
 extern "C" int64_t nfk_ar_seqinv_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch) {
     if (!nfk_ar_seqinv_supported(dim, hidden, K) || batch <= 0) return 0;
     const int64_t M = batch < kSqMaxRows ? batch : kSqMaxRows;
-    return 2 * M * dim + sq_chunks(dim) * M * hidden + M;
+    return 2 * M * dim + (int64_t)sq_chunks(dim) * M * hidden + M;
 }
 
 extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* weights, const float* init_param,
@@ -217,7 +242,8 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         a.ldx = ldx;
         a.feat = workspace;
         a.part = workspace + 2LL * M * dim;
-        a.ldacc = a.part + sq_chunks(dim) * M * hidden;
+        a.ldacc = a.part + (int64_t)sq_chunks(dim) * M * hidden;
+        a.nchmax = sq_chunks(dim);
         a.logdet = logdet_mode != 0 ? logdet + r0 : nullptr;
         a.status = status;
         a.mode = logdet_mode;
@@ -228,12 +254,11 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         a.bnd = (float)tail_bound;
         // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:206-207)
         a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
-        const size_t lds = sq_fin_lds(M, hidden, K);
         static bool attr = false;
         if (!attr) {
-#define NFK_SQ_ATTR(k) \
+#define NFK_SQ_ATTR(k)                                                                                        \
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sq_fin<k>), hipFuncAttributeMaxDynamicSharedMemorySize, \
-                              (int)sq_fin_lds(kSqMaxRows, kSqMaxH, k));
+                              160 * 1024);
             NFK_SQ_ATTR(4) NFK_SQ_ATTR(8) NFK_SQ_ATTR(10) NFK_SQ_ATTR(16) NFK_SQ_ATTR(32)
 #undef NFK_SQ_ATTR
             attr = true;
@@ -244,8 +269,9 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
                 hipLaunchKernelGGL(k_sq_l1, dim3((unsigned)nch), dim3(kSqThreads), 0, st, a, i);
                 if (int e = sq_status()) return e;
             }
+            const size_t lds = sq_fin_lds(nch, hidden, K);
 #define NFK_SQ_FIN(k) \
-    if (K == k) hipLaunchKernelGGL(k_sq_fin<k>, dim3(1), dim3(kSqFin), lds, st, a, i, nch);
+    if (K == k) hipLaunchKernelGGL(k_sq_fin<k>, dim3((unsigned)M), dim3(kSqThreads), lds, st, a, i, nch);
             NFK_SQ_FIN(4) NFK_SQ_FIN(8) NFK_SQ_FIN(10) NFK_SQ_FIN(16) NFK_SQ_FIN(32)
 #undef NFK_SQ_FIN
             if (int e = sq_status()) return e;

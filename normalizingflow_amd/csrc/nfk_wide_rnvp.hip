@@ -46,9 +46,12 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kWlWaves = 4;                    // waves per GEMM workgroup (one per SIMD)
-constexpr int kWlPF = 8;                       // k-blocks of weights in flight per wave
-constexpr int kWlRing = kWlPF + 1;             // LDS slots of input fragments
+// GEMM workgroup shapes (waves NW, output tiles per wave NTW, k-blocks of
+// weights in flight per wave PF; 8 output tiles per workgroup either way):
+// up to 64 rows, 8 waves (two per SIMD) of one tile 16 k-blocks ahead -- twice
+// the bytes in flight of 4 waves x 2 tiles x 8; above, 4 x 2 x 8 (the input
+// ring of 16 + 1 slots would not fit the LDS)
+constexpr int kWlTilesPerWG = 8;
 constexpr int kWlMaxMT = 8;                    // sample tiles per pass: 128 rows
 constexpr int kWlHdr = 64;                     // pack header floats ([0] = 2^-s)
 constexpr float kWlAct = 16384.0f;             // tanh outputs split at 2^14
@@ -134,8 +137,9 @@ struct WlGemm {
     int KS, KC, M, nblk;   // splits, k-blocks per split, rows, feature blocks per group
 };
 
-template <int MT, int NTW>
-__global__ __launch_bounds__(64 * kWlWaves, 1) void k_wl_gemm(WlGemm a) {
+template <int MT, int NTW, int NW, int PF>
+__global__ __launch_bounds__(64 * NW, 1) void k_wl_gemm(WlGemm a) {
+    constexpr int kWlWaves = NW, kWlPF = PF, kWlRing = PF + 1;
     // the input fragments of k-block kk of the chunk: 2 MT 1-KiB blocks in
     // ring slot kk % kWlRing, copied by LDS-DMA kWlPF k-blocks ahead together
     // with the weights (every wave copies D blocks per step; a wave with fewer
@@ -283,18 +287,22 @@ __global__ __launch_bounds__(256) void k_wl_act(WlAct a) {
         const float* P = a.part + ((int64_t)g * a.KS * a.M + m) * a.N + f0;
         const int64_t st = (int64_t)a.M * a.N;
         if (f0 + 8 <= a.N) {
+            // four splits' loads in flight at a time, added in split order
             int ks = 0;
-            for (; ks + 2 <= a.KS; ks += 2) {  // two splits' loads in flight, added in split order
-                const float4 x0 = *reinterpret_cast<const float4*>(P + ks * st);
-                const float4 x1 = *reinterpret_cast<const float4*>(P + ks * st + 4);
-                const float4 y0 = *reinterpret_cast<const float4*>(P + (ks + 1) * st);
-                const float4 y1 = *reinterpret_cast<const float4*>(P + (ks + 1) * st + 4);
-                v[0] += x0.x, v[1] += x0.y, v[2] += x0.z, v[3] += x0.w;
-                v[4] += x1.x, v[5] += x1.y, v[6] += x1.z, v[7] += x1.w;
-                v[0] += y0.x, v[1] += y0.y, v[2] += y0.z, v[3] += y0.w;
-                v[4] += y1.x, v[5] += y1.y, v[6] += y1.z, v[7] += y1.w;
+            for (; ks + 4 <= a.KS; ks += 4) {
+                float4 u[4][2];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    u[r][0] = *reinterpret_cast<const float4*>(P + (ks + r) * st);
+                    u[r][1] = *reinterpret_cast<const float4*>(P + (ks + r) * st + 4);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[0] += u[r][0].x, v[1] += u[r][0].y, v[2] += u[r][0].z, v[3] += u[r][0].w;
+                    v[4] += u[r][1].x, v[5] += u[r][1].y, v[6] += u[r][1].z, v[7] += u[r][1].w;
+                }
             }
-            if (ks < a.KS) {
+            for (; ks < a.KS; ++ks) {
                 const float4 x0 = *reinterpret_cast<const float4*>(P + ks * st);
                 const float4 x1 = *reinterpret_cast<const float4*>(P + ks * st + 4);
                 v[0] += x0.x, v[1] += x0.y, v[2] += x0.z, v[3] += x0.w;
@@ -367,7 +375,21 @@ __global__ __launch_bounds__(kRowThreads) void k_wl_rows(WlRows a) {
             float* orow = a.out + (int64_t)m * a.ldo;
             for (int c = tid; c < a.h; c += kRowThreads) {
                 float s = 0.0f, t = 0.0f;
-                for (int ks = 0; ks < a.KS; ++ks) {
+                int ks = 0;
+                for (; ks + 4 <= a.KS; ks += 4) {  // four splits' loads in flight, added in order
+                    float us4[4], ut4[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        us4[r] = Ps[(ks + r) * st + c];
+                        ut4[r] = Pt[(ks + r) * st + c];
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        s += us4[r];
+                        t += ut4[r];
+                    }
+                }
+                for (; ks < a.KS; ++ks) {
                     s += Ps[ks * st + c];
                     t += Pt[ks * st + c];
                 }
@@ -437,35 +459,34 @@ struct WlPlan {
 };
 
 WlPlan wl_plan(int N, int KB, int MT) {
-    // one round of workgroups over the CUs (one 4-wave workgroup each), as few
-    // k splits (partial sums) as that allows: two output tiles per wave where
-    // that still gives >= 3/4 of a round, else one
+    // one round of workgroups over the CUs (one workgroup each), as few k
+    // splits (partial sums) as that allows
     WlPlan p{};
     const int NT = (N + 15) / 16;
-    for (int ntw = 2; ntw >= 1; --ntw) {
-        const int nblk = (NT + kWlWaves * ntw - 1) / (kWlWaves * ntw);
-        int ks = kWlTarget / (2 * nblk);
-        ks = ks < 1 ? 1 : (ks > KB ? KB : ks);
-        const int kc = (KB + ks - 1) / ks;
-        ks = (KB + kc - 1) / kc;
-        p = WlPlan{ntw, ks, kc, nblk, 0};
-        if (4 * 2 * nblk * ks >= 3 * kWlTarget) break;
-    }
+    const bool deep = MT <= 4;
+    p.NTW = deep ? 1 : 2;
+    const int nw = deep ? 8 : 4, pf = deep ? 16 : 8;
+    p.nblk = (NT + kWlTilesPerWG - 1) / kWlTilesPerWG;
+    int ks = kWlTarget / (2 * p.nblk);
+    ks = ks < 1 ? 1 : (ks > KB ? KB : ks);
+    p.KC = (KB + ks - 1) / ks;
+    p.KS = (KB + p.KC - 1) / p.KC;
     // (at least 84 KiB: one workgroup per CU, so the round spreads over every CU)
-    p.lds = (size_t)kWlRing * 2 * MT * 1024;
+    p.lds = (size_t)(pf + 1) * 2 * MT * 1024;
     p.lds = p.lds > (size_t)84 * 1024 ? p.lds : (size_t)84 * 1024;
+    (void)nw;
     return p;
 }
 
-template <int MT, int NTW>
+template <int MT, int NTW, int NW, int PF>
 int wl_gemm_launch(const WlGemm& a, const WlPlan& p, hipStream_t st) {
-    static bool attr = false;  // (every instance sets its dynamic-LDS size once)
+    static bool attr = false;  // (every instance sets its dynamic-LDS cap once)
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wl_gemm<MT, NTW>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wl_gemm<MT, NTW, NW, PF>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL((k_wl_gemm<MT, NTW>), dim3((unsigned)(2 * p.nblk * p.KS)), dim3(64 * kWlWaves), p.lds, st,
+    hipLaunchKernelGGL((k_wl_gemm<MT, NTW, NW, PF>), dim3((unsigned)(2 * p.nblk * p.KS)), dim3(64 * NW), p.lds, st,
                        a);
     return wl_status("nfk_wide_rnvp: GEMM launch");
 }
@@ -479,15 +500,17 @@ int wl_gemm(const float* const pk[2], const float* const xf[2], float* part, int
     a.xf[0] = xf[0], a.xf[1] = xf[1];
     a.part = part;
     a.N = N, a.NT = (N + 15) / 16, a.KB = KB, a.KS = p.KS, a.KC = p.KC, a.M = M, a.nblk = p.nblk;
-#define NFK_WL_CASE(mt)                                                                   \
-    case mt:                                                                              \
-        return p.NTW == 2 ? wl_gemm_launch<mt, 2>(a, p, st) : wl_gemm_launch<mt, 1>(a, p, st);
     switch (MT) {
-        NFK_WL_CASE(1) NFK_WL_CASE(2) NFK_WL_CASE(3) NFK_WL_CASE(4) NFK_WL_CASE(5) NFK_WL_CASE(6)
-        NFK_WL_CASE(7) NFK_WL_CASE(8)
+        case 1: return wl_gemm_launch<1, 1, 8, 16>(a, p, st);
+        case 2: return wl_gemm_launch<2, 1, 8, 16>(a, p, st);
+        case 3: return wl_gemm_launch<3, 1, 8, 16>(a, p, st);
+        case 4: return wl_gemm_launch<4, 1, 8, 16>(a, p, st);
+        case 5: return wl_gemm_launch<5, 2, 4, 8>(a, p, st);
+        case 6: return wl_gemm_launch<6, 2, 4, 8>(a, p, st);
+        case 7: return wl_gemm_launch<7, 2, 4, 8>(a, p, st);
+        case 8: return wl_gemm_launch<8, 2, 4, 8>(a, p, st);
         default: return nfk_set_error("nfk_wide_rnvp: bad row tile count");
     }
-#undef NFK_WL_CASE
 }
 
 int64_t frag_floats(int MT, int K) { return (int64_t)MT * ((K + 31) / 32) * 512; }

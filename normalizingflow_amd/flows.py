@@ -434,7 +434,7 @@ class RealNVP(_HipFlow):
         return pack
 
     def _wide_pack(self, device, batch):
-        """(packs, biases) of nfk_wide_rnvp -- the layer as a weight stream
+        """The K_.WideRnvpPack of nfk_wide_rnvp -- the layer as a weight stream
         (Polymer_rnvp.yaml's RealNVP(2048, hidden 4000) at its 40-row batches):
         every Linear of the four conditioners packed once (nfk_wlin_pack),
         rebuilt when any parameter changes; None when it does not apply (non-stock
@@ -461,8 +461,9 @@ class RealNVP(_HipFlow):
             return c[1]
         packs = [K_.wlin_pack(n.network[i].weight) for n, i in order]
         biases = [n.network[i].bias.detach().contiguous() for n, i in order]
-        self.__dict__["_wide_cache"] = (key, (packs, biases, hidden))
-        return packs, biases, hidden
+        wp = K_.WideRnvpPack(packs, biases, self.dim // 2, hidden)
+        self.__dict__["_wide_cache"] = (key, wp)
+        return wp
 
     def _chain_shape(self, device):
         """("rnvp", kernel half_dim, hidden, half_dim) when this layer runs as the
@@ -490,7 +491,7 @@ class RealNVP(_HipFlow):
         if wide is not None:
             z = torch.empty_like(x, memory_format=torch.contiguous_format)
             xc = x if x.stride(1) == 1 else x.contiguous()
-            K_.wide_rnvp(xc, wide[0], wide[1], h, wide[2], z, logdet=logdet, logdet_mode=mode, inverse=inverse)
+            K_.wide_rnvp(xc, wide, z, logdet=logdet, logdet_mode=mode, inverse=inverse)
             return z
         z = torch.empty_like(x, memory_format=torch.contiguous_format)
         lo, up = x[:, :h], x[:, h:]

@@ -769,30 +769,47 @@ def wide_rnvp_supported(half, hidden):
     return bool(_lib.load().nfk_wide_rnvp_supported(half, hidden))
 
 
-def wide_rnvp(x, packs, biases, half, hidden, z, *, logdet, logdet_mode, inverse=False):
+class WideRnvpPack:
+    """The twelve packed Linears and biases of one RealNVP layer for
+    wide_rnvp, with their host pointer tables (built once)."""
+
+    def __init__(self, packs, biases, half, hidden):
+        if len(packs) != 12 or len(biases) != 12:
+            raise ValueError("wide_rnvp: 12 packs and 12 biases")
+        for b in biases:
+            if b.dtype != F32 or not b.is_contiguous():
+                raise ValueError("wide_rnvp: biases must be contiguous float32")
+        self.packs, self.biases, self.half, self.hidden = packs, biases, half, hidden
+        self.device = _require_hip(*packs, *biases)
+        self._pk = (ctypes.c_void_p * 12)(*[t.data_ptr() for t in packs])
+        self._bs = (ctypes.c_void_p * 12)(*[t.data_ptr() for t in biases])
+        self.pk, self.bs = ctypes.addressof(self._pk), ctypes.addressof(self._bs)
+        self._ws = {}
+
+    def workspace_floats(self, batch):
+        n = self._ws.get(batch)
+        if n is None:
+            n = self._ws[batch] = int(_lib.load().nfk_wide_rnvp_workspace(self.half, self.hidden, batch))
+        return n
+
+
+def wide_rnvp(x, wp, z, *, logdet, logdet_mode, inverse=False):
     """One RealNVP layer through the weight stream (include/nfk.h
-    nfk_wide_rnvp).  packs / biases: 12 device tensors each, index
-    6 c + 2 l + g (half-coupling c: 0 = s1/t1, 1 = s2/t2; Linear l = network.0,
-    .2, .4; conditioner g: 0 = s, 1 = t)."""
-    dev = _require_hip(x, z, logdet, *packs, *biases)
+    nfk_wide_rnvp); ``wp`` a WideRnvpPack (packs / biases index 6 c + 2 l + g:
+    half-coupling c: 0 = s1/t1, 1 = s2/t2; Linear l = network.0, .2, .4;
+    conditioner g: 0 = s, 1 = t)."""
+    dev = _require_hip(x, z, logdet)
+    if dev != wp.device:
+        raise RuntimeError("wide_rnvp: x on %s, the pack on %s" % (dev, wp.device))
     B = x.shape[0]
     xp, ldx = _mat(x, "x")
     zp, ldz = _mat(z, "z")
-    if x.shape[1] != 2 * half or z.shape != x.shape:
-        raise ValueError("wide_rnvp: x and z must be [B, %d]" % (2 * half))
-    if len(packs) != 12 or len(biases) != 12:
-        raise ValueError("wide_rnvp: 12 packs and 12 biases")
-    for b in biases:
-        if b.dtype != F32 or not b.is_contiguous():
-            raise ValueError("wide_rnvp: biases must be contiguous float32")
-    lib = _lib.load()
-    nws = int(lib.nfk_wide_rnvp_workspace(half, hidden, B))
+    if x.shape[1] != 2 * wp.half or z.shape != x.shape:
+        raise ValueError("wide_rnvp: x and z must be [B, %d]" % (2 * wp.half))
+    nws = wp.workspace_floats(B)
     ws = torch.empty(max(nws, 4), dtype=F32, device=dev)
-    pk = (ctypes.c_void_p * 12)(*[t.data_ptr() for t in packs])
-    bs = (ctypes.c_void_p * 12)(*[t.data_ptr() for t in biases])
-    _timed("nfk_wide_rnvp", dev, "nfk_wide_rnvp", xp, ldx, ctypes.addressof(pk), ctypes.addressof(bs), half, hidden,
-           zp, ldz, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, ws.data_ptr(), nws,
-           _stream(dev))
+    _timed("nfk_wide_rnvp", dev, "nfk_wide_rnvp", xp, ldx, wp.pk, wp.bs, wp.half, wp.hidden, zp, ldz,
+           _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, ws.data_ptr(), nws, _stream(dev))
 
 
 # ---- NSF_AR inverse, column by column from the library (nfk_ar_seqinv.hip)

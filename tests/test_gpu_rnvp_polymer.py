@@ -120,8 +120,7 @@ def test_wide_rnvp_vs_library_path_and_oracle(dim, H, rows, inverse, hip_device)
         # accumulate mode on a preset log|det|
         ld0 = torch.linspace(-2.0, 2.0, rows, device=hip_device)
         z2 = torch.empty_like(xd)
-        p, b, hid = layer._wide_pack(xd.device, rows)
-        K_.wide_rnvp(xd, p, b, dim // 2, hid, z2, logdet=ld0, logdet_mode=2, inverse=inverse)
+        K_.wide_rnvp(xd, layer._wide_pack(xd.device, rows), z2, logdet=ld0, logdet_mode=2, inverse=inverse)
     close(z, ref[0], Z_RTOL, Z_ATOL)
     close(ld, ref[1], LD_RTOL, LD_ATOL)
     close(zl, ref[0], Z_RTOL, Z_ATOL)
@@ -140,10 +139,9 @@ def test_wide_rnvp_reproducible_and_in_place(hip_device):
         outs = [layer(x) for _ in range(3)]
         for z, ld in outs[1:]:
             assert torch.equal(z, outs[0][0]) and torch.equal(ld, outs[0][1])
-        p, b, hid = layer._wide_pack(x.device, 100)
         xi = x.clone()
         ld = torch.empty(100, device=hip_device)
-        K_.wide_rnvp(xi, p, b, 1024, hid, xi, logdet=ld, logdet_mode=1)
+        K_.wide_rnvp(xi, layer._wide_pack(x.device, 100), xi, logdet=ld, logdet_mode=1)
     assert torch.equal(xi, outs[0][0]) and torch.equal(ld, outs[0][1])
 
 

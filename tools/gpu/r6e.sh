@@ -13,3 +13,7 @@ timeout -k 10 300 python -u tools/prof_host_ar354_train.py > $O/host_ar354_train
 head -45 $O/host_ar354_train.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_train_ar354 -o run -- python3 tools/bench_train.py --workload ar354 --batch 40 --steps 10 --no-torch > $O/prof_train_ar354.log 2>&1 || { tail -5 $O/prof_train_ar354.log; exit 1; }
 echo done
+timeout -k 10 300 python -u tools/time_rnvp2048.py > $O/time_rnvp2048.json 2> $O/time_rnvp2048.err || { tail -5 $O/time_rnvp2048.err; exit 1; }
+head -12 $O/time_rnvp2048.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rnvp -o run -- python3 bench.py --workload rnvp2048 --no-cpu-baseline --steps 10 > $O/prof_rnvp.log 2>&1 || { tail -5 $O/prof_rnvp.log; exit 1; }
+echo done2
