@@ -220,6 +220,19 @@ py::object ar_watch(py::handle layer_params, py::handle layer_modules, py::handl
     return py::cast(w.release(), py::return_value_policy::take_ownership);
 }
 
+// a watch over given dicts (version tags) and tensors (storage, offset,
+// version): e.g. a RealNVP layer's module tree and its 24 Linear tensors
+// (flows.RealNVP._wide_pack); None without dict version tags
+py::object make_watch(py::list dicts, py::list tensors) {
+    if (!NFK_DICT_TAGS) return py::none();
+    auto w = std::make_unique<ArWatch>();
+    for (py::handle d : dicts)
+        if (!w->add_dict(d.ptr())) throw py::type_error("make_watch: not a dict");
+    for (py::handle t : tensors)
+        if (!w->add_tensor(t.ptr())) throw py::type_error("make_watch: not a tensor");
+    return py::cast(w.release(), py::return_value_policy::take_ownership);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_nfk_host, m) {
@@ -227,4 +240,5 @@ PYBIND11_MODULE(_nfk_host, m) {
     m.def("ar_state", &ar_state);
     py::class_<ArWatch>(m, "ArWatch").def("valid", &ArWatch::valid).def("__len__", &ArWatch::size);
     m.def("ar_watch", &ar_watch);
+    m.def("make_watch", &make_watch);
 }

@@ -151,3 +151,35 @@ def test_copies_and_pickles_drop_the_watch(hs):
         assert len(c._stock_linears()) == 3 * 5
         assert [n for n, _ in c._named_param_list()] == [n for n, _ in layer.named_parameters()]
     assert layer._pack_cache[4][1] is w and w.valid()
+
+
+def test_make_watch_tracks_realnvp_tree(hs):
+    """The generic watch RealNVP's weight-stream pack is cached on (module-tree
+    dicts + the 24 Linear tensors): valid until a module, parameter or value changes."""
+    torch.manual_seed(0)
+
+    def watch(layer):
+        nets = (layer.s1, layer.t1, layer.s2, layer.t2)
+        dicts, params = [layer.__dict__["_modules"]], []
+        for n in nets:
+            net = n.__dict__["_modules"]["network"]
+            dicts += [n.__dict__["_modules"], net.__dict__["_modules"]]
+            dicts += [net.__dict__["_modules"][str(i)].__dict__["_parameters"] for i in (0, 2, 4)]
+            params += [t for i in (0, 2, 4) for t in (net[i].weight, net[i].bias)]
+        return hs.make_watch(dicts, params)
+
+    for change in ("none", "inplace", "linear", "net", "param"):
+        layer = nff.RealNVP(16, hidden_dim=32)
+        w = watch(layer)
+        if change == "inplace":
+            with torch.no_grad():
+                layer.s2.network[2].weight.mul_(2.0)
+        elif change == "linear":
+            layer.t1.network[4] = nn.Linear(32, 8)
+        elif change == "net":
+            layer.s1 = nff.FCNN(8, 8, 32)
+        elif change == "param":
+            layer.t2.network[0].bias = nn.Parameter(torch.zeros(32))
+        assert w.valid() == (change == "none"), change
+    with pytest.raises(TypeError):
+        hs.make_watch([1], [])
