@@ -5,18 +5,22 @@
 //
 // The inverse is sequential: conditioner i reads the trig features of the
 // coordinates already inverted (x[:, :i], flows.py:201), so coordinate i waits
-// for i - 1.  Per coordinate, two launches driven from C++ (no host round trip
-// and no Python between them):
+// for i - 1.  ONE launch per coordinate, issued from C++ (no host round trip
+// and no Python between them), k_sq_step:
 //
-//   k_sq_l1   layer 1 of conditioner i, [M, 2i] x W1_i^T, the 2i features split
-//             into 64-feature chunks over workgroups (W1_i is up to 100 x 4,094
-//             at Polymer: 1.6 MB); fp32 partial sums per chunk
-//   k_sq_fin  one workgroup: the chunks summed in order + b1, tanh, layer 2,
-//             tanh, the output layer (95 logits per row), the spline's inverse
-//             (nfk_rqs_element_lean: the reference's 2B softmax / softplus,
-//             then RQS, utils.py:27-152), x[:, i], the row's log|det| summed in
-//             column order (flows.py:208), the status word of column i, and
-//             cos / sin (pi x_i / B) for the later conditioners (flows.py:172-173)
+//   workgroups 0 .. M-1     finish conditioner i, one row each: its layer-1
+//                           chunks summed in order, plus the products of x_(i-1)'s
+//                           two features, + b1, tanh, layer 2, tanh, the output
+//                           layer (95 logits), the spline's inverse
+//                           (nfk_rqs_element_lean: the reference's 2B softmax /
+//                           softplus, then RQS, utils.py:27-152), x[m, i], the
+//                           row's log|det| in column order (flows.py:208), the
+//                           status word of column i, cos / sin (pi x_i / B)
+//   workgroups M ..         layer 1 of conditioner i + 1 over its features in
+//                           128-feature chunks, all but x_i's two (which the
+//                           first group is computing): [M, 128] x [128, H]
+//                           register tiles, fp32 partial sums (double-buffered
+//                           by conditioner parity)
 //
 // The conditioners' nn.Linear weights are read in place (fp32, a device table
 // of their pointers: the fused pack's table), and the arithmetic is fp32 FMA
@@ -37,10 +41,10 @@ NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, d
 
 namespace {
 
-constexpr int kSqFC = 128;       // layer-1 features per k_sq_l1 workgroup
+constexpr int kSqFC = 128;       // layer-1 features per chunk workgroup
 constexpr int kSqThreads = 256;  // both kernels
 constexpr int kSqMaxRows = 64;   // rows per pass
-constexpr int kSqMaxH = 128;     // hidden width (k_sq_l1's 4 x 4 register tiles: 64 rows x 128)
+constexpr int kSqMaxH = 128;     // hidden width (the chunks' 4 x 4 register tiles: 64 rows x 128)
 
 struct SqArgs {
     const float* const* w;  // [6 (dim - 1)]: conditioner i = 1 .. dim-1: W1 [H, 2i], b1, W2 [H, H], b2, W3 [P, H], b3
@@ -50,7 +54,7 @@ struct SqArgs {
     float* x;               // ... of the output
     int64_t ldx;
     float* feat;            // [2][M][dim]: cos, sin (pi x / B) of the inverted coordinates
-    float* part;            // [M][chunks][H] layer-1 partial sums
+    float* part;            // [2][M][chunks][H] layer-1 partial sums (by conditioner parity)
     float* ldacc;           // [M] the rows' log|det| so far (column order)
     float* logdet;          // [M] (this pass's rows) or null
     int32_t* status;        // [dim] or null
@@ -59,28 +63,46 @@ struct SqArgs {
     NfkSplineConst c;
 };
 
-// layer 1 of conditioner i over features f0 .. f0 + 127 (workgroup = chunk):
-// the chunk's weights and the rows' features through LDS ([f][h], [f][m]),
-// each thread a 4-row x 4-unit register tile
-__global__ __launch_bounds__(kSqThreads) void k_sq_l1(SqArgs a, int i) {
-    __shared__ float ws[kSqFC][kSqMaxH];
-    __shared__ float fs[kSqFC][kSqMaxRows];
-    const int F = 2 * i, f0 = blockIdx.x * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
+// LDS of a k_sq_step workgroup: the finish part's (the row's layer-1 chunks,
+// h1, h2, logits, one weight matrix at a time) or the layer-1 part's
+// (128 features x 128 units of weights, 128 features x 64 rows), the larger
+inline size_t sq_fin_floats(int nch, int H, int K) {
+    const int P = 3 * K - 1;
+    const int wmax = H * H > P * H ? H * H : P * H;
+    return (size_t)nch * H + 2 * H + P + 1 + wmax;
+}
+inline size_t sq_lds(int nch, int H, int K) {
+    const size_t l1 = (size_t)kSqFC * (kSqMaxH + kSqMaxRows);
+    const size_t f = sq_fin_floats(nch, H, K);
+    return (f > l1 ? f : l1) * sizeof(float);
+}
+
+// layer 1 of conditioner j over features f0 .. f0 + 127 (chunk c), WITHOUT the
+// two features of coordinate j - 1 (cos at f = j - 1, sin at f = 2j - 1: the
+// finish of column j - 1 runs in the same launch and writes them; the finish of
+// conditioner j adds their products itself).  The chunk's weights and the rows'
+// features through LDS ([f][h], [f][m]); each thread a 4-row x 4-unit tile
+__device__ void sq_l1_chunk(const SqArgs& a, int j, int c, float* lds) {
+    float(*ws)[kSqMaxH] = reinterpret_cast<float(*)[kSqMaxH]>(lds);
+    float(*fs)[kSqMaxRows] = reinterpret_cast<float(*)[kSqMaxRows]>(lds + kSqFC * kSqMaxH);
+    const int F = 2 * j, f0 = c * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
     const int H = a.H, M = a.M;
-    const float* W1 = a.w[6 * (i - 1)];
+    const float* W1 = a.w[6 * (j - 1)];
     for (int e = threadIdx.x; e < H * kSqFC; e += kSqThreads) {
         const int h = e / kSqFC, f = e - h * kSqFC;  // (consecutive threads: one weight row)
         ws[f][h] = f < nf ? W1[(int64_t)h * F + f0 + f] : 0.0f;
     }
-    // feature f of conditioner i: cos(pi x_f / B) for f < i, sin(pi x_(f-i) / B)
+    // feature f of conditioner j: cos(pi x_f / B) for f < j, sin(pi x_(f-j) / B)
     // above (trig_transform's cat, flows.py:172-173)
     for (int e = threadIdx.x; e < M * kSqFC; e += kSqThreads) {
         const int m = e / kSqFC, f = e - m * kSqFC, g = f0 + f;
         float v = 0.0f;
-        if (f < nf) v = g < i ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)M + m) * a.dim + (g - i)];
+        if (f < nf && g != j - 1 && g != 2 * j - 1)
+            v = g < j ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)M + m) * a.dim + (g - j)];
         fs[f][m] = v;
     }
     __syncthreads();
+    float* part = a.part + (int64_t)(j & 1) * M * a.nchmax * H;
     const int HT = (H + 3) / 4, MT4 = (M + 3) / 4;
     for (int t = threadIdx.x; t < HT * MT4; t += kSqThreads) {
         const int h0 = 4 * (t % HT), m0 = 4 * (t / HT);
@@ -104,28 +126,19 @@ __global__ __launch_bounds__(kSqThreads) void k_sq_l1(SqArgs a, int i) {
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (m0 + r < M && h0 + u < H)
-                    a.part[((int64_t)(m0 + r) * a.nchmax + blockIdx.x) * H + h0 + u] = acc[r][u];
+                if (m0 + r < M && h0 + u < H) part[((int64_t)(m0 + r) * a.nchmax + c) * H + h0 + u] = acc[r][u];
     }
 }
 
-// dynamic LDS of k_sq_fin: the row's partials [nch][H], h1 [H], h2 [H],
-// logits [P], and one weight matrix at a time (W2 [H][H], then W3 [P][H])
-inline size_t sq_fin_lds(int nch, int H, int K) {
-    const int P = 3 * K - 1;
-    const int wmax = H * H > P * H ? H * H : P * H;
-    return (size_t)(nch * H + 2 * H + P + 1 + wmax) * sizeof(float);
-}
-
-// the rest of conditioner i for ONE row (workgroup = row): the layer-1 chunks
-// summed in order + b1, tanh, layer 2, tanh, the output layer, the spline's
-// inverse, x[m, i], the row's log|det|, the status word, cos / sin of x[m, i]
+// the rest of conditioner i for ONE row m: its layer-1 chunks summed in order,
+// + the products of coordinate i - 1's two features (left out of the chunks),
+// + b1, tanh, layer 2, tanh, the output layer, the spline's inverse, x[m, i],
+// the row's log|det|, the status word, cos / sin of x[m, i]
 template <int K>
-__global__ __launch_bounds__(kSqThreads) void k_sq_fin(SqArgs a, int i, int nch) {
+__device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
     constexpr int P = 3 * K - 1;
-    extern __shared__ float sq_lds[];
-    const int H = a.H, m = blockIdx.x, tid = threadIdx.x;
-    float* pr = sq_lds;        // [nch][H]
+    const int H = a.H, tid = threadIdx.x;
+    float* pr = lds;           // [nch][H]
     float* h1 = pr + nch * H;  // [H]
     float* h2 = h1 + H;        // [H]
     float* lg = h2 + H;        // [P]
@@ -135,15 +148,19 @@ __global__ __launch_bounds__(kSqThreads) void k_sq_fin(SqArgs a, int i, int nch)
         for (int p = tid; p < P; p += kSqThreads) lg[p] = a.init[p];
     } else {
         const float* const* w = a.w + 6 * (i - 1);
-        const float *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
+        const float *W1 = w[0], *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
         // the row's partials (contiguous) and W2, loads in flight together
-        const float* src = a.part + (int64_t)m * a.nchmax * H;
+        const float* src = a.part + ((int64_t)(i & 1) * a.M + m) * a.nchmax * H;
         for (int e = tid; e < nch * H; e += kSqThreads) pr[e] = src[e];
         for (int e = tid; e < H * H; e += kSqThreads) wl[e] = W2[e];
+        const float cp = a.feat[(int64_t)m * a.dim + i - 1], sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
         __syncthreads();
         for (int h = tid; h < H; h += kSqThreads) {
             float s = 0.0f;
             for (int c = 0; c < nch; ++c) s += pr[c * H + h];
+            const float* wr = W1 + (int64_t)h * 2 * i;
+            s = __builtin_fmaf(cp, wr[i - 1], s);
+            s = __builtin_fmaf(sp, wr[2 * i - 1], s);
             h1[h] = tanhf(s + b1[h]);
         }
         __syncthreads();
@@ -192,6 +209,19 @@ __global__ __launch_bounds__(kSqThreads) void k_sq_fin(SqArgs a, int i, int nch)
     }
 }
 
+// one launch per column i: workgroups 0 .. M-1 finish conditioner i (one row
+// each); workgroups M .. M + nch_next - 1 run the layer-1 chunks of conditioner
+// i + 1 that do not need x_i (double-buffered partial sums by parity)
+template <int K>
+__global__ __launch_bounds__(kSqThreads) void k_sq_step(SqArgs a, int i, int nch, int nch_next) {
+    extern __shared__ float sq_smem[];
+    const int b = blockIdx.x;
+    if (b < a.M)
+        sq_finish<K>(a, i, nch, b, sq_smem);
+    else
+        sq_l1_chunk(a, i + 1, b - a.M, sq_smem);
+}
+
 int sq_status() {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -207,15 +237,15 @@ int sq_chunks(int dim) { return (int)((2LL * (dim - 1) + kSqFC - 1) / kSqFC); }
 
 extern "C" int nfk_ar_seqinv_supported(int32_t dim, int32_t hidden, int32_t K) {
     const bool k_ok = K == 4 || K == 8 || K == 10 || K == 16 || K == 32;
-    // (k_sq_fin's LDS: the row's layer-1 chunks, the activations, one weight matrix)
-    const bool lds_ok = dim >= 2 && sq_fin_lds(sq_chunks(dim), hidden, K) <= (size_t)160 * 1024;
+    // (k_sq_step's LDS: the row's layer-1 chunks, the activations, one weight matrix)
+    const bool lds_ok = dim >= 2 && sq_lds(sq_chunks(dim), hidden, K) <= (size_t)160 * 1024;
     return (dim >= 2 && dim <= 65536 && hidden >= 1 && hidden <= kSqMaxH && k_ok && lds_ok) ? 1 : 0;
 }
 
 extern "C" int64_t nfk_ar_seqinv_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch) {
     if (!nfk_ar_seqinv_supported(dim, hidden, K) || batch <= 0) return 0;
     const int64_t M = batch < kSqMaxRows ? batch : kSqMaxRows;
-    return 2 * M * dim + (int64_t)sq_chunks(dim) * M * hidden + M;
+    return 2 * M * dim + 2LL * sq_chunks(dim) * M * hidden + M;
 }
 
 extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* weights, const float* init_param,
@@ -242,7 +272,7 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         a.ldx = ldx;
         a.feat = workspace;
         a.part = workspace + 2LL * M * dim;
-        a.ldacc = a.part + (int64_t)sq_chunks(dim) * M * hidden;
+        a.ldacc = a.part + 2LL * sq_chunks(dim) * M * hidden;
         a.nchmax = sq_chunks(dim);
         a.logdet = logdet_mode != 0 ? logdet + r0 : nullptr;
         a.status = status;
@@ -256,24 +286,23 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
         static bool attr = false;
         if (!attr) {
-#define NFK_SQ_ATTR(k)                                                                                        \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sq_fin<k>), hipFuncAttributeMaxDynamicSharedMemorySize, \
+#define NFK_SQ_ATTR(k)                                                                                         \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sq_step<k>), hipFuncAttributeMaxDynamicSharedMemorySize, \
                               160 * 1024);
             NFK_SQ_ATTR(4) NFK_SQ_ATTR(8) NFK_SQ_ATTR(10) NFK_SQ_ATTR(16) NFK_SQ_ATTR(32)
 #undef NFK_SQ_ATTR
             attr = true;
         }
+        // column 0's launch also runs conditioner 1's chunks (none: its two
+        // features are x_0's); column i's, conditioner i + 1's
         for (int i = 0; i < dim; ++i) {
             const int nch = (2 * i + kSqFC - 1) / kSqFC;
-            if (i > 0) {
-                hipLaunchKernelGGL(k_sq_l1, dim3((unsigned)nch), dim3(kSqThreads), 0, st, a, i);
-                if (int e = sq_status()) return e;
-            }
-            const size_t lds = sq_fin_lds(nch, hidden, K);
-#define NFK_SQ_FIN(k) \
-    if (K == k) hipLaunchKernelGGL(k_sq_fin<k>, dim3((unsigned)M), dim3(kSqThreads), lds, st, a, i, nch);
-            NFK_SQ_FIN(4) NFK_SQ_FIN(8) NFK_SQ_FIN(10) NFK_SQ_FIN(16) NFK_SQ_FIN(32)
-#undef NFK_SQ_FIN
+            const int nxt = i + 1 < dim ? (2 * (i + 1) + kSqFC - 1) / kSqFC : 0;
+            const size_t lds = sq_lds(nch, hidden, K);
+#define NFK_SQ_STEP(k) \
+    if (K == k) hipLaunchKernelGGL(k_sq_step<k>, dim3((unsigned)(M + nxt)), dim3(kSqThreads), lds, st, a, i, nch, nxt);
+            NFK_SQ_STEP(4) NFK_SQ_STEP(8) NFK_SQ_STEP(10) NFK_SQ_STEP(16) NFK_SQ_STEP(32)
+#undef NFK_SQ_STEP
             if (int e = sq_status()) return e;
         }
     }
