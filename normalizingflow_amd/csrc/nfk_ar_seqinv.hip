@@ -77,6 +77,26 @@ inline size_t sq_lds(int nch, int H, int K) {
     return (f > l1 ? f : l1) * sizeof(float);
 }
 
+// LDS <- global with U loads in flight per thread (one load, one wait, one
+// store per element made every staging loop a chain of HBM round trips:
+// 38.8 us per column at Polymer's shape)
+template <int U>
+__device__ __forceinline__ void sq_stage(float* __restrict__ dst, const float* __restrict__ src, int n) {
+    for (int b = threadIdx.x; b < n; b += kSqThreads * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * kSqThreads;
+            v[u] = e < n ? src[e] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * kSqThreads;
+            if (e < n) dst[e] = v[u];
+        }
+    }
+}
+
 // layer 1 of conditioner j over features f0 .. f0 + 127 (chunk c), WITHOUT the
 // two features of coordinate j - 1 (cos at f = j - 1, sin at f = 2j - 1: the
 // finish of column j - 1 runs in the same launch and writes them; the finish of
@@ -88,18 +108,36 @@ __device__ void sq_l1_chunk(const SqArgs& a, int j, int c, float* lds) {
     const int F = 2 * j, f0 = c * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
     const int H = a.H, M = a.M;
     const float* W1 = a.w[6 * (j - 1)];
-    for (int e = threadIdx.x; e < H * kSqFC; e += kSqThreads) {
-        const int h = e / kSqFC, f = e - h * kSqFC;  // (consecutive threads: one weight row)
-        ws[f][h] = f < nf ? W1[(int64_t)h * F + f0 + f] : 0.0f;
+    // (16 loads in flight per thread; consecutive threads: one weight row)
+    for (int b = threadIdx.x; b < H * kSqFC; b += kSqThreads * 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = b + u * kSqThreads, h = e / kSqFC, f = e - h * kSqFC;
+            v[u] = (e < H * kSqFC && f < nf) ? W1[(int64_t)h * F + f0 + f] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = b + u * kSqThreads, h = e / kSqFC, f = e - h * kSqFC;
+            if (e < H * kSqFC) ws[f][h] = v[u];
+        }
     }
     // feature f of conditioner j: cos(pi x_f / B) for f < j, sin(pi x_(f-j) / B)
     // above (trig_transform's cat, flows.py:172-173)
-    for (int e = threadIdx.x; e < M * kSqFC; e += kSqThreads) {
-        const int m = e / kSqFC, f = e - m * kSqFC, g = f0 + f;
-        float v = 0.0f;
-        if (f < nf && g != j - 1 && g != 2 * j - 1)
-            v = g < j ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)M + m) * a.dim + (g - j)];
-        fs[f][m] = v;
+    for (int b = threadIdx.x; b < M * kSqFC; b += kSqThreads * 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = b + u * kSqThreads, m = e / kSqFC, f = e - m * kSqFC, g = f0 + f;
+            v[u] = 0.0f;
+            if (e < M * kSqFC && f < nf && g != j - 1 && g != 2 * j - 1)
+                v[u] = g < j ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)M + m) * a.dim + (g - j)];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = b + u * kSqThreads, m = e / kSqFC, f = e - m * kSqFC;
+            if (e < M * kSqFC) fs[f][m] = v[u];
+        }
     }
     __syncthreads();
     float* part = a.part + (int64_t)(j & 1) * M * a.nchmax * H;
@@ -151,8 +189,8 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
         const float *W1 = w[0], *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
         // the row's partials (contiguous) and W2, loads in flight together
         const float* src = a.part + ((int64_t)(i & 1) * a.M + m) * a.nchmax * H;
-        for (int e = tid; e < nch * H; e += kSqThreads) pr[e] = src[e];
-        for (int e = tid; e < H * H; e += kSqThreads) wl[e] = W2[e];
+        sq_stage<16>(pr, src, nch * H);
+        sq_stage<16>(wl, W2, H * H);
         const float cp = a.feat[(int64_t)m * a.dim + i - 1], sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
         __syncthreads();
         for (int h = tid; h < H; h += kSqThreads) {
@@ -171,7 +209,7 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
             h2[h] = tanhf(s + b2[h]);
         }
         __syncthreads();
-        for (int e = tid; e < P * H; e += kSqThreads) wl[e] = W3[e];
+        sq_stage<16>(wl, W3, P * H);
         __syncthreads();
         for (int p = tid; p < P; p += kSqThreads) {
             const float* wr = wl + p * H;

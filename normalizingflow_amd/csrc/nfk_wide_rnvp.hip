@@ -36,6 +36,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/nfk.h"
 
@@ -47,10 +48,8 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // GEMM workgroup shapes (waves NW, output tiles per wave NTW, k-blocks of
-// weights in flight per wave PF; 8 output tiles per workgroup either way):
-// up to 64 rows, 8 waves (two per SIMD) of one tile 16 k-blocks ahead -- twice
-// the bytes in flight of 4 waves x 2 tiles x 8; above, 4 x 2 x 8 (the input
-// ring of 16 + 1 slots would not fit the LDS)
+// weights in flight per wave PF; 8 output tiles per workgroup either way): see
+// wl_cfg
 constexpr int kWlTilesPerWG = 8;
 constexpr int kWlMaxMT = 8;                    // sample tiles per pass: 128 rows
 constexpr int kWlHdr = 64;                     // pack header floats ([0] = 2^-s)
@@ -458,14 +457,26 @@ struct WlPlan {
     size_t lds;
 };
 
+// GEMM workgroup shape: 0 = 4 waves x 2 tiles x 8 k-blocks in flight (the
+// default: 11 / 28 / 12 us for Polymer_rnvp's three stages at 40 rows,
+// profiles/r6/), 1 = 8 waves x 1 tile x 16 (16 / 30 / 16 us: slower),
+// 2 = 4 x 2 x 10; NFK_WL_CFG selects one for A/B runs (1 and 2 up to 64 rows)
+int wl_cfg(int MT) {
+    static const int env = [] {
+        const char* e = std::getenv("NFK_WL_CFG");
+        return e != nullptr ? std::atoi(e) : 0;
+    }();
+    return MT <= 4 ? env : 0;
+}
+
 WlPlan wl_plan(int N, int KB, int MT) {
     // one round of workgroups over the CUs (one workgroup each), as few k
     // splits (partial sums) as that allows
     WlPlan p{};
     const int NT = (N + 15) / 16;
-    const bool deep = MT <= 4;
-    p.NTW = deep ? 1 : 2;
-    const int nw = deep ? 8 : 4, pf = deep ? 16 : 8;
+    const int cfg = wl_cfg(MT);
+    p.NTW = cfg == 1 ? 1 : 2;
+    const int pf = cfg == 1 ? 16 : (cfg == 2 ? 10 : 8);
     p.nblk = (NT + kWlTilesPerWG - 1) / kWlTilesPerWG;
     int ks = kWlTarget / (2 * p.nblk);
     ks = ks < 1 ? 1 : (ks > KB ? KB : ks);
@@ -474,7 +485,6 @@ WlPlan wl_plan(int N, int KB, int MT) {
     // (at least 84 KiB: one workgroup per CU, so the round spreads over every CU)
     p.lds = (size_t)(pf + 1) * 2 * MT * 1024;
     p.lds = p.lds > (size_t)84 * 1024 ? p.lds : (size_t)84 * 1024;
-    (void)nw;
     return p;
 }
 
@@ -500,11 +510,15 @@ int wl_gemm(const float* const pk[2], const float* const xf[2], float* part, int
     a.xf[0] = xf[0], a.xf[1] = xf[1];
     a.part = part;
     a.N = N, a.NT = (N + 15) / 16, a.KB = KB, a.KS = p.KS, a.KC = p.KC, a.M = M, a.nblk = p.nblk;
+    const int cfg = wl_cfg(MT);
+#define NFK_WL_SMALL(mt)                                                      \
+    case mt:                                                                  \
+        if (cfg == 1) return wl_gemm_launch<mt, 1, 8, 16>(a, p, st);          \
+        if (cfg == 2) return wl_gemm_launch<mt, 2, 4, 10>(a, p, st);          \
+        return wl_gemm_launch<mt, 2, 4, 8>(a, p, st);
     switch (MT) {
-        case 1: return wl_gemm_launch<1, 1, 8, 16>(a, p, st);
-        case 2: return wl_gemm_launch<2, 1, 8, 16>(a, p, st);
-        case 3: return wl_gemm_launch<3, 1, 8, 16>(a, p, st);
-        case 4: return wl_gemm_launch<4, 1, 8, 16>(a, p, st);
+        NFK_WL_SMALL(1) NFK_WL_SMALL(2) NFK_WL_SMALL(3) NFK_WL_SMALL(4)
+#undef NFK_WL_SMALL
         case 5: return wl_gemm_launch<5, 2, 4, 8>(a, p, st);
         case 6: return wl_gemm_launch<6, 2, 4, 8>(a, p, st);
         case 7: return wl_gemm_launch<7, 2, 4, 8>(a, p, st);
