@@ -41,7 +41,7 @@ NfkSplineConst nfk_make_const(int K, double left, double right, double bottom, d
 
 namespace {
 
-constexpr int kSqFC = 128;       // layer-1 features per chunk workgroup
+constexpr int kSqFC = 64;        // layer-1 features per chunk workgroup
 constexpr int kSqThreads = 256;  // both kernels
 constexpr int kSqMaxRows = 64;   // rows per pass
 constexpr int kSqMaxH = 128;     // hidden width (the chunks' 4 x 4 register tiles: 64 rows x 128)
@@ -68,8 +68,8 @@ struct SqArgs {
 // (128 features x 128 units of weights, 128 features x 64 rows), the larger
 inline size_t sq_fin_floats(int nch, int H, int K) {
     const int P = 3 * K - 1;
-    const int wmax = H * H > P * H ? H * H : P * H;
-    return (size_t)nch * H + 2 * H + P + 1 + wmax;
+    auto al = [](int64_t v) { return (v + 3) & ~3LL; };
+    return (size_t)(al((int64_t)nch * H) + 2 * al(H) + al(P) + al((int64_t)H * H) + al((int64_t)P * H));
 }
 inline size_t sq_lds(int nch, int H, int K) {
     const size_t l1 = (size_t)kSqFC * (kSqMaxH + kSqMaxRows);
@@ -97,6 +97,31 @@ __device__ __forceinline__ void sq_stage(float* __restrict__ dst, const float* _
     }
 }
 
+// the same with 16-byte loads where both ends are 16-byte aligned and n % 4 == 0
+template <int U>
+__device__ __forceinline__ void sq_stage4(float* __restrict__ dst, const float* __restrict__ src, int n) {
+    if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) != 0 || (n & 3) != 0) {
+        sq_stage<U>(dst, src, n);
+        return;
+    }
+    const int n4 = n >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int b = threadIdx.x; b < n4; b += kSqThreads * U) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * kSqThreads;
+            if (e < n4) v[u] = s4[e];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * kSqThreads;
+            if (e < n4) d4[e] = v[u];
+        }
+    }
+}
+
 // layer 1 of conditioner j over features f0 .. f0 + 127 (chunk c), WITHOUT the
 // two features of coordinate j - 1 (cos at f = j - 1, sin at f = 2j - 1: the
 // finish of column j - 1 runs in the same launch and writes them; the finish of
@@ -108,18 +133,24 @@ __device__ void sq_l1_chunk(const SqArgs& a, int j, int c, float* lds) {
     const int F = 2 * j, f0 = c * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
     const int H = a.H, M = a.M;
     const float* W1 = a.w[6 * (j - 1)];
-    // (16 loads in flight per thread; consecutive threads: one weight row)
-    for (int b = threadIdx.x; b < H * kSqFC; b += kSqThreads * 16) {
-        float v[16];
+    // (feature pairs: F = 2j is even, so every row segment is 8-byte aligned;
+    // 16 loads in flight per thread, consecutive threads along one weight row)
+    constexpr int FC2 = kSqFC / 2;
+    const float2* W1p = reinterpret_cast<const float2*>(W1);
+    for (int b = threadIdx.x; b < H * FC2; b += kSqThreads * 16) {
+        float2 v[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            const int e = b + u * kSqThreads, h = e / kSqFC, f = e - h * kSqFC;
-            v[u] = (e < H * kSqFC && f < nf) ? W1[(int64_t)h * F + f0 + f] : 0.0f;
+            const int e = b + u * kSqThreads, h = e / FC2, f = 2 * (e - h * FC2);
+            v[u] = (e < H * FC2 && f < nf) ? W1p[((int64_t)h * F + f0 + f) >> 1] : make_float2(0.0f, 0.0f);
         }
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            const int e = b + u * kSqThreads, h = e / kSqFC, f = e - h * kSqFC;
-            if (e < H * kSqFC) ws[f][h] = v[u];
+            const int e = b + u * kSqThreads, h = e / FC2, f = 2 * (e - h * FC2);
+            if (e < H * FC2) {
+                ws[f][h] = v[u].x;
+                ws[f + 1][h] = v[u].y;
+            }
         }
     }
     // feature f of conditioner j: cos(pi x_f / B) for f < j, sin(pi x_(f-j) / B)
@@ -176,11 +207,14 @@ template <int K>
 __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
     constexpr int P = 3 * K - 1;
     const int H = a.H, tid = threadIdx.x;
-    float* pr = lds;           // [nch][H]
-    float* h1 = pr + nch * H;  // [H]
-    float* h2 = h1 + H;        // [H]
-    float* lg = h2 + H;        // [P]
-    float* wl = lg + P + 1;    // W2 or W3 (row-major, as nn.Linear)
+    // (16-byte aligned regions: the staged matrices are copied by float4)
+    const int HA = (H + 3) & ~3, PA = (P + 3) & ~3;
+    float* pr = lds;            // [nch][H]
+    float* h1 = pr + ((nch * H + 3) & ~3);  // [H]
+    float* h2 = h1 + HA;        // [H]
+    float* lg = h2 + HA;        // [P]
+    float* w2 = lg + PA;        // W2 [H][H] (row-major, as nn.Linear)
+    float* w3 = w2 + ((H * H + 3) & ~3);  // W3 [P][H]
     if (i == 0) {
         // coordinate 0: init_param, the same logits for every row (flows.py:196-199)
         for (int p = tid; p < P; p += kSqThreads) lg[p] = a.init[p];
@@ -188,9 +222,11 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
         const float* const* w = a.w + 6 * (i - 1);
         const float *W1 = w[0], *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
         // the row's partials (contiguous) and W2, loads in flight together
+        // the row's partials (contiguous), W2 and W3: every load in flight at once
         const float* src = a.part + ((int64_t)(i & 1) * a.M + m) * a.nchmax * H;
-        sq_stage<16>(pr, src, nch * H);
-        sq_stage<16>(wl, W2, H * H);
+        sq_stage4<8>(pr, src, nch * H);
+        sq_stage4<12>(w2, W2, H * H);
+        sq_stage4<12>(w3, W3, P * H);
         const float cp = a.feat[(int64_t)m * a.dim + i - 1], sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
         __syncthreads();
         for (int h = tid; h < H; h += kSqThreads) {
@@ -203,16 +239,14 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
         }
         __syncthreads();
         for (int h = tid; h < H; h += kSqThreads) {
-            const float* wr = wl + h * H;
+            const float* wr = w2 + h * H;
             float s = 0.0f;
             for (int k = 0; k < H; ++k) s = __builtin_fmaf(h1[k], wr[k], s);
             h2[h] = tanhf(s + b2[h]);
         }
         __syncthreads();
-        sq_stage<16>(wl, W3, P * H);
-        __syncthreads();
         for (int p = tid; p < P; p += kSqThreads) {
-            const float* wr = wl + p * H;
+            const float* wr = w3 + p * H;
             float s = 0.0f;
             for (int k = 0; k < H; ++k) s = __builtin_fmaf(h2[k], wr[k], s);
             lg[p] = s + b3[p];
