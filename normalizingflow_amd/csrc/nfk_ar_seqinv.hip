@@ -221,20 +221,80 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
     } else {
         const float* const* w = a.w + 6 * (i - 1);
         const float *W1 = w[0], *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
-        // the row's partials (contiguous) and W2, loads in flight together
-        // the row's partials (contiguous), W2 and W3: every load in flight at once
+        // ONE round trip for everything the row needs: its layer-1 partials
+        // (contiguous), W2, W3, and x_(i-1)'s two weight columns of W1 -- every
+        // load issued before any is waited for (a wait per region had made the
+        // finish three or four dependent HBM round trips)
         const float* src = a.part + ((int64_t)(i & 1) * a.M + m) * a.nchmax * H;
-        sq_stage4<8>(pr, src, nch * H);
-        sq_stage4<12>(w2, W2, H * H);
-        sq_stage4<12>(w3, W3, P * H);
-        const float cp = a.feat[(int64_t)m * a.dim + i - 1], sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
+        const int np = nch * H, n2 = H * H, n3 = P * H;
+        const bool v4 = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(W2) |
+                          reinterpret_cast<uintptr_t>(W3)) & 15) == 0 && (np & 3) == 0 && (n2 & 3) == 0 &&
+                        (n3 & 3) == 0;
+        constexpr int UP = 8, U2 = 12, U3 = 12;
+        float wa = 0.0f, wb = 0.0f, cp = 0.0f, sp = 0.0f;
+        if (tid < H) {
+            const float* wr = W1 + (int64_t)tid * 2 * i;
+            wa = wr[i - 1];
+            wb = wr[2 * i - 1];
+        }
+        cp = a.feat[(int64_t)m * a.dim + i - 1];
+        sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
+        if (v4) {
+            typedef float f4v __attribute__((ext_vector_type(4)));  // (HIP's float4 struct arrays went to scratch)
+            const f4v *sp4 = reinterpret_cast<const f4v*>(src), *s24 = reinterpret_cast<const f4v*>(W2),
+                      *s34 = reinterpret_cast<const f4v*>(W3);
+            f4v rp[UP], r2[U2], r3[U3];
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const int e = tid + u * kSqThreads;
+                rp[u] = e < np / 4 ? sp4[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int u = 0; u < U2; ++u) {
+                const int e = tid + u * kSqThreads;
+                r2[u] = e < n2 / 4 ? s24[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int u = 0; u < U3; ++u) {
+                const int e = tid + u * kSqThreads;
+                r3[u] = e < n3 / 4 ? s34[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const int e = tid + u * kSqThreads;
+                if (e < np / 4) reinterpret_cast<f4v*>(pr)[e] = rp[u];
+            }
+#pragma unroll
+            for (int u = 0; u < U2; ++u) {
+                const int e = tid + u * kSqThreads;
+                if (e < n2 / 4) reinterpret_cast<f4v*>(w2)[e] = r2[u];
+            }
+#pragma unroll
+            for (int u = 0; u < U3; ++u) {
+                const int e = tid + u * kSqThreads;
+                if (e < n3 / 4) reinterpret_cast<f4v*>(w3)[e] = r3[u];
+            }
+            // (larger shapes: the rest by the loop)
+            if (np / 4 > UP * kSqThreads) sq_stage<8>(pr + 4 * UP * kSqThreads, src + 4 * UP * kSqThreads, np - 4 * UP * kSqThreads);
+            if (n2 / 4 > U2 * kSqThreads) sq_stage<8>(w2 + 4 * U2 * kSqThreads, W2 + 4 * U2 * kSqThreads, n2 - 4 * U2 * kSqThreads);
+            if (n3 / 4 > U3 * kSqThreads) sq_stage<8>(w3 + 4 * U3 * kSqThreads, W3 + 4 * U3 * kSqThreads, n3 - 4 * U3 * kSqThreads);
+        } else {
+            sq_stage<16>(pr, src, np);
+            sq_stage<16>(w2, W2, n2);
+            sq_stage<16>(w3, W3, n3);
+        }
         __syncthreads();
         for (int h = tid; h < H; h += kSqThreads) {
             float s = 0.0f;
             for (int c = 0; c < nch; ++c) s += pr[c * H + h];
-            const float* wr = W1 + (int64_t)h * 2 * i;
-            s = __builtin_fmaf(cp, wr[i - 1], s);
-            s = __builtin_fmaf(sp, wr[2 * i - 1], s);
+            float w_a = wa, w_b = wb;
+            if (h != tid) {  // (H > the workgroup: the rest of the units)
+                const float* wr = W1 + (int64_t)h * 2 * i;
+                w_a = wr[i - 1];
+                w_b = wr[2 * i - 1];
+            }
+            s = __builtin_fmaf(cp, w_a, s);
+            s = __builtin_fmaf(sp, w_b, s);
             h1[h] = tanhf(s + b1[h]);
         }
         __syncthreads();
@@ -285,7 +345,7 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
 // each); workgroups M .. M + nch_next - 1 run the layer-1 chunks of conditioner
 // i + 1 that do not need x_i (double-buffered partial sums by parity)
 template <int K>
-__global__ __launch_bounds__(kSqThreads) void k_sq_step(SqArgs a, int i, int nch, int nch_next) {
+__global__ __launch_bounds__(kSqThreads, 1) void k_sq_step(SqArgs a, int i, int nch, int nch_next) {
     extern __shared__ float sq_smem[];
     const int b = blockIdx.x;
     if (b < a.M)
