@@ -516,9 +516,11 @@ int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const 
  * NSF_AR inverse for the layers the fused kernel's inverse does not take
  * (nfk_fused_ar_inverse_supported == 0: Polymer.yaml's 2,048 coordinates),
  * nfk_ar_seqinv.hip: NSF_AR.inverse (nf/flows.py:193-209) column by column,
- * two launches per coordinate issued from the library (conditioner i's layer 1
- * split over workgroups, then its layers 2-3, the spline's inverse and the
- * trig features of x_i in one workgroup), fp32 arithmetic, the weights read in
+ * one launch per coordinate issued from the library (per row, one workgroup
+ * finishes conditioner i: its layer-1 partial sums plus x_{i-1}'s two
+ * features, layers 2-3, the spline's inverse and the trig features of x_i;
+ * beside them, workgroups run conditioner i+1's layer 1 over the features
+ * already known, 64 at a time), fp32 arithmetic, the weights read in
  * place.  weights: a DEVICE table of 6 (dim - 1) pointers (W1, b1, W2, b2, W3,
  * b3 of conditioners 1 .. dim-1, fp32 contiguous nn.Linear tensors: the same
  * table nfk_fused_ar_pack reads); init_param [3K-1].  z -> x [batch, dim],

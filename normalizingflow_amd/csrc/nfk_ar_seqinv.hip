@@ -17,8 +17,8 @@
 //                           row's log|det| in column order (flows.py:208), the
 //                           status word of column i, cos / sin (pi x_i / B)
 //   workgroups M ..         layer 1 of conditioner i + 1 over its features in
-//                           128-feature chunks, all but x_i's two (which the
-//                           first group is computing): [M, 128] x [128, H]
+//                           64-feature chunks, all but x_i's two (which the
+//                           first group is computing): [M, 64] x [64, H]
 //                           register tiles, fp32 partial sums (double-buffered
 //                           by conditioner parity)
 //
@@ -61,15 +61,23 @@ struct SqArgs {
     int mode, dim, H, M, nchmax;
     float pi, bnd;
     NfkSplineConst c;
+    unsigned long long* tdbg;  // diagnostic phase clocks (nfk_debug_sq_timing), normally null
 };
+
+// diagnostic: thread 0 of row 0's finish and of the first chunk workgroup stamp
+// the shader clock at their phase boundaries, [dim][12] per pass
+__device__ __forceinline__ void sq_stamp(const SqArgs& a, int i, int slot) {
+    if (a.tdbg != nullptr && threadIdx.x == 0) a.tdbg[(int64_t)i * 12 + slot] = __builtin_readcyclecounter();
+}
 
 // LDS of a k_sq_step workgroup: the finish part's (the row's layer-1 chunks,
 // h1, h2, logits, one weight matrix at a time) or the layer-1 part's
-// (128 features x 128 units of weights, 128 features x 64 rows), the larger
+// (64 features x 128 units of weights, 64 features x 64 rows), the larger
 inline size_t sq_fin_floats(int nch, int H, int K) {
     const int P = 3 * K - 1;
     auto al = [](int64_t v) { return (v + 3) & ~3LL; };
-    return (size_t)(al((int64_t)nch * H) + 2 * al(H) + al(P) + al((int64_t)H * H) + al((int64_t)P * H));
+    const int S = H | 1;  // (the staged W2 / W3 rows' stride, sq_finish)
+    return (size_t)(al((int64_t)nch * H) + 2 * al(H) + al(P) + al((int64_t)H * S) + al((int64_t)P * S));
 }
 inline size_t sq_lds(int nch, int H, int K) {
     const size_t l1 = (size_t)kSqFC * (kSqMaxH + kSqMaxRows);
@@ -122,7 +130,57 @@ __device__ __forceinline__ void sq_stage4(float* __restrict__ dst, const float* 
     }
 }
 
-// layer 1 of conditioner j over features f0 .. f0 + 127 (chunk c), WITHOUT the
+typedef float sq_f4 __attribute__((ext_vector_type(4)));  // (HIP's float4 struct arrays went to scratch)
+
+// row r, column c of a row-major [., H] matrix from its flat index (a float
+// estimate, then corrected: exact for the staged sizes)
+__device__ __forceinline__ void sq_rc(int flat, int H, float invH, int& r, int& c) {
+    r = (int)((float)flat * invH);
+    c = flat - r * H;
+    if (c >= H) {
+        ++r;
+        c -= H;
+    } else if (c < 0) {
+        --r;
+        c += H;
+    }
+}
+
+// four consecutive elements (flat index flat0) of a row-major [., H] matrix
+// into LDS rows of stride S = H | 1: an odd stride, so the layer dots (lane h
+// reading row h) hit 64 different banks.  H >= 4: at most one row break.
+__device__ __forceinline__ void sq_put4(float* dst, int flat0, sq_f4 v, int H, int S, float invH) {
+    int r, c;
+    sq_rc(flat0, H, invH, r, c);
+    const int base = r * S + c, d = S - H;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[base + q + (c + q >= H ? d : 0)] = v[q];
+}
+
+// the same staging, element by element, for elements from .. n - 1
+template <int U>
+__device__ __forceinline__ void sq_stage_pad(float* __restrict__ dst, const float* __restrict__ src, int from, int n,
+                                             int H, int S, float invH) {
+    for (int b = from + threadIdx.x; b < n; b += kSqThreads * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * kSqThreads;
+            v[u] = e < n ? src[e] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * kSqThreads;
+            if (e < n) {
+                int r, c;
+                sq_rc(e, H, invH, r, c);
+                dst[r * S + c] = v[u];
+            }
+        }
+    }
+}
+
+// layer 1 of conditioner j over features f0 .. f0 + 63 (chunk c), WITHOUT the
 // two features of coordinate j - 1 (cos at f = j - 1, sin at f = 2j - 1: the
 // finish of column j - 1 runs in the same launch and writes them; the finish of
 // conditioner j adds their products itself).  The chunk's weights and the rows'
@@ -132,6 +190,7 @@ __device__ void sq_l1_chunk(const SqArgs& a, int j, int c, float* lds) {
     float(*fs)[kSqMaxRows] = reinterpret_cast<float(*)[kSqMaxRows]>(lds + kSqFC * kSqMaxH);
     const int F = 2 * j, f0 = c * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
     const int H = a.H, M = a.M;
+    if (c == 0) sq_stamp(a, j - 1, 8);
     const float* W1 = a.w[6 * (j - 1)];
     // (feature pairs: F = 2j is even, so every row segment is 8-byte aligned;
     // 16 loads in flight per thread, consecutive threads along one weight row)
@@ -171,6 +230,7 @@ __device__ void sq_l1_chunk(const SqArgs& a, int j, int c, float* lds) {
         }
     }
     __syncthreads();
+    if (c == 0) sq_stamp(a, j - 1, 9);
     float* part = a.part + (int64_t)(j & 1) * M * a.nchmax * H;
     const int HT = (H + 3) / 4, MT4 = (M + 3) / 4;
     for (int t = threadIdx.x; t < HT * MT4; t += kSqThreads) {
@@ -197,6 +257,7 @@ __device__ void sq_l1_chunk(const SqArgs& a, int j, int c, float* lds) {
             for (int u = 0; u < 4; ++u)
                 if (m0 + r < M && h0 + u < H) part[((int64_t)(m0 + r) * a.nchmax + c) * H + h0 + u] = acc[r][u];
     }
+    if (c == 0) sq_stamp(a, j - 1, 10);
 }
 
 // the rest of conditioner i for ONE row m: its layer-1 chunks summed in order,
@@ -213,14 +274,32 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
     float* h1 = pr + ((nch * H + 3) & ~3);  // [H]
     float* h2 = h1 + HA;        // [H]
     float* lg = h2 + HA;        // [P]
-    float* w2 = lg + PA;        // W2 [H][H] (row-major, as nn.Linear)
-    float* w3 = w2 + ((H * H + 3) & ~3);  // W3 [P][H]
+    float* w2 = lg + PA;        // W2 [H][H] (row-major, as nn.Linear; rows S apart)
+    const int S = H | 1;        // (odd row stride: sq_put4)
+    float* w3 = w2 + ((H * S + 3) & ~3);  // W3 [P][H]
+    // every operand a thread needs from memory is requested up front (a load
+    // issued after a barrier is one more dependent round trip on the column's
+    // critical path): the biases (H <= 128 and P <= 95 < the workgroup, so one
+    // unit / logit per thread), thread 0's z[m, i] and the row's log|det| so far
+    if (m == 0) sq_stamp(a, i, 0);
+    const float* const* wt = a.w + 6 * (i > 0 ? i - 1 : 0);
+    float bias1 = 0.0f, bias2 = 0.0f, bias3 = 0.0f, zv = 0.0f, ldprev = 0.0f;
+    if (i > 0) {
+        if (tid < H) {
+            bias1 = wt[1][tid];
+            bias2 = wt[3][tid];
+        }
+        if (tid < P) bias3 = wt[5][tid];
+    }
+    if (tid == 0) {
+        zv = a.z[(int64_t)m * a.ldz + i];
+        ldprev = i == 0 ? 0.0f : a.ldacc[m];
+    }
     if (i == 0) {
         // coordinate 0: init_param, the same logits for every row (flows.py:196-199)
         for (int p = tid; p < P; p += kSqThreads) lg[p] = a.init[p];
     } else {
-        const float* const* w = a.w + 6 * (i - 1);
-        const float *W1 = w[0], *b1 = w[1], *W2 = w[2], *b2 = w[3], *W3 = w[4], *b3 = w[5];
+        const float *W1 = wt[0], *W2 = wt[2], *W3 = wt[4];
         // ONE round trip for everything the row needs: its layer-1 partials
         // (contiguous), W2, W3, and x_(i-1)'s two weight columns of W1 -- every
         // load issued before any is waited for (a wait per region had made the
@@ -240,7 +319,8 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
         cp = a.feat[(int64_t)m * a.dim + i - 1];
         sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
         if (v4) {
-            typedef float f4v __attribute__((ext_vector_type(4)));  // (HIP's float4 struct arrays went to scratch)
+            typedef sq_f4 f4v;
+            const float invH = 1.0f / (float)H;
             const f4v *sp4 = reinterpret_cast<const f4v*>(src), *s24 = reinterpret_cast<const f4v*>(W2),
                       *s34 = reinterpret_cast<const f4v*>(W3);
             f4v rp[UP], r2[U2], r3[U3];
@@ -267,53 +347,52 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
 #pragma unroll
             for (int u = 0; u < U2; ++u) {
                 const int e = tid + u * kSqThreads;
-                if (e < n2 / 4) reinterpret_cast<f4v*>(w2)[e] = r2[u];
+                if (e < n2 / 4) sq_put4(w2, 4 * e, r2[u], H, S, invH);
             }
 #pragma unroll
             for (int u = 0; u < U3; ++u) {
                 const int e = tid + u * kSqThreads;
-                if (e < n3 / 4) reinterpret_cast<f4v*>(w3)[e] = r3[u];
+                if (e < n3 / 4) sq_put4(w3, 4 * e, r3[u], H, S, invH);
             }
             // (larger shapes: the rest by the loop)
             if (np / 4 > UP * kSqThreads) sq_stage<8>(pr + 4 * UP * kSqThreads, src + 4 * UP * kSqThreads, np - 4 * UP * kSqThreads);
-            if (n2 / 4 > U2 * kSqThreads) sq_stage<8>(w2 + 4 * U2 * kSqThreads, W2 + 4 * U2 * kSqThreads, n2 - 4 * U2 * kSqThreads);
-            if (n3 / 4 > U3 * kSqThreads) sq_stage<8>(w3 + 4 * U3 * kSqThreads, W3 + 4 * U3 * kSqThreads, n3 - 4 * U3 * kSqThreads);
+            if (n2 / 4 > U2 * kSqThreads) sq_stage_pad<8>(w2, W2, 4 * U2 * kSqThreads, n2, H, S, invH);
+            if (n3 / 4 > U3 * kSqThreads) sq_stage_pad<8>(w3, W3, 4 * U3 * kSqThreads, n3, H, S, invH);
         } else {
             sq_stage<16>(pr, src, np);
-            sq_stage<16>(w2, W2, n2);
-            sq_stage<16>(w3, W3, n3);
+            const float invH = 1.0f / (float)H;
+            sq_stage_pad<16>(w2, W2, 0, n2, H, S, invH);
+            sq_stage_pad<16>(w3, W3, 0, n3, H, S, invH);
         }
         __syncthreads();
-        for (int h = tid; h < H; h += kSqThreads) {
+        if (m == 0) sq_stamp(a, i, 1);
+        if (tid < H) {
             float s = 0.0f;
-            for (int c = 0; c < nch; ++c) s += pr[c * H + h];
-            float w_a = wa, w_b = wb;
-            if (h != tid) {  // (H > the workgroup: the rest of the units)
-                const float* wr = W1 + (int64_t)h * 2 * i;
-                w_a = wr[i - 1];
-                w_b = wr[2 * i - 1];
-            }
-            s = __builtin_fmaf(cp, w_a, s);
-            s = __builtin_fmaf(sp, w_b, s);
-            h1[h] = tanhf(s + b1[h]);
+            for (int c = 0; c < nch; ++c) s += pr[c * H + tid];
+            s = __builtin_fmaf(cp, wa, s);
+            s = __builtin_fmaf(sp, wb, s);
+            h1[tid] = tanhf(s + bias1);
         }
         __syncthreads();
-        for (int h = tid; h < H; h += kSqThreads) {
-            const float* wr = w2 + h * H;
+        if (m == 0) sq_stamp(a, i, 2);
+        if (tid < H) {
+            const float* wr = w2 + tid * S;
             float s = 0.0f;
             for (int k = 0; k < H; ++k) s = __builtin_fmaf(h1[k], wr[k], s);
-            h2[h] = tanhf(s + b2[h]);
+            h2[tid] = tanhf(s + bias2);
         }
         __syncthreads();
-        for (int p = tid; p < P; p += kSqThreads) {
-            const float* wr = w3 + p * H;
+        if (m == 0) sq_stamp(a, i, 3);
+        if (tid < P) {
+            const float* wr = w3 + tid * S;
             float s = 0.0f;
             for (int k = 0; k < H; ++k) s = __builtin_fmaf(h2[k], wr[k], s);
-            lg[p] = s + b3[p];
+            lg[tid] = s + bias3;
         }
     }
     __syncthreads();
     if (tid != 0) return;
+    if (m == 0) sq_stamp(a, i, 4);
     float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
 #pragma unroll
     for (int p = 0; p < K; ++p) wr[p] = lg[p];
@@ -321,12 +400,12 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
     for (int p = 0; p < K; ++p) hr[p] = lg[K + p];
 #pragma unroll
     for (int p = 0; p < K - 1; ++p) dr[p] = lg[2 * K + p];
-    const float zv = a.z[(int64_t)m * a.ldz + i];
     float out, lad;
     bool in, nd;
     nfk_rqs_element_lean<K, true>(zv, wr, hr, dr, a.c, out, lad, in, nd);
+    if (m == 0) sq_stamp(a, i, 5);
     a.x[(int64_t)m * a.ldx + i] = out;
-    const float acc = (i == 0 ? 0.0f : a.ldacc[m]) + lad;
+    const float acc = ldprev + lad;
     if (i + 1 < a.dim) {
         a.ldacc[m] = acc;
         const float arg = (a.pi * out) / a.bnd;  // (pi x) / B, flows.py:173's operation order
@@ -337,8 +416,9 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
     }
     if (a.status != nullptr) {
         const int bits = (in ? NFK_ST_INSIDE_SEEN : 0) | (in && nd ? NFK_ST_NEG_DISC : 0);
-        if (bits != 0 && (a.status[i] & bits) != bits) atomicOr(a.status + i, bits);
+        if (bits != 0) atomicOr(a.status + i, bits);  // (no read first: one round trip less)
     }
+    if (m == 0) sq_stamp(a, i, 6);
 }
 
 // one launch per column i: workgroups 0 .. M-1 finish conditioner i (one row
@@ -365,13 +445,25 @@ int sq_status() {
 
 int sq_chunks(int dim) { return (int)((2LL * (dim - 1) + kSqFC - 1) / kSqFC); }
 
+unsigned long long* g_sq_tdbg = nullptr;
+
 }  // namespace
+
+// diagnostic: a device buffer of dim * 12 uint64 for the phase clocks of the
+// next nfk_ar_seqinv calls (null: off).  Returns the previous buffer.
+extern "C" void* nfk_debug_sq_timing(void* buf) {
+    void* prev = g_sq_tdbg;
+    g_sq_tdbg = static_cast<unsigned long long*>(buf);
+    return prev;
+}
 
 extern "C" int nfk_ar_seqinv_supported(int32_t dim, int32_t hidden, int32_t K) {
     const bool k_ok = K == 4 || K == 8 || K == 10 || K == 16 || K == 32;
     // (k_sq_step's LDS: the row's layer-1 chunks, the activations, one weight matrix)
     const bool lds_ok = dim >= 2 && sq_lds(sq_chunks(dim), hidden, K) <= (size_t)160 * 1024;
-    return (dim >= 2 && dim <= 65536 && hidden >= 1 && hidden <= kSqMaxH && k_ok && lds_ok) ? 1 : 0;
+    static_assert(kSqMaxH <= kSqThreads && 3 * 32 - 1 <= kSqThreads, "sq_finish: one unit / logit per thread");
+    // (hidden >= 4: sq_put4's single row break)
+    return (dim >= 2 && dim <= 65536 && hidden >= 4 && hidden <= kSqMaxH && k_ok && lds_ok) ? 1 : 0;
 }
 
 extern "C" int64_t nfk_ar_seqinv_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch) {
@@ -416,6 +508,7 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         a.bnd = (float)tail_bound;
         // unconstrained_RQS(..., tail_bound=B) with the default minimum bin sizes (flows.py:206-207)
         a.c = nfk_make_const(K, -tail_bound, tail_bound, -tail_bound, tail_bound, 1, 1e-3, 1e-3, 1e-3);
+        a.tdbg = g_sq_tdbg;
         static bool attr = false;
         if (!attr) {
 #define NFK_SQ_ATTR(k)                                                                                         \
