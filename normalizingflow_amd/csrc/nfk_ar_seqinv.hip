@@ -11,16 +11,19 @@
 //   workgroups 0 .. M-1     finish conditioner i, one row each: its layer-1
 //                           chunks summed in order, plus the products of x_(i-1)'s
 //                           two features, + b1, tanh, layer 2, tanh, the output
-//                           layer (95 logits), the spline's inverse
-//                           (nfk_rqs_element_lean: the reference's 2B softmax /
+//                           layer (95 logits), the spline's inverse on one
+//                           wave (sq_spline_inv: the reference's 2B softmax /
 //                           softplus, then RQS, utils.py:27-152), x[m, i], the
 //                           row's log|det| in column order (flows.py:208), the
 //                           status word of column i, cos / sin (pi x_i / B)
 //   workgroups M ..         layer 1 of conditioner i + 1 over its features in
 //                           64-feature chunks, all but x_i's two (which the
-//                           first group is computing): [M, 64] x [64, H]
+//                           first group is computing), two workgroups per chunk
+//                           (the halves of the units): [M, 64] x [64, H / 2]
 //                           register tiles, fp32 partial sums (double-buffered
 //                           by conditioner parity)
+//   the last 8              conditioner i + 1's W2, W3, biases and two W1
+//                           columns read into each XCD's L2 for the next launch
 //
 // The conditioners' nn.Linear weights are read in place (fp32, a device table
 // of their pointers: the fused pack's table), and the arithmetic is fp32 FMA
@@ -31,6 +34,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <vector>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -44,10 +48,24 @@ namespace {
 constexpr int kSqFC = 64;        // layer-1 features per chunk workgroup
 constexpr int kSqThreads = 256;  // both kernels
 constexpr int kSqMaxRows = 64;   // rows per pass
-constexpr int kSqMaxH = 128;     // hidden width (the chunks' 4 x 4 register tiles: 64 rows x 128)
+constexpr int kSqMaxH = 128;     // hidden width (a chunk workgroup takes half of the units)
+
+typedef float sq_f4 __attribute__((ext_vector_type(4)));  // (HIP's float4 struct arrays went to scratch)
+typedef float sq_f2 __attribute__((ext_vector_type(2)));
+// The conditioners' weights come through a device table of pointers, which the
+// compiler cannot place in an address space: their loads were FLAT ones (which
+// every LDS wait also waits for).  Each such pointer is cast to global.
+typedef __attribute__((address_space(1))) const float sq_gf;
+typedef __attribute__((address_space(1))) const sq_f4 sq_gf4;
+typedef __attribute__((address_space(1))) const sq_f2 sq_gf2;
+__device__ __forceinline__ sq_gf* sq_glb(const float* p) { return (sq_gf*)p; }
+
+// one conditioner's nn.Linear tensors: W1 [H, 2i], b1, W2 [H, H], b2, W3 [P, H], b3
+struct SqCond {
+    const float *W1, *b1, *W2, *b2, *W3, *b3;
+};
 
 struct SqArgs {
-    const float* const* w;  // [6 (dim - 1)]: conditioner i = 1 .. dim-1: W1 [H, 2i], b1, W2 [H, H], b2, W3 [P, H], b3
     const float* init;      // init_param [P]
     const float* z;         // this pass's rows of the layer input
     int64_t ldz;
@@ -62,6 +80,7 @@ struct SqArgs {
     float pi, bnd;
     NfkSplineConst c;
     unsigned long long* tdbg;  // diagnostic phase clocks (nfk_debug_sq_timing), normally null
+    float* sink;               // [kSqThreads] workspace floats the prefetch workgroups' sums feed (never read)
 };
 
 // diagnostic: thread 0 of row 0's finish and of the first chunk workgroup stamp
@@ -70,228 +89,231 @@ __device__ __forceinline__ void sq_stamp(const SqArgs& a, int i, int slot) {
     if (a.tdbg != nullptr && threadIdx.x == 0) a.tdbg[(int64_t)i * 12 + slot] = __builtin_readcyclecounter();
 }
 
-// LDS of a k_sq_step workgroup: the finish part's (the row's layer-1 chunks,
-// h1, h2, logits, one weight matrix at a time) or the layer-1 part's
-// (64 features x 128 units of weights, 64 features x 64 rows), the larger
-inline size_t sq_fin_floats(int nch, int H, int K) {
-    const int P = 3 * K - 1;
-    auto al = [](int64_t v) { return (v + 3) & ~3LL; };
-    const int S = H | 1;  // (the staged W2 / W3 rows' stride, sq_finish)
-    return (size_t)(al((int64_t)nch * H) + 2 * al(H) + al(P) + al((int64_t)H * S) + al((int64_t)P * S));
+// LDS of a k_sq_step workgroup: the finish part's (h1, h2, the logits) or the
+// layer-1 part's (64 features x 64 units of weights, 64 features x 64 rows),
+// the larger
+inline size_t sq_fin_floats(int H, int K) {
+    (void)H;
+    return (size_t)(2 * 128 + 3 * K - 1);  // h1, h2 (kSqMaxH each), logits
 }
+// chunk workgroups' LDS strides: weights [unit][feature] rows kSqWS apart (odd:
+// the staging stores and the GEMM's per-unit reads both conflict-free), the
+// rows' features [feature][row] kSqFS apart (16-byte aligned row quads)
+constexpr int kSqWS = kSqFC + 1;
+constexpr int kSqFS = kSqMaxRows + 4;
 inline size_t sq_lds(int nch, int H, int K) {
-    const size_t l1 = (size_t)kSqFC * (kSqMaxH + kSqMaxRows);
-    const size_t f = sq_fin_floats(nch, H, K);
+    const size_t l1 = (size_t)(kSqMaxH / 2) * kSqWS + (size_t)kSqFC * kSqFS;
+    const size_t f = sq_fin_floats(H, K);
+    (void)nch;
     return (f > l1 ? f : l1) * sizeof(float);
 }
 
-// LDS <- global with U loads in flight per thread (one load, one wait, one
-// store per element made every staging loop a chain of HBM round trips:
-// 38.8 us per column at Polymer's shape)
-template <int U>
-__device__ __forceinline__ void sq_stage(float* __restrict__ dst, const float* __restrict__ src, int n) {
-    for (int b = threadIdx.x; b < n; b += kSqThreads * U) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = b + u * kSqThreads;
-            v[u] = e < n ? src[e] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = b + u * kSqThreads;
-            if (e < n) dst[e] = v[u];
-        }
-    }
-}
-
-// the same with 16-byte loads where both ends are 16-byte aligned and n % 4 == 0
-template <int U>
-__device__ __forceinline__ void sq_stage4(float* __restrict__ dst, const float* __restrict__ src, int n) {
-    if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) != 0 || (n & 3) != 0) {
-        sq_stage<U>(dst, src, n);
-        return;
-    }
-    const int n4 = n >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
-    float4* d4 = reinterpret_cast<float4*>(dst);
-    for (int b = threadIdx.x; b < n4; b += kSqThreads * U) {
-        float4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = b + u * kSqThreads;
-            if (e < n4) v[u] = s4[e];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = b + u * kSqThreads;
-            if (e < n4) d4[e] = v[u];
-        }
-    }
-}
-
-typedef float sq_f4 __attribute__((ext_vector_type(4)));  // (HIP's float4 struct arrays went to scratch)
-
-// row r, column c of a row-major [., H] matrix from its flat index (a float
-// estimate, then corrected: exact for the staged sizes)
-__device__ __forceinline__ void sq_rc(int flat, int H, float invH, int& r, int& c) {
-    r = (int)((float)flat * invH);
-    c = flat - r * H;
-    if (c >= H) {
-        ++r;
-        c -= H;
-    } else if (c < 0) {
-        --r;
-        c += H;
-    }
-}
-
-// four consecutive elements (flat index flat0) of a row-major [., H] matrix
-// into LDS rows of stride S = H | 1: an odd stride, so the layer dots (lane h
-// reading row h) hit 64 different banks.  H >= 4: at most one row break.
-__device__ __forceinline__ void sq_put4(float* dst, int flat0, sq_f4 v, int H, int S, float invH) {
-    int r, c;
-    sq_rc(flat0, H, invH, r, c);
-    const int base = r * S + c, d = S - H;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dst[base + q + (c + q >= H ? d : 0)] = v[q];
-}
-
-// the same staging, element by element, for elements from .. n - 1
-template <int U>
-__device__ __forceinline__ void sq_stage_pad(float* __restrict__ dst, const float* __restrict__ src, int from, int n,
-                                             int H, int S, float invH) {
-    for (int b = from + threadIdx.x; b < n; b += kSqThreads * U) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = b + u * kSqThreads;
-            v[u] = e < n ? src[e] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = b + u * kSqThreads;
-            if (e < n) {
-                int r, c;
-                sq_rc(e, H, invH, r, c);
-                dst[r * S + c] = v[u];
-            }
-        }
-    }
-}
-
-// layer 1 of conditioner j over features f0 .. f0 + 63 (chunk c), WITHOUT the
-// two features of coordinate j - 1 (cos at f = j - 1, sin at f = 2j - 1: the
-// finish of column j - 1 runs in the same launch and writes them; the finish of
-// conditioner j adds their products itself).  The chunk's weights and the rows'
-// features through LDS ([f][h], [f][m]); each thread a 4-row x 4-unit tile
-__device__ void sq_l1_chunk(const SqArgs& a, int j, int c, float* lds) {
-    float(*ws)[kSqMaxH] = reinterpret_cast<float(*)[kSqMaxH]>(lds);
-    float(*fs)[kSqMaxRows] = reinterpret_cast<float(*)[kSqMaxRows]>(lds + kSqFC * kSqMaxH);
-    const int F = 2 * j, f0 = c * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
-    const int H = a.H, M = a.M;
-    if (c == 0) sq_stamp(a, j - 1, 8);
-    const float* W1 = a.w[6 * (j - 1)];
+// layer 1 of conditioner j over features f0 .. f0 + 63 (chunk c = cc / 2) for
+// one half of its units (cc % 2), WITHOUT the two features of coordinate j - 1
+// (cos at f = j - 1, sin at f = 2j - 1: the finish of column j - 1 runs in the
+// same launch and writes them; the finish of conditioner j adds their products
+// itself).  Every operand is requested before any is stored (one memory round
+// trip), through LDS as ws [unit][feature] and fs [feature][row]; each thread a
+// 4-row x 2-unit tile
+__device__ void sq_l1_chunk(const SqArgs& a, const float* W1j, int j, int cc, float* lds) {
+    float* ws = lds;                                      // [kSqMaxH / 2][kSqWS]
+    float* fs = lds + (kSqMaxH / 2) * kSqWS;              // [kSqFC][kSqFS]
+    const int c = cc >> 1, F = 2 * j, f0 = c * kSqFC, nf = F - f0 < kSqFC ? F - f0 : kSqFC;
+    const int H = a.H, M = a.M, HH = ((H + 3) / 4) * 2;  // (units per half: even)
+    const int u_lo = (cc & 1) * HH, nu = H - u_lo < HH ? H - u_lo : HH;
+    if (cc == 0) sq_stamp(a, j - 1, 8);
     // (feature pairs: F = 2j is even, so every row segment is 8-byte aligned;
-    // 16 loads in flight per thread, consecutive threads along one weight row)
-    constexpr int FC2 = kSqFC / 2;
-    const float2* W1p = reinterpret_cast<const float2*>(W1);
-    for (int b = threadIdx.x; b < H * FC2; b += kSqThreads * 16) {
-        float2 v[16];
+    // 32 pairs per unit row, consecutive threads along one row.  Branch-free
+    // loads: a clamped index, then a select -- loads under divergent branches
+    // had each been followed by a wait)
+    constexpr int FC2 = kSqFC / 2, UW = (kSqMaxH / 2) * FC2 / kSqThreads, UF = kSqMaxRows * kSqFC / kSqThreads;
+    sq_gf2* W1p = reinterpret_cast<sq_gf2*>(sq_glb(W1j));
+    sq_f2 wv[UW];
+    float fv[UF];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int e = b + u * kSqThreads, h = e / FC2, f = 2 * (e - h * FC2);
-            v[u] = (e < H * FC2 && f < nf) ? W1p[((int64_t)h * F + f0 + f) >> 1] : make_float2(0.0f, 0.0f);
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int e = b + u * kSqThreads, h = e / FC2, f = 2 * (e - h * FC2);
-            if (e < H * FC2) {
-                ws[f][h] = v[u].x;
-                ws[f + 1][h] = v[u].y;
-            }
-        }
+    for (int u = 0; u < UW; ++u) {
+        const int e = threadIdx.x + u * kSqThreads, h = e / FC2, f = 2 * (e - h * FC2);
+        const bool ok = h < nu && f < nf;
+        wv[u] = W1p[ok ? ((int64_t)(u_lo + h) * F + f0 + f) >> 1 : 0];
+        wv[u] = ok ? wv[u] : sq_f2{0.0f, 0.0f};
     }
     // feature f of conditioner j: cos(pi x_f / B) for f < j, sin(pi x_(f-j) / B)
     // above (trig_transform's cat, flows.py:172-173)
-    for (int b = threadIdx.x; b < M * kSqFC; b += kSqThreads * 16) {
-        float v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int e = b + u * kSqThreads, m = e / kSqFC, f = e - m * kSqFC, g = f0 + f;
-            v[u] = 0.0f;
-            if (e < M * kSqFC && f < nf && g != j - 1 && g != 2 * j - 1)
-                v[u] = g < j ? a.feat[(int64_t)m * a.dim + g] : a.feat[((int64_t)M + m) * a.dim + (g - j)];
-        }
+    for (int u = 0; u < UF; ++u) {
+        const int e = threadIdx.x + u * kSqThreads, m = e / kSqFC, f = e - m * kSqFC, g = f0 + f;
+        const bool ok = m < M && f < nf && g != j - 1 && g != 2 * j - 1;
+        const int64_t idx = g < j ? (int64_t)m * a.dim + g : ((int64_t)M + m) * a.dim + (g - j);
+        fv[u] = a.feat[ok ? idx : 0];
+        fv[u] = ok ? fv[u] : 0.0f;
+    }
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int e = b + u * kSqThreads, m = e / kSqFC, f = e - m * kSqFC;
-            if (e < M * kSqFC) fs[f][m] = v[u];
-        }
+    for (int u = 0; u < UW; ++u) {
+        const int e = threadIdx.x + u * kSqThreads, h = e / FC2, f = 2 * (e - h * FC2);
+        ws[h * kSqWS + f] = wv[u].x;
+        ws[h * kSqWS + f + 1] = wv[u].y;
+    }
+#pragma unroll
+    for (int u = 0; u < UF; ++u) {
+        const int e = threadIdx.x + u * kSqThreads, m = e / kSqFC, f = e - m * kSqFC;
+        fs[f * kSqFS + m] = fv[u];
     }
     __syncthreads();
-    if (c == 0) sq_stamp(a, j - 1, 9);
+    if (cc == 0) sq_stamp(a, j - 1, 9);
     float* part = a.part + (int64_t)(j & 1) * M * a.nchmax * H;
-    const int HT = (H + 3) / 4, MT4 = (M + 3) / 4;
+    const int HT = (nu + 1) / 2, MT4 = (M + 3) / 4;
+    typedef float f4v __attribute__((ext_vector_type(4)));
     for (int t = threadIdx.x; t < HT * MT4; t += kSqThreads) {
-        const int h0 = 4 * (t % HT), m0 = 4 * (t / HT);
-        float acc[4][4];
+        const int u0 = 2 * (t % HT), m0 = 4 * (t / HT);
+        const float* w0 = ws + u0 * kSqWS;
+        const float* w1 = w0 + kSqWS;  // (u0 + 1 <= HH - 1 < kSqMaxH / 2: inside the buffer)
+        float acc[4][2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[r][u] = 0.0f;
+        for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = 0.0f;
+#pragma unroll 8
         for (int f = 0; f < nf; ++f) {
-            float fv[4], wv[4];
+            const f4v x = *reinterpret_cast<const f4v*>(fs + f * kSqFS + m0);
+            const float wa = w0[f], wb = w1[f];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) fv[r] = fs[f][(m0 + r) & (kSqMaxRows - 1)];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) wv[u] = ws[f][(h0 + u) & (kSqMaxH - 1)];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) acc[r][u] = __builtin_fmaf(fv[r], wv[u], acc[r][u]);
+            for (int r = 0; r < 4; ++r) {
+                acc[r][0] = __builtin_fmaf(x[r], wa, acc[r][0]);
+                acc[r][1] = __builtin_fmaf(x[r], wb, acc[r][1]);
+            }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (m0 + r < M && h0 + u < H) part[((int64_t)(m0 + r) * a.nchmax + c) * H + h0 + u] = acc[r][u];
+            for (int q = 0; q < 2; ++q)
+                if (m0 + r < M && u0 + q < nu)
+                    part[((int64_t)(m0 + r) * a.nchmax + c) * H + u_lo + u0 + q] = acc[r][q];
     }
-    if (c == 0) sq_stamp(a, j - 1, 10);
+    if (cc == 0) sq_stamp(a, j - 1, 10);
 }
 
-// the rest of conditioner i for ONE row m: its layer-1 chunks summed in order,
-// + the products of coordinate i - 1's two features (left out of the chunks),
-// + b1, tanh, layer 2, tanh, the output layer, the spline's inverse, x[m, i],
-// the row's log|det|, the status word, cos / sin of x[m, i]
+// the operands the next launch's finish stages from the conditioners' weights
+// (conditioner j: W2, W3, the biases, x_(j-1)'s two columns of W1) read into
+// this XCD's L2 (one such workgroup per XCD: 8 consecutive workgroups), their
+// sum fed to a store that never happens so the loads are kept
+__device__ void sq_prefetch(const SqArgs& a, const SqCond& w, int j, int K3) {
+    const int H = a.H, P = K3;
+    sq_gf *W1 = sq_glb(w.W1), *W2 = sq_glb(w.W2), *W3 = sq_glb(w.W3);
+    float acc = 0.0f;
+    const int n2 = H * H, n3 = P * H;
+    // one 4-byte load per 64-byte segment is enough to bring the line in
+    for (int e = threadIdx.x * 16; e < n2; e += kSqThreads * 16) acc += W2[e];
+    for (int e = threadIdx.x * 16; e < n3; e += kSqThreads * 16) acc += W3[e];
+    const int h = threadIdx.x < H ? threadIdx.x : 0, p = threadIdx.x < P ? threadIdx.x : 0;
+    sq_gf* wr = W1 + (int64_t)h * 2 * j;
+    acc += wr[j - 1] + wr[2 * j - 1] + sq_glb(w.b1)[h] + sq_glb(w.b2)[h] + sq_glb(w.b3)[p];
+    if (acc == 1.0e-30f) a.sink[threadIdx.x] = acc;
+}
+
+// The spline's inverse for one element on one wave (nfk_rqs_element_lean's
+// algorithm, utils.py:58-152 with the 2B softmax / softplus of flows.py:206-207,
+// spread over lanes): lanes 0-31 take the K width logits, 32-63 the K height
+// logits; max, the two softmax sums (xor butterflies over 32 lanes, every lane
+// the same sum) and the integer knot prefixes (a lane scan: exact, so the
+// knots are those of the sequential prefix) run in parallel, the bin is a
+// ballot count, and every lane then evaluates the same bin.  Every lane of the
+// wave must call it.
 template <int K>
-__device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
-    constexpr int P = 3 * K - 1;
-    const int H = a.H, tid = threadIdx.x;
-    // (16-byte aligned regions: the staged matrices are copied by float4)
-    const int HA = (H + 3) & ~3, PA = (P + 3) & ~3;
-    float* pr = lds;            // [nch][H]
-    float* h1 = pr + ((nch * H + 3) & ~3);  // [H]
-    float* h2 = h1 + HA;        // [H]
-    float* lg = h2 + HA;        // [P]
-    float* w2 = lg + PA;        // W2 [H][H] (row-major, as nn.Linear; rows S apart)
-    const int S = H | 1;        // (odd row stride: sq_put4)
-    float* w3 = w2 + ((H * S + 3) & ~3);  // W3 [P][H]
-    // every operand a thread needs from memory is requested up front (a load
-    // issued after a barrier is one more dependent round trip on the column's
-    // critical path): the biases (H <= 128 and P <= 95 < the workgroup, so one
-    // unit / logit per thread), thread 0's z[m, i] and the row's log|det| so far
-    if (m == 0) sq_stamp(a, i, 0);
-    const float* const* wt = a.w + 6 * (i > 0 ? i - 1 : 0);
-    float bias1 = 0.0f, bias2 = 0.0f, bias3 = 0.0f, zv = 0.0f, ldprev = 0.0f;
-    if (i > 0) {
-        if (tid < H) {
-            bias1 = wt[1][tid];
-            bias2 = wt[3][tid];
-        }
-        if (tid < P) bias3 = wt[5][tid];
+__device__ __forceinline__ void sq_spline_inv(const float* lg, float x, const NfkSplineConst& c, float& out,
+                                              float& lad, bool& inside, bool& neg_disc) {
+    static_assert(K >= 2 && K <= 32, "sq_spline_inv: one logit per lane of a 32-lane half");
+    const int lane = threadIdx.x & 63, hb = lane >> 5, p = lane & 31;
+    const bool act = p < K;
+    inside = !c.tails || ((x >= c.lo) && (x <= c.hi));
+    neg_disc = false;
+    const float two30 = 1073741824.0f;
+    const float sp30 = c.span * (1.0f / two30), inv30 = two30 / c.span;
+    const float fb30 = c.fw * two30, mb30 = c.min_w * two30;
+    const float raw = lg[hb * K + (act ? p : 0)];
+    float mx = act ? raw : -INFINITY;
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) mx = fmaxf(mx, __shfl_xor(mx, w, 32));
+    const float mL = mx * kL2E;
+    float e = act ? __builtin_amdgcn_exp2f(__builtin_fmaf(raw, kL2E, -mL)) : 0.0f;
+    float s1 = e;
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) s1 += __shfl_xor(s1, w, 32);
+    const float q = c.m2b * __builtin_amdgcn_rcpf(s1);
+    e = act ? __builtin_amdgcn_exp2f(__builtin_fmaf(e, q, -c.m2b)) : 0.0f;
+    float s2 = e;
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) s2 += __shfl_xor(s2, w, 32);
+    const float f30 = fb30 * __builtin_amdgcn_rcpf(s2);
+    const int v = p < K - 1 ? (int)__builtin_fmaf(e, f30, mb30) : 0;
+    int sc = v;
+#pragma unroll
+    for (int w = 1; w < 32; w <<= 1) {
+        const int t = __shfl_up(sc, w, 32);
+        sc += p >= w ? t : 0;
     }
-    if (tid == 0) {
+    const int pre = sc - v;  // knot p's integer position (pre[0] = 0)
+    const float s2w = __shfl(s2, 0), s2h = __shfl(s2, 32);
+    // the bin: how many inner height knots x has passed
+    const int xi = __float2int_rd(__builtin_fmaf(x, inv30, -c.lo * inv30));
+    const int k = __popcll(__ballot(hb == 1 && p >= 1 && p < K && xi >= pre));
+    const int k1 = k + 1 < K ? k + 1 : 0;
+    const int pw0 = __shfl(pre, k), pw1 = __shfl(pre, k1), ph0 = __shfl(pre, 32 + k), ph1 = __shfl(pre, 32 + k1);
+    const float low = __builtin_fmaf(s2w, 0.0f, c.lo), loh = __builtin_fmaf(s2h, 0.0f, c.lo);
+    const float cw_k = __builtin_fmaf(sp30, (float)pw0, low);
+    const float w_k = ((k == K - 1) ? c.hi : __builtin_fmaf(sp30, (float)pw1, low)) - cw_k;
+    const float ch_k = __builtin_fmaf(sp30, (float)ph0, loh);
+    const float h_k = ((k == K - 1) ? c.hi : __builtin_fmaf(sp30, (float)ph1, loh)) - ch_k;
+    // padded derivative index j + 1 holds logit j (utils.py:36-39)
+    const float raw_k = lg[2 * K + (k >= 1 ? k - 1 : 0)], raw_k1 = lg[2 * K + (k < K - 1 ? k : 0)];
+    const float d_k = (k == 0) ? c.d_edge : nfk_deriv_lean(raw_k, c.min_d);
+    const float d_k1 = (k == K - 1) ? c.d_edge : nfk_deriv_lean(raw_k1, c.min_d);
+    const float rw = nfk_rcp_fast(w_k);
+    const float delta = h_k * rw;
+    const float gap = (d_k + d_k1) - 2.0f * delta;
+    const float y = x - ch_k;
+    const float qa = y * gap + h_k * (delta - d_k);
+    const float qb = h_k * d_k - y * gap;
+    const float qc = (-delta) * y;
+    const float disc = qb * qb - (4.0f * qa) * qc;
+    neg_disc = inside && !(disc >= 0.0f);
+    const float th = nfk_div_fast(2.0f * qc, -qb - sqrtf(disc));
+    out = th * w_k + cw_k;
+    const float t1mt = th * (1.0f - th);
+    const float den = delta + gap * t1mt;
+    const float omt = 1.0f - th;
+    const float dnum = (delta * delta) * ((d_k1 * (th * th) + (2.0f * delta) * t1mt) + d_k * (omt * omt));
+    const float l = (__builtin_amdgcn_logf(dnum) - 2.0f * __builtin_amdgcn_logf(den)) * kLN2;
+    lad = inside ? -l : 0.0f;
+    out = inside ? out : x;
+}
+
+// the rest of conditioner i for ONE row m: its layer-1 chunk sums, + the
+// products of coordinate i - 1's two features (left out of the chunks), + b1,
+// tanh, layer 2, tanh, the output layer, the spline's inverse, x[m, i], the
+// row's log|det|, the status word, cos / sin of x[m, i].
+// Register form, every operand loaded once at the start (one round trip), only
+// the activations through LDS:
+//   layer 1   lanes 2o, 2o + 1: unit o, the row's chunk sums c = half, half + 2,
+//             ... (consecutive lanes on consecutive units: coalesced), the
+//             halves added by a lane swap (the same sum on both lanes)
+//   layers    16-lane groups g = tid / 16: outputs o = g + 16 p (pass p), lane
+//   2 and 3   l of the group on inputs 4l .. 4l + 3 and 64 + 4l .. 67 + 4l, so a
+//             group reads 256 contiguous bytes of a weight row per load; the
+//             16 lanes' dot products added by an xor butterfly (the same sum
+//             on every lane), lane p then finishing output g + 16 p
+template <int K>
+__device__ void sq_finish(const SqArgs& a, const SqCond& wt, int i, int nch, int m, float* lds) {
+    constexpr int P = 3 * K - 1;
+    constexpr int NP2 = kSqMaxH / 16, NP3 = (P + 15) / 16;  // passes of layers 2, 3
+    constexpr int CQ = 32;                                  // partial sums per lane per round
+    static_assert(kSqMaxH <= 128 && kSqThreads == 256, "sq_finish: 16 groups of 16 lanes, inputs 4l and 64 + 4l");
+    typedef sq_f4 f4v;
+    const int H = a.H, tid = threadIdx.x, ho = tid >> 1, half = tid & 1, g = tid >> 4, l = tid & 15;
+    const int HA = (H + 3) & ~3;
+    float* h1 = lds;         // [128] (zero past H: the layer reads run to 128)
+    float* h2 = h1 + 128;    // [128]
+    float* lg = h2 + 128;    // [P]
+    if (m == 0) sq_stamp(a, i, 0);
+    float zv = 0.0f, ldprev = 0.0f;
+    if (tid < 64) {  // (the spline's wave)
         zv = a.z[(int64_t)m * a.ldz + i];
         ldprev = i == 0 ? 0.0f : a.ldacc[m];
     }
@@ -299,118 +321,152 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
         // coordinate 0: init_param, the same logits for every row (flows.py:196-199)
         for (int p = tid; p < P; p += kSqThreads) lg[p] = a.init[p];
     } else {
-        const float *W1 = wt[0], *W2 = wt[2], *W3 = wt[4];
-        // ONE round trip for everything the row needs: its layer-1 partials
-        // (contiguous), W2, W3, and x_(i-1)'s two weight columns of W1 -- every
-        // load issued before any is waited for (a wait per region had made the
-        // finish three or four dependent HBM round trips)
-        const float* src = a.part + ((int64_t)(i & 1) * a.M + m) * a.nchmax * H;
-        const int np = nch * H, n2 = H * H, n3 = P * H;
-        const bool v4 = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(W2) |
-                          reinterpret_cast<uintptr_t>(W3)) & 15) == 0 && (np & 3) == 0 && (n2 & 3) == 0 &&
-                        (n3 & 3) == 0;
-        constexpr int UP = 8, U2 = 12, U3 = 12;
-        float wa = 0.0f, wb = 0.0f, cp = 0.0f, sp = 0.0f;
-        if (tid < H) {
-            const float* wr = W1 + (int64_t)tid * 2 * i;
-            wa = wr[i - 1];
-            wb = wr[2 * i - 1];
+        // every load issued before any is waited for; indices clamped (no branches)
+        const bool al = (H & 3) == 0 &&
+                        ((reinterpret_cast<uintptr_t>(wt.W2) | reinterpret_cast<uintptr_t>(wt.W3)) & 15) == 0;
+        sq_gf *W2 = sq_glb(wt.W2), *W3 = sq_glb(wt.W3);
+        f4v w2r[NP2][2], w3r[NP3][2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = 64 * j + 4 * l, kc = k < H ? k : 0;
+#pragma unroll
+            for (int p = 0; p < NP2; ++p) {
+                const int o = g + 16 * p, oc = o < H ? o : 0;
+                if (al) {
+                    w2r[p][j] = *reinterpret_cast<sq_gf4*>(W2 + (int64_t)oc * H + kc);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w2r[p][j][e] = W2[(int64_t)oc * H + (k + e < H ? k + e : 0)];
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < NP3; ++p) {
+                const int o = g + 16 * p, oc = o < P ? o : 0;
+                if (al) {
+                    w3r[p][j] = *reinterpret_cast<sq_gf4*>(W3 + (int64_t)oc * H + kc);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w3r[p][j][e] = W3[(int64_t)oc * H + (k + e < H ? k + e : 0)];
+                }
+            }
         }
-        cp = a.feat[(int64_t)m * a.dim + i - 1];
-        sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
-        if (v4) {
-            typedef sq_f4 f4v;
-            const float invH = 1.0f / (float)H;
-            const f4v *sp4 = reinterpret_cast<const f4v*>(src), *s24 = reinterpret_cast<const f4v*>(W2),
-                      *s34 = reinterpret_cast<const f4v*>(W3);
-            f4v rp[UP], r2[U2], r3[U3];
+        const int o1 = ho < H ? ho : 0;
+        sq_gf* pp = sq_glb(a.part + ((int64_t)(i & 1) * a.M + m) * a.nchmax * H + o1);
+        float pv[CQ];
 #pragma unroll
-            for (int u = 0; u < UP; ++u) {
-                const int e = tid + u * kSqThreads;
-                rp[u] = e < np / 4 ? sp4[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-            }
-#pragma unroll
-            for (int u = 0; u < U2; ++u) {
-                const int e = tid + u * kSqThreads;
-                r2[u] = e < n2 / 4 ? s24[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-            }
-#pragma unroll
-            for (int u = 0; u < U3; ++u) {
-                const int e = tid + u * kSqThreads;
-                r3[u] = e < n3 / 4 ? s34[e] : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-            }
-#pragma unroll
-            for (int u = 0; u < UP; ++u) {
-                const int e = tid + u * kSqThreads;
-                if (e < np / 4) reinterpret_cast<f4v*>(pr)[e] = rp[u];
-            }
-#pragma unroll
-            for (int u = 0; u < U2; ++u) {
-                const int e = tid + u * kSqThreads;
-                if (e < n2 / 4) sq_put4(w2, 4 * e, r2[u], H, S, invH);
-            }
-#pragma unroll
-            for (int u = 0; u < U3; ++u) {
-                const int e = tid + u * kSqThreads;
-                if (e < n3 / 4) sq_put4(w3, 4 * e, r3[u], H, S, invH);
-            }
-            // (larger shapes: the rest by the loop)
-            if (np / 4 > UP * kSqThreads) sq_stage<8>(pr + 4 * UP * kSqThreads, src + 4 * UP * kSqThreads, np - 4 * UP * kSqThreads);
-            if (n2 / 4 > U2 * kSqThreads) sq_stage_pad<8>(w2, W2, 4 * U2 * kSqThreads, n2, H, S, invH);
-            if (n3 / 4 > U3 * kSqThreads) sq_stage_pad<8>(w3, W3, 4 * U3 * kSqThreads, n3, H, S, invH);
-        } else {
-            sq_stage<16>(pr, src, np);
-            const float invH = 1.0f / (float)H;
-            sq_stage_pad<16>(w2, W2, 0, n2, H, S, invH);
-            sq_stage_pad<16>(w3, W3, 0, n3, H, S, invH);
+        for (int u = 0; u < CQ; ++u) {
+            const int c = half + 2 * u;
+            pv[u] = pp[(int64_t)(c < nch ? c : 0) * H];
         }
-        __syncthreads();
+        sq_gf* w1r = sq_glb(wt.W1) + (int64_t)o1 * 2 * i;
+        const float wa = w1r[i - 1], wb = w1r[2 * i - 1];
+        const float cp = a.feat[(int64_t)m * a.dim + i - 1];
+        const float sp = a.feat[((int64_t)a.M + m) * a.dim + i - 1];
+        // biases: b1 of unit ho (layer 1); b2, b3 of output g + 16 l (lane l finishes pass l)
+        const int o2 = g + 16 * l;
+        const float bias1 = sq_glb(wt.b1)[o1], bias2 = sq_glb(wt.b2)[o2 < H ? o2 : 0];
+        const float bias3 = sq_glb(wt.b3)[o2 < P ? o2 : 0];
+        if (tid >= H && tid < 128) h1[tid] = h2[tid] = 0.0f;
+        // (the weights past a row's end or past the last output: zero)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool kin = 64 * j + 4 * l + e < H;
+#pragma unroll
+                for (int p = 0; p < NP2; ++p) w2r[p][j][e] = kin && g + 16 * p < H ? w2r[p][j][e] : 0.0f;
+#pragma unroll
+                for (int p = 0; p < NP3; ++p) w3r[p][j][e] = kin && g + 16 * p < P ? w3r[p][j][e] : 0.0f;
+            }
         if (m == 0) sq_stamp(a, i, 1);
-        if (tid < H) {
-            float s = 0.0f;
-            for (int c = 0; c < nch; ++c) s += pr[c * H + tid];
-            s = __builtin_fmaf(cp, wa, s);
-            s = __builtin_fmaf(sp, wb, s);
-            h1[tid] = tanhf(s + bias1);
+        // layer 1: the chunk sums in chunk order within each lane's half
+        float s = 0.0f;
+#pragma unroll
+        for (int u = 0; u < CQ; ++u)
+            if (half + 2 * u < nch) s += pv[u];
+        for (int c0 = half + 2 * CQ; c0 < nch; c0 += 2 * CQ) {  // (more than 2 CQ chunks: dim > 2049)
+#pragma unroll
+            for (int u = 0; u < CQ; ++u) {
+                const int c = c0 + 2 * u;
+                pv[u] = pp[(int64_t)(c < nch ? c : 0) * H];
+            }
+#pragma unroll
+            for (int u = 0; u < CQ; ++u)
+                if (c0 + 2 * u < nch) s += pv[u];
         }
+        s += __shfl_xor(s, 1);
+        s = __builtin_fmaf(cp, wa, s);
+        s = __builtin_fmaf(sp, wb, s);
+        if (half == 0 && ho < H) h1[ho] = tanhf(s + bias1);
         __syncthreads();
         if (m == 0) sq_stamp(a, i, 2);
-        if (tid < H) {
-            const float* wr = w2 + tid * S;
-            float s = 0.0f;
-            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h1[k], wr[k], s);
-            h2[tid] = tanhf(s + bias2);
+        // layer 2
+        {
+            const f4v x0 = *reinterpret_cast<const f4v*>(h1 + 4 * l);
+            const f4v x1 = *reinterpret_cast<const f4v*>(h1 + 64 + 4 * l);
+            float d[NP2];
+#pragma unroll
+            for (int p = 0; p < NP2; ++p) {
+                float t = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t = __builtin_fmaf(x0[e], w2r[p][0][e], t);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t = __builtin_fmaf(x1[e], w2r[p][1][e], t);
+                d[p] = t;
+            }
+#pragma unroll
+            for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+                for (int p = 0; p < NP2; ++p) d[p] += __shfl_xor(d[p], w, 16);
+            float mine = d[0];
+#pragma unroll
+            for (int p = 1; p < NP2; ++p) mine = l == p ? d[p] : mine;
+            if (l < NP2 && o2 < H) h2[o2] = tanhf(mine + bias2);
         }
         __syncthreads();
         if (m == 0) sq_stamp(a, i, 3);
-        if (tid < P) {
-            const float* wr = w3 + tid * S;
-            float s = 0.0f;
-            for (int k = 0; k < H; ++k) s = __builtin_fmaf(h2[k], wr[k], s);
-            lg[tid] = s + bias3;
+        // layer 3
+        {
+            const f4v x0 = *reinterpret_cast<const f4v*>(h2 + 4 * l);
+            const f4v x1 = *reinterpret_cast<const f4v*>(h2 + 64 + 4 * l);
+            float d[NP3];
+#pragma unroll
+            for (int p = 0; p < NP3; ++p) {
+                float t = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t = __builtin_fmaf(x0[e], w3r[p][0][e], t);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t = __builtin_fmaf(x1[e], w3r[p][1][e], t);
+                d[p] = t;
+            }
+#pragma unroll
+            for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+                for (int p = 0; p < NP3; ++p) d[p] += __shfl_xor(d[p], w, 16);
+            float mine = d[0];
+#pragma unroll
+            for (int p = 1; p < NP3; ++p) mine = l == p ? d[p] : mine;
+            if (l < NP3 && o2 < P) lg[o2] = mine + bias3;
         }
+        (void)HA;
     }
     __syncthreads();
-    if (tid != 0) return;
+    if (tid >= 64) return;
     if (m == 0) sq_stamp(a, i, 4);
-    float wr[K], hr[K], dr[K - 1 > 0 ? K - 1 : 1];
-#pragma unroll
-    for (int p = 0; p < K; ++p) wr[p] = lg[p];
-#pragma unroll
-    for (int p = 0; p < K; ++p) hr[p] = lg[K + p];
-#pragma unroll
-    for (int p = 0; p < K - 1; ++p) dr[p] = lg[2 * K + p];
     float out, lad;
     bool in, nd;
-    nfk_rqs_element_lean<K, true>(zv, wr, hr, dr, a.c, out, lad, in, nd);
+    sq_spline_inv<K>(lg, zv, a.c, out, lad, in, nd);
+    if (tid != 0) return;
     if (m == 0) sq_stamp(a, i, 5);
     a.x[(int64_t)m * a.ldx + i] = out;
     const float acc = ldprev + lad;
     if (i + 1 < a.dim) {
         a.ldacc[m] = acc;
         const float arg = (a.pi * out) / a.bnd;  // (pi x) / B, flows.py:173's operation order
-        a.feat[(int64_t)m * a.dim + i] = cosf(arg);
-        a.feat[((int64_t)a.M + m) * a.dim + i] = sinf(arg);
+        float sv, cv;
+        sincosf(arg, &sv, &cv);
+        a.feat[(int64_t)m * a.dim + i] = cv;
+        a.feat[((int64_t)a.M + m) * a.dim + i] = sv;
     } else if (a.logdet != nullptr && a.mode != 0) {
         a.logdet[m] = a.mode == 2 ? a.logdet[m] + acc : acc;
     }
@@ -422,16 +478,23 @@ __device__ void sq_finish(const SqArgs& a, int i, int nch, int m, float* lds) {
 }
 
 // one launch per column i: workgroups 0 .. M-1 finish conditioner i (one row
-// each); workgroups M .. M + nch_next - 1 run the layer-1 chunks of conditioner
-// i + 1 that do not need x_i (double-buffered partial sums by parity)
+// each); workgroups M .. M + 2 nch_next - 1 run the layer-1 chunks of
+// conditioner i + 1 that do not need x_i (two per 64 features: the halves of
+// its units; double-buffered partial sums by parity); the last 8 read the
+// operands of conditioner i + 1's finish into every XCD's L2
 template <int K>
-__global__ __launch_bounds__(kSqThreads, 1) void k_sq_step(SqArgs a, int i, int nch, int nch_next) {
+// (the conditioners' tensor pointers are kernel arguments: read from a device
+// table they were one more dependent memory round trip per launch)
+__global__ __launch_bounds__(kSqThreads, 1) void k_sq_step(SqArgs a, SqCond cur, SqCond next, int i, int nch,
+                                                           int nch_next) {
     extern __shared__ float sq_smem[];
     const int b = blockIdx.x;
     if (b < a.M)
-        sq_finish<K>(a, i, nch, b, sq_smem);
+        sq_finish<K>(a, cur, i, nch, b, sq_smem);
+    else if (b < a.M + 2 * nch_next)
+        sq_l1_chunk(a, next.W1, i + 1, b - a.M, sq_smem);
     else
-        sq_l1_chunk(a, i + 1, b - a.M, sq_smem);
+        sq_prefetch(a, next, i + 1, 3 * K - 1);
 }
 
 int sq_status() {
@@ -462,14 +525,14 @@ extern "C" int nfk_ar_seqinv_supported(int32_t dim, int32_t hidden, int32_t K) {
     // (k_sq_step's LDS: the row's layer-1 chunks, the activations, one weight matrix)
     const bool lds_ok = dim >= 2 && sq_lds(sq_chunks(dim), hidden, K) <= (size_t)160 * 1024;
     static_assert(kSqMaxH <= kSqThreads && 3 * 32 - 1 <= kSqThreads, "sq_finish: one unit / logit per thread");
-    // (hidden >= 4: sq_put4's single row break)
+    // (hidden >= 4: the layer halves' split point KS stays inside a row)
     return (dim >= 2 && dim <= 65536 && hidden >= 4 && hidden <= kSqMaxH && k_ok && lds_ok) ? 1 : 0;
 }
 
 extern "C" int64_t nfk_ar_seqinv_workspace(int32_t dim, int32_t hidden, int32_t K, int64_t batch) {
     if (!nfk_ar_seqinv_supported(dim, hidden, K) || batch <= 0) return 0;
     const int64_t M = batch < kSqMaxRows ? batch : kSqMaxRows;
-    return 2 * M * dim + 2LL * sq_chunks(dim) * M * hidden + M;
+    return 2 * M * dim + 2LL * sq_chunks(dim) * M * hidden + M + kSqThreads;
 }
 
 extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* weights, const float* init_param,
@@ -485,10 +548,19 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
     if (workspace_floats < nfk_ar_seqinv_workspace(dim, hidden, K, batch))
         return nfk_set_error("nfk_ar_seqinv: workspace too small (nfk_ar_seqinv_workspace)");
     hipStream_t st = (hipStream_t)stream;
+    // the pointer table to the host once per call (ordered after the stream's
+    // earlier work), so each launch takes its conditioners' pointers as arguments
+    std::vector<const float*> tab((size_t)6 * (dim - 1));
+    if (hipMemcpyAsync(tab.data(), weights, tab.size() * sizeof(const float*), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return nfk_set_error("nfk_ar_seqinv: reading the weight pointer table failed");
+    auto cond = [&](int j) {  // conditioner j = 1 .. dim-1 (j out of range: conditioner 1, unused)
+        const float* const* w = tab.data() + 6 * ((j >= 1 && j < dim ? j : 1) - 1);
+        return SqCond{w[0], w[1], w[2], w[3], w[4], w[5]};
+    };
     for (int64_t r0 = 0; r0 < batch; r0 += kSqMaxRows) {
         const int M = (int)(batch - r0 < kSqMaxRows ? batch - r0 : kSqMaxRows);
         SqArgs a;
-        a.w = weights;
         a.init = init_param;
         a.z = z + r0 * ldz;
         a.ldz = ldz;
@@ -498,6 +570,7 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         a.part = workspace + 2LL * M * dim;
         a.ldacc = a.part + 2LL * sq_chunks(dim) * M * hidden;
         a.nchmax = sq_chunks(dim);
+        a.sink = a.ldacc + M;
         a.logdet = logdet_mode != 0 ? logdet + r0 : nullptr;
         a.status = status;
         a.mode = logdet_mode;
@@ -523,9 +596,13 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         for (int i = 0; i < dim; ++i) {
             const int nch = (2 * i + kSqFC - 1) / kSqFC;
             const int nxt = i + 1 < dim ? (2 * (i + 1) + kSqFC - 1) / kSqFC : 0;
+            const int pre = i + 1 < dim ? 8 : 0;  // (one prefetch workgroup per XCD)
+            const SqCond cur = cond(i), next = cond(i + 1);
             const size_t lds = sq_lds(nch, hidden, K);
 #define NFK_SQ_STEP(k) \
-    if (K == k) hipLaunchKernelGGL(k_sq_step<k>, dim3((unsigned)(M + nxt)), dim3(kSqThreads), lds, st, a, i, nch, nxt);
+    if (K == k)    \
+        hipLaunchKernelGGL(k_sq_step<k>, dim3((unsigned)(M + 2 * nxt + pre)), dim3(kSqThreads), lds, st, a, cur, next, \
+                           i, nch, nxt);
             NFK_SQ_STEP(4) NFK_SQ_STEP(8) NFK_SQ_STEP(10) NFK_SQ_STEP(16) NFK_SQ_STEP(32)
 #undef NFK_SQ_STEP
             if (int e = sq_status()) return e;
