@@ -521,9 +521,10 @@ int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const 
  * features, layers 2-3, the spline's inverse and the trig features of x_i;
  * beside them, workgroups run conditioner i+1's layer 1 over the features
  * already known, 64 at a time), fp32 arithmetic, the weights read in
- * place.  weights: a DEVICE table of 6 (dim - 1) pointers (W1, b1, W2, b2, W3,
- * b3 of conditioners 1 .. dim-1, fp32 contiguous nn.Linear tensors: the same
- * table nfk_fused_ar_pack reads); init_param [3K-1].  z -> x [batch, dim],
+ * place.  weights: a HOST array of 6 (dim - 1) device pointers (W1, b1, W2,
+ * b2, W3, b3 of conditioners 1 .. dim-1, fp32 contiguous nn.Linear tensors: the
+ * entries of the table nfk_fused_ar_pack reads; each launch takes its
+ * conditioners' pointers as arguments); init_param [3K-1].  z -> x [batch, dim],
  * logdet mode 0/1/2 (the inverse's -log|det|), status [dim] (nullable).
  * workspace: nfk_ar_seqinv_workspace(dim, hidden, K, batch) floats.  64 rows
  * per pass.  hidden <= 128, K in {4, 8, 10, 16, 32}.

@@ -25,8 +25,8 @@
 //   the last 8              conditioner i + 1's W2, W3, biases and two W1
 //                           columns read into each XCD's L2 for the next launch
 //
-// The conditioners' nn.Linear weights are read in place (fp32, a device table
-// of their pointers: the fused pack's table), and the arithmetic is fp32 FMA
+// The conditioners' nn.Linear weights are read in place (fp32; a host table of
+// their device pointers, passed to each launch as arguments), and the arithmetic is fp32 FMA
 // throughout: the inverse is latency-bound (4,095 dependent launches per layer
 // at Polymer's shape), not bandwidth- or FLOP-bound, and every weight is read
 // once per layer (1.68 GB at Polymer, 0.2 ms of HBM time).
@@ -34,7 +34,6 @@
 
 #include <cmath>
 #include <cstdint>
-#include <vector>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -208,6 +207,23 @@ __device__ void sq_prefetch(const SqArgs& a, const SqCond& w, int j, int K3) {
     if (acc == 1.0e-30f) a.sink[threadIdx.x] = acc;
 }
 
+// sums over lane pairs / 16-lane groups by DPP moves (no LDS round trip, as
+// __shfl_xor's ds_bpermute has): xor 1, xor 2 (quad permutes), then the
+// half-row and row mirrors, which swap the already-equal quads / halves; each
+// step adds a lane's value and its partner's, so every lane ends with the
+// same sum
+template <int CTRL>
+__device__ __forceinline__ float sq_dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float sq_sum2(float v) { return v + sq_dpp<0xB1>(v); }
+__device__ __forceinline__ float sq_sum16(float v) {
+    v += sq_dpp<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += sq_dpp<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += sq_dpp<0x141>(v);  // row_half_mirror
+    return v + sq_dpp<0x140>(v);  // row_mirror
+}
+
 // The spline's inverse for one element on one wave (nfk_rqs_element_lean's
 // algorithm, utils.py:58-152 with the 2B softmax / softplus of flows.py:206-207,
 // spread over lanes): lanes 0-31 take the K width logits, 32-63 the K height
@@ -297,8 +313,8 @@ __device__ __forceinline__ void sq_spline_inv(const float* lg, float x, const Nf
 //   layers    16-lane groups g = tid / 16: outputs o = g + 16 p (pass p), lane
 //   2 and 3   l of the group on inputs 4l .. 4l + 3 and 64 + 4l .. 67 + 4l, so a
 //             group reads 256 contiguous bytes of a weight row per load; the
-//             16 lanes' dot products added by an xor butterfly (the same sum
-//             on every lane), lane p then finishing output g + 16 p
+//             16 lanes' dot products added by DPP moves (sq_sum16: the same
+//             sum on every lane), lane p then finishing output g + 16 p
 template <int K>
 __device__ void sq_finish(const SqArgs& a, const SqCond& wt, int i, int nch, int m, float* lds) {
     constexpr int P = 3 * K - 1;
@@ -394,7 +410,7 @@ __device__ void sq_finish(const SqArgs& a, const SqCond& wt, int i, int nch, int
             for (int u = 0; u < CQ; ++u)
                 if (c0 + 2 * u < nch) s += pv[u];
         }
-        s += __shfl_xor(s, 1);
+        s = sq_sum2(s);
         s = __builtin_fmaf(cp, wa, s);
         s = __builtin_fmaf(sp, wb, s);
         if (half == 0 && ho < H) h1[ho] = tanhf(s + bias1);
@@ -415,9 +431,7 @@ __device__ void sq_finish(const SqArgs& a, const SqCond& wt, int i, int nch, int
                 d[p] = t;
             }
 #pragma unroll
-            for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-                for (int p = 0; p < NP2; ++p) d[p] += __shfl_xor(d[p], w, 16);
+            for (int p = 0; p < NP2; ++p) d[p] = sq_sum16(d[p]);
             float mine = d[0];
 #pragma unroll
             for (int p = 1; p < NP2; ++p) mine = l == p ? d[p] : mine;
@@ -440,9 +454,7 @@ __device__ void sq_finish(const SqArgs& a, const SqCond& wt, int i, int nch, int
                 d[p] = t;
             }
 #pragma unroll
-            for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-                for (int p = 0; p < NP3; ++p) d[p] += __shfl_xor(d[p], w, 16);
+            for (int p = 0; p < NP3; ++p) d[p] = sq_sum16(d[p]);
             float mine = d[0];
 #pragma unroll
             for (int p = 1; p < NP3; ++p) mine = l == p ? d[p] : mine;
@@ -548,14 +560,9 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
     if (workspace_floats < nfk_ar_seqinv_workspace(dim, hidden, K, batch))
         return nfk_set_error("nfk_ar_seqinv: workspace too small (nfk_ar_seqinv_workspace)");
     hipStream_t st = (hipStream_t)stream;
-    // the pointer table to the host once per call (ordered after the stream's
-    // earlier work), so each launch takes its conditioners' pointers as arguments
-    std::vector<const float*> tab((size_t)6 * (dim - 1));
-    if (hipMemcpyAsync(tab.data(), weights, tab.size() * sizeof(const float*), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return nfk_set_error("nfk_ar_seqinv: reading the weight pointer table failed");
+    // (a HOST table: each launch takes its conditioners' pointers as arguments)
     auto cond = [&](int j) {  // conditioner j = 1 .. dim-1 (j out of range: conditioner 1, unused)
-        const float* const* w = tab.data() + 6 * ((j >= 1 && j < dim ? j : 1) - 1);
+        const float* const* w = weights + 6 * ((j >= 1 && j < dim ? j : 1) - 1);
         return SqCond{w[0], w[1], w[2], w[3], w[4], w[5]};
     };
     for (int64_t r0 = 0; r0 < batch; r0 += kSqMaxRows) {

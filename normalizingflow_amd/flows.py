@@ -921,11 +921,11 @@ class NSF_AR(_HipFlow):
         pack = self._fused_pack(x.device)
         if pack is not None and inverse and not K_.fused_ar_inverse_supported(self.dim, self._pack_cache[2], self.K):
             # a streamed-forward shape (Polymer's 2,048 coordinates): the inverse
-            # column by column, both launches per column issued by the library
+            # column by column, one launch per column issued by the library
             hidden, keep = self._pack_cache[2], self._pack_cache[3]
             if config.USE_AR_SEQINV and K_.ar_seqinv_supported(self.dim, hidden, self.K):
                 z = torch.empty_like(x, memory_format=torch.contiguous_format)
-                K_.ar_seqinv(x, keep[0], keep[1], self.dim, hidden, self.K, float(self.B), z, logdet=logdet,
+                K_.ar_seqinv(x, keep[3], keep[1], self.dim, hidden, self.K, float(self.B), z, logdet=logdet,
                              logdet_mode=mode, status=status)
                 return z
             pack = None  # (the per-column path below)

@@ -486,8 +486,9 @@ def fused_ar_inverse_supported(dim, hidden, K):
 def fused_ar_pack(weights, init_param, dim, hidden, K):
     """The fused NSF_AR pack from the conditioners' Linear parameters:
     ``weights`` = [(W1, b1, W2, b2, W3, b3) for conditioner 1 .. dim-1].
-    Returns (pack, keep): ``keep`` holds the pointer table and any contiguous
-    copies the pack kernel read (alive until the stream has run it)."""
+    Returns (pack, keep): ``keep`` = (device pointer table, init_param, the
+    tensors -- contiguous copies where needed, alive until the stream has run
+    the pack kernel --, the same pointers as a host array for ar_seqinv)."""
     flat = [t.detach() for ws in weights for t in ws]
     dev = _require_hip(init_param, *flat)
     flat = [t if t.is_contiguous() and t.dtype == F32 else t.contiguous().to(F32) for t in flat]
@@ -501,7 +502,8 @@ def fused_ar_pack(weights, init_param, dim, hidden, K):
     pack = torch.empty(n, dtype=F32, device=dev)
     _lib.call("nfk_fused_ar_pack", table.data_ptr(), init.data_ptr(), dim, hidden, K, pack.data_ptr(),
               _stream(dev))
-    return pack, (table, init, flat)
+    host = (ctypes.c_void_p * len(flat))(*[t.data_ptr() for t in flat])
+    return pack, (table, init, flat, host)
 
 
 def fused_ar(x, pack, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, inverse=False, status=None,
@@ -817,21 +819,22 @@ def ar_seqinv_supported(dim, hidden, K):
     return bool(_lib.load().nfk_ar_seqinv_supported(dim, hidden, K))
 
 
-def ar_seqinv(z, table, init_param, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, status=None):
-    """NSF_AR.inverse of one layer (include/nfk.h nfk_ar_seqinv): ``table`` is
-    the device table of the conditioners' Linear tensors that fused_ar_pack
-    built (6 per conditioner)."""
-    dev = _require_hip(z, table, init_param, out, logdet, status)
+def ar_seqinv(z, ptrs, init_param, dim, hidden, K, tail_bound, out, *, logdet, logdet_mode, status=None):
+    """NSF_AR.inverse of one layer (include/nfk.h nfk_ar_seqinv): ``ptrs`` is
+    the HOST array of the conditioners' Linear tensor pointers that
+    fused_ar_pack returns (keep[3], 6 per conditioner)."""
+    dev = _require_hip(z, init_param, out, logdet, status)
     B = z.shape[0]
     zp, ldz = _mat(z, "z")
     op, ldo = _mat(out, "out")
     if z.shape[1] != dim or out.shape != z.shape:
         raise ValueError("ar_seqinv: z and out must be [B, %d]" % dim)
-    if table.dtype != torch.int64 or table.numel() != 6 * (dim - 1):
-        raise ValueError("ar_seqinv: the pointer table must hold 6 (dim - 1) int64 entries")
+    if not isinstance(ptrs, ctypes.Array) or len(ptrs) != 6 * (dim - 1):
+        raise ValueError("ar_seqinv: ptrs must be a ctypes array of 6 (dim - 1) pointers (fused_ar_pack's keep[3])")
     lib = _lib.load()
     nws = int(lib.nfk_ar_seqinv_workspace(dim, hidden, K, B))
     ws = torch.empty(max(nws, 4), dtype=F32, device=dev)
-    _timed("nfk_ar_seqinv", dev, "nfk_ar_seqinv", zp, ldz, table.data_ptr(), _vec(init_param, 3 * K - 1, "init_param"),
+    _timed("nfk_ar_seqinv", dev, "nfk_ar_seqinv", zp, ldz, ctypes.cast(ptrs, ctypes.c_void_p).value,
+           _vec(init_param, 3 * K - 1, "init_param"),
            dim, hidden, K, float(tail_bound), op, ldo, _vec(logdet, B, "logdet"), logdet_mode, B,
            _vec(status, dim, "status", torch.int32), ws.data_ptr(), nws, _stream(dev))

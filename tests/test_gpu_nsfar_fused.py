@@ -522,7 +522,7 @@ def test_ar_seqinv_vs_oracle(dim, K, rows, hip_device):
             out = torch.empty_like(zd)
             st = torch.zeros(dim, dtype=torch.int32, device=hip_device)
             keep = layer._pack_cache[3]
-            K_.ar_seqinv(zd, keep[0], keep[1], dim, 100, K, 1.5, out, logdet=ld0, logdet_mode=2, status=st)
+            K_.ar_seqinv(zd, keep[3], keep[1], dim, 100, K, 1.5, out, logdet=ld0, logdet_mode=2, status=st)
     finally:
         lib.nfk_debug_ar_stream(prev)
         layer.invalidate_caches()
