@@ -254,6 +254,141 @@ __global__ __launch_bounds__(64 * NW, 1) void k_wl_gemm(WlGemm a) {
 }
 
 // ---------------------------------------------------------------------------
+// GEMM + activation in one launch (hidden layers 1 and 2 at <= 64 rows): a
+// workgroup owns TWO output tiles of one group over the WHOLE contraction, its
+// 4 waves each a quarter of the k-blocks.  Each wave streams its weights AND
+// its input fragments (L2-resident) straight into a register ring PF k-blocks
+// deep -- no LDS and no barrier per step -- then the four waves' sums meet in
+// LDS, are added in wave order (fixed: deterministic), unscaled, + bias, tanh,
+// and written as the next GEMM's fp16 hi/lo fragments.  No split-K partial
+// sums and no k_wl_act launch (whose ~6 us, plus a kernel boundary, per stage
+// were a sixth of a layer).
+struct WlGemmAct {
+    const float* pack[2];  // the two groups' packs
+    const float* xf[2];    // their input fragments: halfs [mt][kb][part][lane][8]
+    const float* bias[2];
+    const float* xun;      // per-row input unscale (nullptr: 2^-14, a hidden layer's input)
+    float* out[2];         // output fragments [MT][KBo][part][64][8] halfs
+    int N, NT, KB, M, KBo, npair;
+};
+
+template <int MT, int PF>
+__global__ __launch_bounds__(256, 1) void k_wl_gemm_act(WlGemmAct a) {
+    constexpr int PER = 4 + 2 * MT;  // vector-memory operations per wave and step
+    extern __shared__ __attribute__((aligned(16))) float4 red4[];  // [4 waves][2 tiles][MT][64]
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tp = blockIdx.x % a.npair, g = blockIdx.x / a.npair;
+    const float4* xg = reinterpret_cast<const float4*>(a.xf[g]);
+    const f32x4* wg = reinterpret_cast<const f32x4*>(a.pack[g] + kWlHdr);
+    int ntc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) ntc[t] = 2 * tp + t < a.NT ? 2 * tp + t : a.NT - 1;
+    // this wave's k-blocks [kb0, kb0 + nk)
+    const int KW = (a.KB + 3) >> 2;
+    const int kb0 = wid * KW < a.KB ? wid * KW : a.KB;
+    const int nk = a.KB - kb0 < KW ? a.KB - kb0 : KW;
+    const int64_t zoff = (int64_t)a.NT * a.KB * 2 * 64;  // the pack's zero block (f32x4 units)
+    f32x4 w[PF][2][2];
+    float4 x[PF][MT][2];
+    auto issue = [&](int kk, f32x4 (&dw)[2][2], float4 (&dx)[MT][2]) {
+        // steps past the wave's range: zero weights (the zero block) times a
+        // valid input block -- branch-free, so the counted waits stay exact
+        const int64_t live = kk < nk ? 1 : 0;
+        const int kx = kb0 + (kk < nk ? kk : 0);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int64_t off = ((int64_t)ntc[t] * a.KB + kb0 + kk) * 2 * 64;
+            const f32x4* p = wg + (zoff + live * (off - zoff)) + lane;
+#if NFK_WL_NT
+            dw[t][0] = __builtin_nontemporal_load(p);
+            dw[t][1] = __builtin_nontemporal_load(p + 64);
+#else
+            dw[t][0] = p[0];
+            dw[t][1] = p[64];
+#endif
+        }
+#pragma unroll
+        for (int s = 0; s < MT; ++s) {
+            const float4* f = xg + ((int64_t)(s * a.KB + (kx < a.KB ? kx : a.KB - 1)) * 2) * 64 + lane;
+            dx[s][0] = f[0];
+            dx[s][1] = f[64];
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < PF; ++j) issue(j, w[j], x[j]);
+    f32x4 acc[2][MT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < MT; ++s) acc[t][s] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int nkr = (KW + PF - 1) / PF * PF;  // (uniform over the workgroup's waves)
+    for (int k0 = 0; k0 < nkr; k0 += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PF - 1) * PER) : "memory");
+            h8 xh[MT], xl[MT];
+#pragma unroll
+            for (int s = 0; s < MT; ++s) {
+                xh[s] = __builtin_bit_cast(h8, x[j][s][0]);
+                xl[s] = __builtin_bit_cast(h8, x[j][s][1]);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const h8 ah = __builtin_bit_cast(h8, w[j][t][0]), al = __builtin_bit_cast(h8, w[j][t][1]);
+#pragma unroll
+                for (int s = 0; s < MT; ++s) {
+                    acc[t][s] = mfma16(al, xh[s], acc[t][s]);
+                    acc[t][s] = mfma16(ah, xl[s], acc[t][s]);
+                    acc[t][s] = mfma16(ah, xh[s], acc[t][s]);
+                }
+            }
+            issue(k0 + j + PF, w[j], x[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the waves' sums through LDS; wave v then finishes the (tile, sample
+    // tile) pairs p = v, v + 4, ...: sum over waves 0..3 in order, activation
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < MT; ++s)
+            red4[((wid * 2 + t) * MT + s) * 64 + lane] = make_float4(acc[t][s][0], acc[t][s][1], acc[t][s][2], acc[t][s][3]);
+    __syncthreads();
+    const int q = lane >> 4, n = lane & 15;
+    for (int pr = wid; pr < 2 * MT; pr += 4) {
+        const int t = pr / MT, sm = pr - t * MT, nt = 2 * tp + t;
+        if (nt >= 2 * a.KBo) continue;  // (wave-uniform) past the fragments' features
+        float4 v = red4[((0 * 2 + t) * MT + sm) * 64 + lane];
+#pragma unroll
+        for (int wv = 1; wv < 4; ++wv) {
+            const float4 o = red4[((wv * 2 + t) * MT + sm) * 64 + lane];
+            v.x += o.x, v.y += o.y, v.z += o.z, v.w += o.w;
+        }
+        const int m = 16 * sm + n, f0 = 16 * nt + 4 * q;
+        const float u = a.pack[g][0] * (a.xun != nullptr ? a.xun[m < a.M ? m : 0] : 1.0f / kWlAct);
+        const float* bz = a.bias[g];
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        _Float16 hi[4], lo[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float h = 0.0f;
+            if (m < a.M && nt < a.NT && f0 + e < a.N) h = tanhf(vv[e] * u + bz[f0 + e]) * kWlAct;
+            hi[e] = (_Float16)h;
+            lo[e] = (_Float16)(h - (float)hi[e]);
+        }
+        // feature f0 + e of row m: k-block nt / 2, lane 16 (2 (nt & 1) + q / 2) + n, element 4 (q & 1) + e
+        _Float16* o = reinterpret_cast<_Float16*>(a.out[g]) +
+                      ((((int64_t)sm * a.KBo + (nt >> 1)) * 2) * 64 + 16 * (2 * (nt & 1) + (q >> 1)) + n) * 8 +
+                      4 * (q & 1);
+        typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<h4v*>(o) = h4v{hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<h4v*>(o + 64 * 8) = h4v{lo[0], lo[1], lo[2], lo[3]};
+    }
+}
+
+// ---------------------------------------------------------------------------
 // hidden activations: h = tanh(sum_split P * 2^-s * u_row + b), split at 2^14
 // into the next GEMM's fragments.  One thread per (group, row, 8 features)
 struct WlAct {
@@ -527,6 +662,47 @@ int wl_gemm(const float* const pk[2], const float* const xf[2], float* part, int
     }
 }
 
+// hidden layers' GEMM + activation in one launch (k_wl_gemm_act) up to 64
+// rows; NFK_WL_FUSED=0 selects the split-K GEMM + k_wl_act pair (A/B)
+bool wl_fused(int MT) {
+    static const bool env = [] {
+        const char* e = std::getenv("NFK_WL_FUSED");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return env && MT <= 4;
+}
+
+template <int MT, int PF>
+int wl_gemm_act_launch(const WlGemmAct& a, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wl_gemm_act<MT, PF>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    // (at least 84 KiB: one workgroup per CU, so the grid spreads over every CU)
+    size_t lds = (size_t)4 * 2 * MT * 1024;
+    lds = lds > (size_t)84 * 1024 ? lds : (size_t)84 * 1024;
+    hipLaunchKernelGGL((k_wl_gemm_act<MT, PF>), dim3((unsigned)(2 * a.npair)), dim3(256), lds, st, a);
+    return wl_status("nfk_wide_rnvp: GEMM + activation launch");
+}
+
+int wl_gemm_act(const float* const pk[2], const float* const xf[2], const float* const bias[2], const float* xun,
+                float* const out[2], int N, int K, int M, int MT, hipStream_t st) {
+    WlGemmAct a;
+    for (int g = 0; g < 2; ++g) a.pack[g] = pk[g], a.xf[g] = xf[g], a.bias[g] = bias[g], a.out[g] = out[g];
+    a.xun = xun;
+    a.N = N, a.NT = (N + 15) / 16, a.KB = (K + 31) / 32, a.M = M, a.KBo = (N + 31) / 32;
+    a.npair = (a.NT + 1) / 2;
+    switch (MT) {
+        case 1: return wl_gemm_act_launch<1, 8>(a, st);
+        case 2: return wl_gemm_act_launch<2, 8>(a, st);
+        case 3: return wl_gemm_act_launch<3, 6>(a, st);
+        case 4: return wl_gemm_act_launch<4, 6>(a, st);
+        default: return nfk_set_error("nfk_wide_rnvp: bad row tile count for the fused stage");
+    }
+}
+
 int64_t frag_floats(int MT, int K) { return (int64_t)MT * ((K + 31) / 32) * 512; }
 
 // workspace of one pass of MT sample tiles (floats, each region 16-byte aligned)
@@ -640,7 +816,13 @@ extern "C" int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* pa
             const float* const* bs = biases + 6 * c;
             const int fi = step;  // this coupling's input fragments
             // L1: [M, h] -> [M, H] (s and t), + b1, tanh
-            {
+            if (wl_fused(MT)) {
+                const float* p2[2] = {pk[0], pk[1]};
+                const float* x2[2] = {w.fx[fi], w.fx[fi]};
+                const float* b2[2] = {bs[0], bs[1]};
+                float* o2[2] = {w.fh[0][0], w.fh[0][1]};
+                if (int e = wl_gemm_act(p2, x2, b2, w.fun[fi], o2, H, h, M, MT, st)) return e;
+            } else {
                 const float* p2[2] = {pk[0], pk[1]};
                 const float* x2[2] = {w.fx[fi], w.fx[fi]};
                 if (int e = wl_gemm(p2, x2, w.part, H, h, M, MT, st)) return e;
@@ -654,7 +836,13 @@ extern "C" int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* pa
                 if (int e = wl_status("nfk_wide_rnvp: act launch")) return e;
             }
             // L2: [M, H] -> [M, H], + b2, tanh
-            {
+            if (wl_fused(MT)) {
+                const float* p2[2] = {pk[2], pk[3]};
+                const float* x2[2] = {w.fh[0][0], w.fh[0][1]};
+                const float* b2[2] = {bs[2], bs[3]};
+                float* o2[2] = {w.fh[1][0], w.fh[1][1]};
+                if (int e = wl_gemm_act(p2, x2, b2, nullptr, o2, H, H, M, MT, st)) return e;
+            } else {
                 const float* p2[2] = {pk[2], pk[3]};
                 const float* x2[2] = {w.fh[0][0], w.fh[0][1]};
                 if (int e = wl_gemm(p2, x2, w.part, H, H, M, MT, st)) return e;
