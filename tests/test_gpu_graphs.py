@@ -94,6 +94,24 @@ def test_graphed_replay_after_update_and_eager_call(hip_device):
     flush_status_checks()
 
 
+def test_graphed_stale_after_module_replaced(hip_device):
+    """The staleness test (a C++ watch over the module tree's dicts and the
+    parameters) sees a replaced layer, not only versioned in-place updates."""
+    import copy
+    model = _nsf_model(hip_device, n_layers=2)
+    x = torch.randn(512, 64, generator=torch.Generator(device=hip_device).manual_seed(6), device=hip_device)
+    gl = GraphedLogProb(model, x)
+    gl()
+    assert not gl.stale()
+    model.flows[0] = copy.deepcopy(model.flows[0])
+    assert gl.stale()
+    eager = model.log_prob(x)
+    torch.cuda.synchronize()
+    assert torch.equal(gl().clone(), eager)
+    assert not gl.stale()
+    flush_status_checks()
+
+
 def test_graphed_keeps_captured_packs_alive(hip_device):
     """Writes through ``p.data`` bump no version: after invalidate_caches() and
     an eager call the graph still replays its capture's weights from the packs
@@ -144,16 +162,17 @@ def test_graphed_sample_consistent_with_eager_kernels(hip_device):
     flush_status_checks()
 
 
-@pytest.mark.parametrize("workload", ["c2", "c3", "c5", "ar"])
+@pytest.mark.parametrize("workload", ["c2", "c3", "c5", "ar", "ar354", "fe162", "poly2048", "rnvp2048"])
 def test_graphed_bench_workloads_bitwise(workload, hip_device):
     """bench.py replays log_prob as a graph for per-rank batches <= 2^17 (the
-    8-GPU strong-scaling shard): the replay of every bench workload's model is
+    8-GPU strong-scaling shard, and the applications' 40-row NSF_AR and
+    RealNVP-2048 batches): the replay of every bench workload's model is
     bitwise its eager call (c5 at 512 rows: the wide kernel's shape, not its
     batch, is what the graph must carry)."""
     import bench
     model, _, _ = bench.build_model(workload, hip_device)
     D = bench.WORKLOADS[workload][3]
-    rows = 512 if workload == "c5" else 3000
+    rows = 512 if workload == "c5" else (40 if workload in ("ar354", "fe162", "poly2048", "rnvp2048") else 3000)
     x = torch.randn(rows, D, generator=torch.Generator(device=hip_device).manual_seed(5), device=hip_device)
     gl = GraphedLogProb(model, x)
     out = gl().clone()
