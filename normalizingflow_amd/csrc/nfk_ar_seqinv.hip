@@ -217,6 +217,33 @@ __device__ __forceinline__ float sq_dpp(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float sq_sum2(float v) { return v + sq_dpp<0xB1>(v); }
+// the same over a 32-lane half: the rows by DPP, then one swap of the rows
+__device__ __forceinline__ float sq_max32(float v) {
+    v = fmaxf(v, sq_dpp<0xB1>(v));
+    v = fmaxf(v, sq_dpp<0x4E>(v));
+    v = fmaxf(v, sq_dpp<0x141>(v));
+    v = fmaxf(v, sq_dpp<0x140>(v));
+    return fmaxf(v, __shfl_xor(v, 16, 32));
+}
+__device__ __forceinline__ float sq_sum16(float v);
+__device__ __forceinline__ float sq_sum32(float v) {
+    v = sq_sum16(v);
+    return v + __shfl_xor(v, 16, 32);
+}
+// inclusive prefix sum of ints over each 32-lane half: row_shr 1, 2, 4, 8
+// within each 16-lane row (lanes shifted in from outside the row add 0), then
+// row_bcast:15 carries row 0's (row 2's) total into row 1 (row 3)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int sq_idpp(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, true);
+}
+__device__ __forceinline__ int sq_scan32(int v) {
+    v += sq_idpp<0x111, 0xF>(v);
+    v += sq_idpp<0x112, 0xF>(v);
+    v += sq_idpp<0x114, 0xF>(v);
+    v += sq_idpp<0x118, 0xF>(v);
+    return v + __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+}
 __device__ __forceinline__ float sq_sum16(float v) {
     v += sq_dpp<0xB1>(v);   // quad_perm [1, 0, 3, 2]
     v += sq_dpp<0x4E>(v);   // quad_perm [2, 3, 0, 1]
@@ -227,11 +254,11 @@ __device__ __forceinline__ float sq_sum16(float v) {
 // The spline's inverse for one element on one wave (nfk_rqs_element_lean's
 // algorithm, utils.py:58-152 with the 2B softmax / softplus of flows.py:206-207,
 // spread over lanes): lanes 0-31 take the K width logits, 32-63 the K height
-// logits; max, the two softmax sums (xor butterflies over 32 lanes, every lane
-// the same sum) and the integer knot prefixes (a lane scan: exact, so the
-// knots are those of the sequential prefix) run in parallel, the bin is a
-// ballot count, and every lane then evaluates the same bin.  Every lane of the
-// wave must call it.
+// logits; max, the two softmax sums (DPP within 16-lane rows, then one row
+// swap: every lane the same sum) and the integer knot prefixes (a DPP lane
+// scan: exact, so the knots are those of the sequential prefix) run in
+// parallel, the bin is a ballot count, and every lane then evaluates the same
+// bin.  Every lane of the wave must call it.
 template <int K>
 __device__ __forceinline__ void sq_spline_inv(const float* lg, float x, const NfkSplineConst& c, float& out,
                                               float& lad, bool& inside, bool& neg_disc) {
@@ -244,34 +271,25 @@ __device__ __forceinline__ void sq_spline_inv(const float* lg, float x, const Nf
     const float sp30 = c.span * (1.0f / two30), inv30 = two30 / c.span;
     const float fb30 = c.fw * two30, mb30 = c.min_w * two30;
     const float raw = lg[hb * K + (act ? p : 0)];
-    float mx = act ? raw : -INFINITY;
-#pragma unroll
-    for (int w = 16; w >= 1; w >>= 1) mx = fmaxf(mx, __shfl_xor(mx, w, 32));
+    const float mx = sq_max32(act ? raw : -INFINITY);
     const float mL = mx * kL2E;
     float e = act ? __builtin_amdgcn_exp2f(__builtin_fmaf(raw, kL2E, -mL)) : 0.0f;
-    float s1 = e;
-#pragma unroll
-    for (int w = 16; w >= 1; w >>= 1) s1 += __shfl_xor(s1, w, 32);
+    const float s1 = sq_sum32(e);
     const float q = c.m2b * __builtin_amdgcn_rcpf(s1);
     e = act ? __builtin_amdgcn_exp2f(__builtin_fmaf(e, q, -c.m2b)) : 0.0f;
-    float s2 = e;
-#pragma unroll
-    for (int w = 16; w >= 1; w >>= 1) s2 += __shfl_xor(s2, w, 32);
+    const float s2 = sq_sum32(e);
     const float f30 = fb30 * __builtin_amdgcn_rcpf(s2);
     const int v = p < K - 1 ? (int)__builtin_fmaf(e, f30, mb30) : 0;
-    int sc = v;
-#pragma unroll
-    for (int w = 1; w < 32; w <<= 1) {
-        const int t = __shfl_up(sc, w, 32);
-        sc += p >= w ? t : 0;
-    }
-    const int pre = sc - v;  // knot p's integer position (pre[0] = 0)
-    const float s2w = __shfl(s2, 0), s2h = __shfl(s2, 32);
+    const int pre = sq_scan32(v) - v;  // knot p's integer position (pre[0] = 0)
+    // (wave-uniform values by v_readlane: no LDS round trips)
+    const float s2w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s2), 0));
+    const float s2h = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s2), 32));
     // the bin: how many inner height knots x has passed
     const int xi = __float2int_rd(__builtin_fmaf(x, inv30, -c.lo * inv30));
     const int k = __popcll(__ballot(hb == 1 && p >= 1 && p < K && xi >= pre));
     const int k1 = k + 1 < K ? k + 1 : 0;
-    const int pw0 = __shfl(pre, k), pw1 = __shfl(pre, k1), ph0 = __shfl(pre, 32 + k), ph1 = __shfl(pre, 32 + k1);
+    const int pw0 = __builtin_amdgcn_readlane(pre, k), pw1 = __builtin_amdgcn_readlane(pre, k1);
+    const int ph0 = __builtin_amdgcn_readlane(pre, 32 + k), ph1 = __builtin_amdgcn_readlane(pre, 32 + k1);
     const float low = __builtin_fmaf(s2w, 0.0f, c.lo), loh = __builtin_fmaf(s2h, 0.0f, c.lo);
     const float cw_k = __builtin_fmaf(sp30, (float)pw0, low);
     const float w_k = ((k == K - 1) ? c.hi : __builtin_fmaf(sp30, (float)pw1, low)) - cw_k;
