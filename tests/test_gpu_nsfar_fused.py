@@ -534,6 +534,40 @@ def test_ar_seqinv_vs_oracle(dim, K, rows, hip_device):
     assert int(st[dim // 3]) & 1 and all(int(v) & 1 for v in st.cpu())  # NFK_ST_INSIDE_SEEN in every column
 
 
+@pytest.mark.parametrize("dim,K,H,rows", [(20, 8, 16, 33), (37, 10, 37, 70), (70, 4, 128, 64), (12, 16, 64, 5)])
+def test_ar_seqinv_shapes_vs_oracle(dim, K, H, rows, hip_device):
+    """nfk_ar_seqinv over its supported range, called directly with the
+    layer's own Linear pointers: hidden widths 16 / 37 (not a multiple of 4:
+    the element-wise weight loads) / 64 / 128 (the maximum), K 4 / 8 / 10 / 16,
+    against the oracle's inverse; one and two 64-row passes."""
+    import ctypes
+    assert K_.ar_seqinv_supported(dim, H, K)
+    torch.manual_seed(1000 + dim + H)
+    layer = nff.NSF_AR(dim=dim, K=K, B=1.5, hidden_dim=H)
+    sd = _sd(layer)
+    layer = layer.to(hip_device)
+    z = torch.randn(rows, dim, generator=torch.Generator().manual_seed(rows + H)) * 0.7
+    xi_ref, ldi_ref, _, ldi64 = _oracle_ar(z, sd, dim, K, 1.5, inverse=True)
+    flat = [t.detach().contiguous() for m in layer._stock_linears() for t in (m.weight, m.bias)]
+    assert len(flat) == 6 * (dim - 1)
+    ptrs = (ctypes.c_void_p * len(flat))(*[t.data_ptr() for t in flat])
+    zd = z.to(hip_device)
+    out = torch.empty_like(zd)
+    ld = torch.zeros(rows, device=hip_device)
+    st = torch.zeros(dim, dtype=torch.int32, device=hip_device)
+    with torch.no_grad():
+        K_.ar_seqinv(zd, ptrs, layer.init_param.detach().contiguous(), dim, H, K, 1.5, out, logdet=ld,
+                     logdet_mode=1, status=st)
+        out2 = torch.empty_like(zd)
+        K_.ar_seqinv(zd, ptrs, layer.init_param.detach().contiguous(), dim, H, K, 1.5, out2, logdet=None,
+                     logdet_mode=0)
+    torch.cuda.synchronize()
+    close(out, xi_ref, 1e-5, 1e-4)
+    close_or_on_par(ld, ldi_ref, ldi64, LD_RTOL, LD_ATOL)
+    assert torch.equal(out, out2)
+    assert all(int(v) & 1 for v in st.cpu())
+
+
 def test_polymer2048_inverse_speed(hip_device):
     """Polymer.yaml's layer inverted at the 40-row batch: the library-driven
     column loop (nfk_ar_seqinv) bitwise-run-to-run, close to the per-column host
