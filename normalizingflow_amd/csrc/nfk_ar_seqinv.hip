@@ -26,10 +26,11 @@
 //                           columns read into each XCD's L2 for the next launch
 //
 // The conditioners' nn.Linear weights are read in place (fp32; a host table of
-// their device pointers, passed to each launch as arguments), and the arithmetic is fp32 FMA
-// throughout: the inverse is latency-bound (4,095 dependent launches per layer
-// at Polymer's shape), not bandwidth- or FLOP-bound, and every weight is read
-// once per layer (1.68 GB at Polymer, 0.2 ms of HBM time).
+// their device pointers, passed to each launch as arguments), and the
+// arithmetic is fp32 FMA throughout: the inverse is latency-bound (2,048
+// dependent launches per layer at Polymer's shape, ~7.3 us each), not
+// bandwidth- or FLOP-bound, and every weight is read once per layer (1.68 GB
+// at Polymer, 0.2 ms of HBM time).
 #include <hip/hip_runtime.h>
 
 #include <cmath>

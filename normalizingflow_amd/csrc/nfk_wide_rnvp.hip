@@ -14,6 +14,8 @@
 //   k_wl_act    sum the partials, unscale, + b1, tanh -> hi/lo fragments (2^14)
 //   k_wl_gemm   L2: [M, H] x W2^T (s, t)              -> partials
 //   k_wl_act    + b2, tanh                             -> fragments
+//   (up to 64 rows each GEMM + act pair is ONE k_wl_gemm_act launch: 9
+//   launches per layer instead of 13)
 //   k_wl_gemm   L3: [M, H] x W3^T (s, t)              -> partials
 //   k_wl_rows   s, t = partials + b3; the affine coupling (flows.py:56, 59 /
 //               69, 72), log|det| += (-)sum s per row (fixed order), and the
