@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 6 (x): one-wave workgroups for the wide NSF_AR inverse at sampling batches
+# (NFK_AR_INV_WAVES and the one-wave inverse it selected were measured slower and removed; profiles/r6/r6x_ar_inverse_waves_ab.txt)
 set -u
 O=gpurun_out/r6x; mkdir -p $O
 export TMPDIR=/tmp
