@@ -158,7 +158,7 @@ ARITH = {
     "fe162": _SPLIT + "; the 2 tail features of H=354 as one 16x16x16 f16 MFMA per tile"
              " (nfk_fused_ar.hip, one wave per SIMD; layer 1 on the fp16-split trig features)",
     "poly2048": _SPLIT + _TAIL + " (nfk_fused_ar.hip; layer 1 on the fp16-split trig features)",
-    "rnvp2048": _SPLIT + " (nfk_wide_rnvp.hip: split-K weight-stream GEMMs, fp32 partial sums added in split order)",
+    "rnvp2048": _SPLIT + " (nfk_wide_rnvp.hip: weight-stream GEMMs, the hidden layers' GEMM + tanh fused up to 64 rows, the output layer split-K with fp32 partial sums added in split order; the 10 layers in one nfk_wide_rnvp_chain call)",
 }
 # the line's dtype: what the path computes in (fp32 values and outputs; the
 # conditioner's products on the fp16 matrix cores as a two-way split)
@@ -494,19 +494,21 @@ def roofline(workload, timer_summary, per_gpu_batch, traffic, n_steps):
         return out
     if name == "nfk_fused_ar":
         return roofline_ar(kw, B, L * n_steps / n_launch, n_launch, mean_ms, traffic, insts)
-    if name == "nfk_wide_rnvp":
-        # one layer per launch: its four FCNNs' weights read once (fp16 hi + lo:
-        # 4 B per weight, the fp32 bytes) + x in, z out, log|det| RMW
+    if name in ("nfk_wide_rnvp", "nfk_wide_rnvp_chain"):
+        # nl layers per launch (the chain: the model's whole run of them), each
+        # layer's four FCNNs' weights read once (fp16 hi + lo: 4 B per weight,
+        # the fp32 bytes) + x in, z out, log|det| RMW
+        nl = max(1, int(round(L * n_steps / n_launch)))
         D2, H = kw["dim"] // 2, kw["hidden_dim"]
         wts = 4 * 4 * (D2 * H + H + H * H + H + H * D2 + D2)
-        byts = wts + (2 * kw["dim"] * 4 + 8) * B
+        byts = nl * wts + (2 * kw["dim"] * 4 + 8) * B
         achieved = byts / (mean_ms * 1e-3) / 1e9
         return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                 **hbm_fields(traffic, byts, mean_ms), "launches": n_launch, "mean_ms": round(mean_ms, 4),
                 "floor_ms": round(byts / (PEAK_HBM_GBS * 1e9) * 1e3, 4),
-                "per_launch": "%d samples x 1 layer: %d B algorithmic (the layer's weights once + x, z, "
-                              "log|det|; the kernel streams them once per 128-row pass)" % (B, byts)}
+                "per_launch": "%d samples x %d layer(s): %d B algorithmic (each layer's weights once + x, z, "
+                              "log|det|; streamed once per 128-row pass)" % (B, nl, byts)}
     if name == "nfk_rqs_coupling" and kind == "NSF_AR":
         P = 3 * kw["K"] - 1
         byts = (4 + P * 4 + 4 + 8) * B                            # one column: x, params, z, log|det| RMW

@@ -511,6 +511,18 @@ int64_t nfk_wide_rnvp_workspace(int32_t half, int32_t hidden, int64_t batch);
 int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const float* const* biases, int32_t half,
                   int32_t hidden, float* z, int64_t ldz, float* logdet, int32_t logdet_mode, int64_t batch,
                   int32_t inverse, float* workspace, int64_t workspace_floats, nfk_stream_t stream);
+/* nfk_wide_rnvp_chain: nlayers consecutive such layers in ONE call (the
+ * model's layer loop, nf/models.py:13-29 / 22-35, over RealNVP layers of one
+ * shape): packs / biases hold 12 pointers per layer in EXECUTION order (the
+ * inverse's caller passes the layers last to first).  Bitwise the per-layer
+ * calls; the last half-coupling of each layer also writes the next layer's
+ * input fragments, so only the first layer converts x.  workspace:
+ * nfk_wide_rnvp_chain_workspace(half, hidden, batch) floats. */
+int64_t nfk_wide_rnvp_chain_workspace(int32_t half, int32_t hidden, int64_t batch);
+int nfk_wide_rnvp_chain(const float* x, int64_t ldx, const float* const* packs, const float* const* biases,
+                        int32_t nlayers, int32_t half, int32_t hidden, float* z, int64_t ldz, float* logdet,
+                        int32_t logdet_mode, int64_t batch, int32_t inverse, float* workspace,
+                        int64_t workspace_floats, nfk_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * NSF_AR inverse for the layers the fused kernel's inverse does not take

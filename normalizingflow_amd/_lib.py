@@ -128,6 +128,8 @@ SIGNATURES = {
     "nfk_wide_rnvp_supported": (ctypes.c_int, [I32, I32]),
     "nfk_wide_rnvp_workspace": (ctypes.c_int64, [I32, I32, I64]),
     "nfk_wide_rnvp": (ctypes.c_int, [P, I64, P, P, I32, I32, P, I64, P, I32, I64, I32, P, I64, P]),
+    "nfk_wide_rnvp_chain_workspace": (ctypes.c_int64, [I32, I32, I64]),
+    "nfk_wide_rnvp_chain": (ctypes.c_int, [P, I64, P, P, I32, I32, I32, P, I64, P, I32, I64, I32, P, I64, P]),
     "nfk_ar_seqinv_supported": (ctypes.c_int, [I32, I32, I32]),
     "nfk_ar_seqinv_workspace": (ctypes.c_int64, [I32, I32, I32, I64]),
     "nfk_ar_seqinv": (ctypes.c_int, [P, I64, P, P, I32, I32, I32, ctypes.c_double, P, I64, P, I32, I64, P, P, I64,

@@ -774,111 +774,167 @@ extern "C" int64_t nfk_wide_rnvp_workspace(int32_t half, int32_t hidden, int64_t
     return wl_ws(nullptr, half, hidden, (int)(mt < kWlMaxMT ? mt : kWlMaxMT)).total;
 }
 
-extern "C" int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const float* const* biases,
-                             int32_t half, int32_t hidden, float* z, int64_t ldz, float* logdet, int32_t logdet_mode,
-                             int64_t batch, int32_t inverse, float* workspace, int64_t workspace_floats,
-                             nfk_stream_t stream) {
-    if (!nfk_wide_rnvp_supported(half, hidden)) return nfk_set_error("nfk_wide_rnvp: shape not supported");
-    if (batch < 0) return nfk_set_error("nfk_wide_rnvp: bad batch");
-    if (batch == 0) return 0;
-    if (!x || !packs || !biases || !z || !workspace) return nfk_set_error("nfk_wide_rnvp: null pointer");
-    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_wide_rnvp: null logdet");
-    if (ldx < 2 * half || ldz < 2 * half) return nfk_set_error("nfk_wide_rnvp: bad leading dimension");
-    if (workspace_floats < nfk_wide_rnvp_workspace(half, hidden, batch))
-        return nfk_set_error("nfk_wide_rnvp: workspace too small (nfk_wide_rnvp_workspace)");
-    for (int i = 0; i < 12; ++i)
-        if (!packs[i] || !biases[i]) return nfk_set_error("nfk_wide_rnvp: null pack or bias");
-    hipStream_t st = (hipStream_t)stream;
-    const int h = half, H = hidden;
-    // half-couplings in execution order: forward 1 then 2, inverse 2 then 1.
-    // Coupling c (0 = s1/t1: reads the lower half, changes the upper; 1 =
-    // s2/t2: reads the upper, changes the lower), packs [6 c + 2 layer + group]
+namespace {
+
+// nl layers in execution order (packs / biases: 12 per layer), each layer's
+// half-couplings in its direction.  Within a row block the layers run back to
+// back: layer l reads the previous layer's output rows (ping-ponged through
+// tmp, the last layer writing z), and the last coupling of every layer but
+// the last also writes the fragments of its output half -- the next layer's
+// first conditioner input -- so only the first layer converts x (no per-layer
+// k_wl_rows prep launch).
+int wl_layers(const float* x, int64_t ldx, const float* const* packs, const float* const* biases, int nl, int h,
+              int H, float* z, int64_t ldz, float* logdet, int logdet_mode, int64_t batch, bool inverse,
+              float* workspace, float* tmp, hipStream_t st) {
     for (int64_t r0 = 0; r0 < batch; r0 += 16 * kWlMaxMT) {
         const int M = (int)(batch - r0 < 16 * kWlMaxMT ? batch - r0 : 16 * kWlMaxMT);
         const int MT = (M + 15) / 16;
         const WlWs w = wl_ws(workspace, h, H, MT);
-        const float* xr = x + r0 * ldx;
-        float* zr = z + r0 * ldz;
         float* ldr = logdet_mode != 0 ? logdet + r0 : nullptr;
         const int first = inverse ? 1 : 0;
-        // the first conditioner's input: x's lower half (forward) or upper (inverse)
-        {
-            WlRows a{};
-            a.xin = xr + (first == 0 ? 0 : h);
-            a.ldin = ldx;
-            a.frag = w.fx[0];
-            a.frag_un = w.fun[0];
-            a.h = h, a.M = M, a.MT = MT, a.KBf = (h + 31) / 32;
-            hipLaunchKernelGGL(k_wl_rows, dim3(16 * MT), dim3(kRowThreads), (size_t)h * sizeof(float), st, a);
-            if (int e = wl_status("nfk_wide_rnvp: rows launch")) return e;
-        }
-        for (int step = 0; step < 2; ++step) {
-            const int c = inverse ? 1 - step : step;
-            const float* const* pk = packs + 6 * c;
-            const float* const* bs = biases + 6 * c;
-            const int fi = step;  // this coupling's input fragments
-            // L1: [M, h] -> [M, H] (s and t), + b1, tanh
-            if (wl_fused(MT)) {
-                const float* p2[2] = {pk[0], pk[1]};
-                const float* x2[2] = {w.fx[fi], w.fx[fi]};
-                const float* b2[2] = {bs[0], bs[1]};
-                float* o2[2] = {w.fh[0][0], w.fh[0][1]};
-                if (int e = wl_gemm_act(p2, x2, b2, w.fun[fi], o2, H, h, M, MT, st)) return e;
+        for (int l = 0; l < nl; ++l) {
+            // layer l's input and output rows of this block
+            const float* xr;
+            int64_t ldxr;
+            if (l == 0) {
+                xr = x + r0 * ldx, ldxr = ldx;
             } else {
-                const float* p2[2] = {pk[0], pk[1]};
-                const float* x2[2] = {w.fx[fi], w.fx[fi]};
-                if (int e = wl_gemm(p2, x2, w.part, H, h, M, MT, st)) return e;
-                const WlPlan p = wl_plan(H, (h + 31) / 32, MT);
-                WlAct a{};
-                a.part = w.part, a.pack[0] = pk[0], a.pack[1] = pk[1], a.bias[0] = bs[0], a.bias[1] = bs[1];
-                a.xun = w.fun[fi], a.out[0] = w.fh[0][0], a.out[1] = w.fh[0][1];
-                a.N = H, a.KS = p.KS, a.M = M, a.MT = MT, a.KBo = (H + 31) / 32;
-                const int64_t n = 2LL * MT * a.KBo * 64;
-                hipLaunchKernelGGL(k_wl_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
-                if (int e = wl_status("nfk_wide_rnvp: act launch")) return e;
+                const bool prev_z = ((nl - 1 - (l - 1)) & 1) == 0;
+                xr = prev_z ? z + r0 * ldz : tmp, ldxr = prev_z ? ldz : 2 * h;
             }
-            // L2: [M, H] -> [M, H], + b2, tanh
-            if (wl_fused(MT)) {
-                const float* p2[2] = {pk[2], pk[3]};
-                const float* x2[2] = {w.fh[0][0], w.fh[0][1]};
-                const float* b2[2] = {bs[2], bs[3]};
-                float* o2[2] = {w.fh[1][0], w.fh[1][1]};
-                if (int e = wl_gemm_act(p2, x2, b2, nullptr, o2, H, H, M, MT, st)) return e;
-            } else {
-                const float* p2[2] = {pk[2], pk[3]};
-                const float* x2[2] = {w.fh[0][0], w.fh[0][1]};
-                if (int e = wl_gemm(p2, x2, w.part, H, H, M, MT, st)) return e;
-                const WlPlan p = wl_plan(H, (H + 31) / 32, MT);
-                WlAct a{};
-                a.part = w.part, a.pack[0] = pk[2], a.pack[1] = pk[3], a.bias[0] = bs[2], a.bias[1] = bs[3];
-                a.xun = nullptr, a.out[0] = w.fh[1][0], a.out[1] = w.fh[1][1];
-                a.N = H, a.KS = p.KS, a.M = M, a.MT = MT, a.KBo = (H + 31) / 32;
-                const int64_t n = 2LL * MT * a.KBo * 64;
-                hipLaunchKernelGGL(k_wl_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
-                if (int e = wl_status("nfk_wide_rnvp: act launch")) return e;
-            }
-            // L3: [M, H] -> [M, h] (s, t), + b3; the coupling of the other half
-            {
-                const float* p2[2] = {pk[4], pk[5]};
-                const float* x2[2] = {w.fh[1][0], w.fh[1][1]};
-                if (int e = wl_gemm(p2, x2, w.part, h, H, M, MT, st)) return e;
-                const WlPlan p = wl_plan(h, (H + 31) / 32, MT);
-                const int col = c == 0 ? h : 0;  // the half this coupling changes
+            const bool out_z = ((nl - 1 - l) & 1) == 0;
+            float* zr = out_z ? z + r0 * ldz : tmp;
+            const int64_t ldzr = out_z ? ldz : 2 * h;
+            const float* const* lp = packs + 12 * l;
+            const float* const* lb = biases + 12 * l;
+            if (l == 0) {
+                // the first conditioner's input: x's lower half (forward) or upper (inverse)
                 WlRows a{};
-                a.part = w.part, a.pack[0] = pk[4], a.pack[1] = pk[5], a.bias[0] = bs[4], a.bias[1] = bs[5];
-                a.xin = xr + col, a.ldin = ldx, a.out = zr + col, a.ldo = ldz;
-                a.logdet = ldr;
-                a.mode = ldr == nullptr ? 0 : (step == 0 ? logdet_mode : 2);
-                a.inverse = inverse ? 1 : 0;
-                // the first coupling's output is the second one's input
-                a.frag = step == 0 ? w.fx[1] : nullptr;
-                a.frag_un = step == 0 ? w.fun[1] : nullptr;
-                a.h = h, a.KS = p.KS, a.M = M, a.MT = MT, a.KBf = (h + 31) / 32;
-                hipLaunchKernelGGL(k_wl_rows, dim3(16 * MT), dim3(kRowThreads),
-                                   step == 0 ? (size_t)h * sizeof(float) : 0, st, a);
-                if (int e = wl_status("nfk_wide_rnvp: coupling launch")) return e;
+                a.xin = xr + (first == 0 ? 0 : h);
+                a.ldin = ldxr;
+                a.frag = w.fx[0];
+                a.frag_un = w.fun[0];
+                a.h = h, a.M = M, a.MT = MT, a.KBf = (h + 31) / 32;
+                hipLaunchKernelGGL(k_wl_rows, dim3(16 * MT), dim3(kRowThreads), (size_t)h * sizeof(float), st, a);
+                if (int e = wl_status("nfk_wide_rnvp: rows launch")) return e;
+            }
+            for (int step = 0; step < 2; ++step) {
+                const int c = inverse ? 1 - step : step;
+                const float* const* pk = lp + 6 * c;
+                const float* const* bs = lb + 6 * c;
+                const int fi = step;  // this coupling's input fragments
+                // L1: [M, h] -> [M, H] (s and t), + b1, tanh
+                if (wl_fused(MT)) {
+                    const float* p2[2] = {pk[0], pk[1]};
+                    const float* x2[2] = {w.fx[fi], w.fx[fi]};
+                    const float* b2[2] = {bs[0], bs[1]};
+                    float* o2[2] = {w.fh[0][0], w.fh[0][1]};
+                    if (int e = wl_gemm_act(p2, x2, b2, w.fun[fi], o2, H, h, M, MT, st)) return e;
+                } else {
+                    const float* p2[2] = {pk[0], pk[1]};
+                    const float* x2[2] = {w.fx[fi], w.fx[fi]};
+                    if (int e = wl_gemm(p2, x2, w.part, H, h, M, MT, st)) return e;
+                    const WlPlan p = wl_plan(H, (h + 31) / 32, MT);
+                    WlAct a{};
+                    a.part = w.part, a.pack[0] = pk[0], a.pack[1] = pk[1], a.bias[0] = bs[0], a.bias[1] = bs[1];
+                    a.xun = w.fun[fi], a.out[0] = w.fh[0][0], a.out[1] = w.fh[0][1];
+                    a.N = H, a.KS = p.KS, a.M = M, a.MT = MT, a.KBo = (H + 31) / 32;
+                    const int64_t n = 2LL * MT * a.KBo * 64;
+                    hipLaunchKernelGGL(k_wl_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+                    if (int e = wl_status("nfk_wide_rnvp: act launch")) return e;
+                }
+                // L2: [M, H] -> [M, H], + b2, tanh
+                if (wl_fused(MT)) {
+                    const float* p2[2] = {pk[2], pk[3]};
+                    const float* x2[2] = {w.fh[0][0], w.fh[0][1]};
+                    const float* b2[2] = {bs[2], bs[3]};
+                    float* o2[2] = {w.fh[1][0], w.fh[1][1]};
+                    if (int e = wl_gemm_act(p2, x2, b2, nullptr, o2, H, H, M, MT, st)) return e;
+                } else {
+                    const float* p2[2] = {pk[2], pk[3]};
+                    const float* x2[2] = {w.fh[0][0], w.fh[0][1]};
+                    if (int e = wl_gemm(p2, x2, w.part, H, H, M, MT, st)) return e;
+                    const WlPlan p = wl_plan(H, (H + 31) / 32, MT);
+                    WlAct a{};
+                    a.part = w.part, a.pack[0] = pk[2], a.pack[1] = pk[3], a.bias[0] = bs[2], a.bias[1] = bs[3];
+                    a.xun = nullptr, a.out[0] = w.fh[1][0], a.out[1] = w.fh[1][1];
+                    a.N = H, a.KS = p.KS, a.M = M, a.MT = MT, a.KBo = (H + 31) / 32;
+                    const int64_t n = 2LL * MT * a.KBo * 64;
+                    hipLaunchKernelGGL(k_wl_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+                    if (int e = wl_status("nfk_wide_rnvp: act launch")) return e;
+                }
+                // L3: [M, H] -> [M, h] (s, t), + b3; the coupling of the other half
+                {
+                    const float* p2[2] = {pk[4], pk[5]};
+                    const float* x2[2] = {w.fh[1][0], w.fh[1][1]};
+                    if (int e = wl_gemm(p2, x2, w.part, h, H, M, MT, st)) return e;
+                    const WlPlan p = wl_plan(h, (H + 31) / 32, MT);
+                    const int col = c == 0 ? h : 0;  // the half this coupling changes
+                    WlRows a{};
+                    a.part = w.part, a.pack[0] = pk[4], a.pack[1] = pk[5], a.bias[0] = bs[4], a.bias[1] = bs[5];
+                    a.xin = xr + col, a.ldin = ldxr, a.out = zr + col, a.ldo = ldzr;
+                    a.logdet = ldr;
+                    a.mode = ldr == nullptr ? 0 : (step == 0 && l == 0 ? logdet_mode : 2);
+                    a.inverse = inverse ? 1 : 0;
+                    // the first coupling's output is the second one's input; the
+                    // second's, the next layer's first input
+                    const bool fr = step == 0 || l + 1 < nl;
+                    a.frag = step == 0 ? w.fx[1] : (fr ? w.fx[0] : nullptr);
+                    a.frag_un = step == 0 ? w.fun[1] : (fr ? w.fun[0] : nullptr);
+                    a.h = h, a.KS = p.KS, a.M = M, a.MT = MT, a.KBf = (h + 31) / 32;
+                    hipLaunchKernelGGL(k_wl_rows, dim3(16 * MT), dim3(kRowThreads), fr ? (size_t)h * sizeof(float) : 0,
+                                       st, a);
+                    if (int e = wl_status("nfk_wide_rnvp: coupling launch")) return e;
+                }
             }
         }
     }
     return 0;
+}
+
+int wl_check(int32_t half, int32_t hidden, int64_t batch, const float* x, const float* const* packs,
+             const float* const* biases, int nl, float* z, float* logdet, int32_t logdet_mode, int64_t ldx,
+             int64_t ldz, const float* workspace) {
+    if (!nfk_wide_rnvp_supported(half, hidden)) return nfk_set_error("nfk_wide_rnvp: shape not supported");
+    if (batch < 0 || nl < 1) return nfk_set_error("nfk_wide_rnvp: bad batch or layer count");
+    if (!x || !packs || !biases || !z || !workspace) return nfk_set_error("nfk_wide_rnvp: null pointer");
+    if (logdet_mode != 0 && !logdet) return nfk_set_error("nfk_wide_rnvp: null logdet");
+    if (ldx < 2 * half || ldz < 2 * half) return nfk_set_error("nfk_wide_rnvp: bad leading dimension");
+    for (int i = 0; i < 12 * nl; ++i)
+        if (!packs[i] || !biases[i]) return nfk_set_error("nfk_wide_rnvp: null pack or bias");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int nfk_wide_rnvp(const float* x, int64_t ldx, const float* const* packs, const float* const* biases,
+                             int32_t half, int32_t hidden, float* z, int64_t ldz, float* logdet, int32_t logdet_mode,
+                             int64_t batch, int32_t inverse, float* workspace, int64_t workspace_floats,
+                             nfk_stream_t stream) {
+    if (int e = wl_check(half, hidden, batch, x, packs, biases, 1, z, logdet, logdet_mode, ldx, ldz, workspace))
+        return e;
+    if (batch == 0) return 0;
+    if (workspace_floats < nfk_wide_rnvp_workspace(half, hidden, batch))
+        return nfk_set_error("nfk_wide_rnvp: workspace too small (nfk_wide_rnvp_workspace)");
+    return wl_layers(x, ldx, packs, biases, 1, half, hidden, z, ldz, logdet, logdet_mode, batch, inverse != 0,
+                     workspace, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int64_t nfk_wide_rnvp_chain_workspace(int32_t half, int32_t hidden, int64_t batch) {
+    const int64_t w = nfk_wide_rnvp_workspace(half, hidden, batch);
+    return w == 0 ? 0 : w + (int64_t)16 * kWlMaxMT * 2 * half;  // + one row block's ping-pong rows
+}
+
+extern "C" int nfk_wide_rnvp_chain(const float* x, int64_t ldx, const float* const* packs, const float* const* biases,
+                                   int32_t nlayers, int32_t half, int32_t hidden, float* z, int64_t ldz, float* logdet,
+                                   int32_t logdet_mode, int64_t batch, int32_t inverse, float* workspace,
+                                   int64_t workspace_floats, nfk_stream_t stream) {
+    if (int e = wl_check(half, hidden, batch, x, packs, biases, nlayers, z, logdet, logdet_mode, ldx, ldz, workspace))
+        return e;
+    if (batch == 0) return 0;
+    if (workspace_floats < nfk_wide_rnvp_chain_workspace(half, hidden, batch))
+        return nfk_set_error("nfk_wide_rnvp_chain: workspace too small (nfk_wide_rnvp_chain_workspace)");
+    float* tmp = workspace + nfk_wide_rnvp_workspace(half, hidden, batch);
+    return wl_layers(x, ldx, packs, biases, nlayers, half, hidden, z, ldz, logdet, logdet_mode, batch, inverse != 0,
+                     workspace, tmp, (hipStream_t)stream);
 }

@@ -814,6 +814,47 @@ def wide_rnvp(x, wp, z, *, logdet, logdet_mode, inverse=False):
            _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, ws.data_ptr(), nws, _stream(dev))
 
 
+class WideRnvpChain:
+    """Host pointer tables of a run of WideRnvpPacks in execution order (12
+    packs and 12 biases per layer) for wide_rnvp_chain; built once per run."""
+
+    def __init__(self, wps):
+        if not wps or any(w.half != wps[0].half or w.hidden != wps[0].hidden or w.device != wps[0].device
+                          for w in wps):
+            raise ValueError("wide_rnvp_chain: layers of one shape and device")
+        self.wps, self.n = list(wps), len(wps)
+        self.half, self.hidden, self.device = wps[0].half, wps[0].hidden, wps[0].device
+        self._pk = (ctypes.c_void_p * (12 * self.n))(*[t.data_ptr() for w in wps for t in w.packs])
+        self._bs = (ctypes.c_void_p * (12 * self.n))(*[t.data_ptr() for w in wps for t in w.biases])
+        self.pk, self.bs = ctypes.addressof(self._pk), ctypes.addressof(self._bs)
+        self._ws = {}
+
+    def workspace_floats(self, batch):
+        n = self._ws.get(batch)
+        if n is None:
+            n = self._ws[batch] = int(_lib.load().nfk_wide_rnvp_chain_workspace(self.half, self.hidden, batch))
+        return n
+
+
+def wide_rnvp_chain(x, chain, z, *, logdet, logdet_mode, inverse=False):
+    """``chain.n`` RealNVP layers through the weight stream in one call
+    (include/nfk.h nfk_wide_rnvp_chain), bitwise the per-layer wide_rnvp
+    calls; ``chain`` a WideRnvpChain in execution order."""
+    dev = _require_hip(x, z, logdet)
+    if dev != chain.device:
+        raise RuntimeError("wide_rnvp_chain: x on %s, the packs on %s" % (dev, chain.device))
+    B = x.shape[0]
+    xp, ldx = _mat(x, "x")
+    zp, ldz = _mat(z, "z")
+    if x.shape[1] != 2 * chain.half or z.shape != x.shape:
+        raise ValueError("wide_rnvp_chain: x and z must be [B, %d]" % (2 * chain.half))
+    nws = chain.workspace_floats(B)
+    ws = torch.empty(max(nws, 4), dtype=F32, device=dev)
+    _timed("nfk_wide_rnvp_chain", dev, "nfk_wide_rnvp_chain", xp, ldx, chain.pk, chain.bs, chain.n, chain.half,
+           chain.hidden, zp, ldz, _vec(logdet, B, "logdet"), logdet_mode, B, 1 if inverse else 0, ws.data_ptr(), nws,
+           _stream(dev))
+
+
 # ---- NSF_AR inverse, column by column from the library (nfk_ar_seqinv.hip)
 def ar_seqinv_supported(dim, hidden, K):
     return bool(_lib.load().nfk_ar_seqinv_supported(dim, hidden, K))

@@ -231,7 +231,7 @@ class NormalizingFlowModel(nn.Module):
         off = 0
         flows = self.flows[::-1] if inverse else self.flows
         with torch.set_grad_enabled(grad):
-            for item in self._groups(flows, x.device, grad, inverse):
+            for item in self._groups(flows, x.device, grad, inverse, batch=m):
                 if isinstance(item, tuple):  # a run of fused NSF_CL or RealNVP layers: one launch
                     run, shape = item
                     k = sum(f._n_status for f in run)
@@ -271,7 +271,11 @@ class NormalizingFlowModel(nn.Module):
     def _is_rnvp(shape):
         return shape[0] == "rnvp"
 
-    def _groups(self, flows, device, grad, inverse=False):
+    @staticmethod
+    def _is_wide(shape):
+        return shape[0] == "wide"
+
+    def _groups(self, flows, device, grad, inverse=False, batch=None):
         """The layer sequence with every run of consecutive NSF_CL layers (or of
         RealNVP layers) that share one fused-kernel shape replaced by (run,
         shape) tuples of at most nfk_fused_nsf_chain_max /
@@ -280,7 +284,10 @@ class NormalizingFlowModel(nn.Module):
         half-dimension the kernel does not take runs zero-padded to one it
         does (RealNVP._fused_half).  Under autograd (``grad``) only NSF_CL runs
         in the forward direction that nfk_fused_nsf_chain_saved takes are
-        grouped (config.USE_TRAIN_CHAIN; _ChainFn)."""
+        grouped (config.USE_TRAIN_CHAIN; _ChainFn).  With ``batch``, runs of
+        RealNVP layers that take the weight-stream form at that batch
+        (RealNVP._wide_pack: Polymer_rnvp's width) group as ("wide", half,
+        hidden): one nfk_wide_rnvp_chain call."""
         if not (config.USE_FUSED and config.USE_CHAIN):
             return list(flows)
         if grad and (inverse or not config.USE_TRAIN_CHAIN):
@@ -290,6 +297,8 @@ class NormalizingFlowModel(nn.Module):
         def flush():
             if shape is None:
                 nmax = 0
+            elif self._is_wide(shape):
+                nmax = len(run)
             elif self._is_rnvp(shape):
                 nmax = K_.fused_realnvp_chain_max(shape[1], shape[2])
             else:
@@ -309,6 +318,9 @@ class NormalizingFlowModel(nn.Module):
         kinds = (NSF_CL,) if grad else (NSF_CL, RealNVP)
         for flow in flows:
             sh = flow._chain_shape(device) if isinstance(flow, kinds) else None
+            if sh is None and batch is not None and not grad and isinstance(flow, RealNVP):
+                wp = flow._wide_pack(device, batch)
+                sh = ("wide", wp.half, wp.hidden) if wp is not None else None
             if sh is not None and sh == shape:
                 run.append(flow)
                 continue
@@ -430,6 +442,19 @@ class NormalizingFlowModel(nn.Module):
         return 2 * shape[3] if cls._is_rnvp(shape) else shape[0] + shape[1]
 
     def _run_chain(self, run, shape, x, inverse, logdet, status):
+        if self._is_wide(shape):
+            # consecutive weight-stream RealNVP layers: one call (the packs were
+            # validated by _wide_pack while grouping; the host pointer tables
+            # are kept per run and rebuilt when any layer's pack changed)
+            wps = tuple(f._wide_pack(x.device, x.shape[0]) for f in run)
+            key = ("wide", tuple(id(f) for f in run), str(x.device))
+            ent = self._chain_cache.get(key)
+            if ent is None or len(ent[0]) != len(wps) or any(a is not b for a, b in zip(ent[0], wps)):
+                ent = self._chain_cache[key] = (wps, K_.WideRnvpChain(list(wps)))
+            xc = x if x.stride(1) == 1 else x.contiguous()
+            z = torch.empty_like(xc, memory_format=torch.contiguous_format)
+            K_.wide_rnvp_chain(xc, ent[1], z, logdet=logdet, logdet_mode=K_.MODE_ACC, inverse=inverse)
+            return z
         if self._is_rnvp(shape):
             _, hp, hidden, h = shape
             if x.shape[1] != 2 * h or (hp == h and not self._chain_layout_ok(x, 2 * h)):

@@ -79,6 +79,44 @@ def test_rnvp2048_sample(model2, hip_device):
     flush_status_checks()
 
 
+@pytest.mark.parametrize("rows", [40, 100, 200])
+def test_wide_rnvp_chain_bitwise_per_layer(rows, hip_device):
+    """Consecutive weight-stream RealNVP layers run as ONE nfk_wide_rnvp_chain
+    call (the next layer's input fragments written by the previous layer's
+    last coupling, ping-ponged rows): bitwise the per-layer calls, forward
+    (log_prob) and inverse (model.inverse), three layers (an odd count: the
+    first layer writes z), one launch counted; 200 rows = two row blocks."""
+    from normalizingflow_amd import config
+    from normalizingflow_amd import kernels as K_
+    torch.manual_seed(rows)
+    flows = [nff.RealNVP(96, hidden_dim=200) for _ in range(3)]
+    prior = torch.distributions.MultivariateNormal(torch.zeros(96), torch.eye(96))
+    model = nfm.NormalizingFlowModel(prior, flows).to(hip_device)
+    model.prior = torch.distributions.MultivariateNormal(torch.zeros(96, device=hip_device),
+                                                        torch.eye(96, device=hip_device))
+    x = torch.randn(rows, 96, generator=torch.Generator().manual_seed(7)).to(hip_device)
+    with torch.no_grad():
+        K_.TIMER = K_.KernelTimer()
+        try:
+            lp = model.log_prob(x)
+            xi, ldi = model.inverse(x)
+            torch.cuda.synchronize()
+        finally:
+            summary, K_.TIMER = K_.TIMER.summary(), None
+        assert summary["nfk_wide_rnvp_chain"][0] == 2, summary  # (launches, ...): one per direction
+        prev = config.USE_CHAIN
+        config.USE_CHAIN = False
+        try:
+            lp1 = model.log_prob(x)
+            xi1, ldi1 = model.inverse(x)
+        finally:
+            config.USE_CHAIN = prev
+    torch.cuda.synchronize()
+    assert torch.equal(lp, lp1)
+    assert torch.equal(xi, xi1) and torch.equal(ldi, ldi1)
+    flush_status_checks()
+
+
 def _lib_path(fn):
     """fn() with the weight-stream path off (library GEMMs + nfk_affine_coupling)."""
     from normalizingflow_amd import config
