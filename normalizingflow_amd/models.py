@@ -164,6 +164,19 @@ class NormalizingFlowModel(nn.Module):
         self._lp_plan_cache = None
         self.register_load_state_dict_post_hook(_invalidate_after_load)
 
+    def __getstate__(self):
+        """Copies and pickles carry no derived state: the chained-launch
+        arguments (device pointer tables, and the weight-stream chain's ctypes
+        pointer arrays, which neither copy nor pickle) and the log_prob plan are
+        rebuilt on the copy's first call, like the layers' packs
+        (flows._HipFlow.__getstate__)."""
+        state = super().__getstate__()
+        state["_chain_cache"] = {}
+        state["_lp_plan_cache"] = None
+        state["_prior_key"] = None
+        state["_prior_iso"] = None
+        return state
+
     def invalidate_caches(self):
         """Drop every cached derivative of the parameters and the prior: the
         layers' fused weight packs, the chained-launch arguments and the

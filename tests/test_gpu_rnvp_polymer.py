@@ -114,6 +114,11 @@ def test_wide_rnvp_chain_bitwise_per_layer(rows, hip_device):
     torch.cuda.synchronize()
     assert torch.equal(lp, lp1)
     assert torch.equal(xi, xi1) and torch.equal(ldi, ldi1)
+    # a copy after the chained call (its cache holds ctypes pointer arrays)
+    import copy
+    twin = copy.deepcopy(model)
+    with torch.no_grad():
+        assert torch.equal(twin.log_prob(x), lp)
     flush_status_checks()
 
 
