@@ -402,17 +402,11 @@ __device__ void sq_finish(const SqArgs& a, const SqCond& wt, int i, int nch, int
         const float bias1 = sq_glb(wt.b1)[o1], bias2 = sq_glb(wt.b2)[o2 < H ? o2 : 0];
         const float bias3 = sq_glb(wt.b3)[o2 < P ? o2 : 0];
         if (tid >= H && tid < 128) h1[tid] = h2[tid] = 0.0f;
-        // (the weights past a row's end or past the last output: zero)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const bool kin = 64 * j + 4 * l + e < H;
-#pragma unroll
-                for (int p = 0; p < NP2; ++p) w2r[p][j][e] = kin && g + 16 * p < H ? w2r[p][j][e] : 0.0f;
-#pragma unroll
-                for (int p = 0; p < NP3; ++p) w3r[p][j][e] = kin && g + 16 * p < P ? w3r[p][j][e] : 0.0f;
-            }
+        // (no masks: past a row's end the clamped loads re-read the same row's
+        // first weights, finite wherever the row's own output is, and meet
+        // h1 / h2's zero padding -- fma(0, w, t) = t exactly; the rows past
+        // the last output are computed and dropped.  Masking the weights had
+        // cost 112 selects per lane on the critical path.)
         if (m == 0) sq_stamp(a, i, 1);
         // layer 1: the chunk sums in chunk order within each lane's half
         float s = 0.0f;
