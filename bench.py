@@ -731,7 +731,9 @@ def main():
         first."""
         if args.graph != "auto":
             return args.graph == "on"
-        return args.workload == "c1" or (B <= (1 << 17) and args.workload != "poly2048")
+        # c3 at the metric's 2^20 rows too: its one launch per step replays
+        # 0.2-0.5 % faster than the eager call (profiles/r6/r6ai_c3_graph_ab.txt)
+        return args.workload in ("c1", "c3") or (B <= (1 << 17) and args.workload != "poly2048")
 
     def run(mode):
         """One mode's timed loop: W warm-up steps, then K steps bracketed by a
