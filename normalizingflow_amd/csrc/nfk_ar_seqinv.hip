@@ -35,6 +35,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/nfk.h"
 #include "nfk_spline.h"
@@ -535,6 +536,15 @@ int sq_chunks(int dim) { return (int)((2LL * (dim - 1) + kSqFC - 1) / kSqFC); }
 
 unsigned long long* g_sq_tdbg = nullptr;
 
+// NFK_SQ_PREFETCH=0 drops the prefetch workgroups (A/B)
+bool sq_prefetch_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("NFK_SQ_PREFETCH");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return on;
+}
+
 }  // namespace
 
 // diagnostic: a device buffer of dim * 12 uint64 for the phase clocks of the
@@ -616,7 +626,7 @@ extern "C" int nfk_ar_seqinv(const float* z, int64_t ldz, const float* const* we
         for (int i = 0; i < dim; ++i) {
             const int nch = (2 * i + kSqFC - 1) / kSqFC;
             const int nxt = i + 1 < dim ? (2 * (i + 1) + kSqFC - 1) / kSqFC : 0;
-            const int pre = i + 1 < dim ? 8 : 0;  // (one prefetch workgroup per XCD)
+            const int pre = i + 1 < dim && sq_prefetch_on() ? 8 : 0;  // (one prefetch workgroup per XCD)
             const SqCond cur = cond(i), next = cond(i + 1);
             const size_t lds = sq_lds(nch, hidden, K);
 #define NFK_SQ_STEP(k) \
